@@ -1,0 +1,337 @@
+#!/usr/bin/env python
+"""Benchmark: graph-edges/sec through the WSWGAT stack fwd+bwd (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    torchrun --nproc-per-node N bench.py --gpus N ...       (driver launches N>1)
+
+One step = forward + backward of the HSG GAT stack W2S + n_iter x (S2W, W2S)
+(HiGraph.py:99-106, n_iter=2), all heads, FFNs included, in training mode
+(reference dropout 0.1), on one synthetic CNN/DM-shaped batch per GPU (config 2:
+32 docs x N=35 sentences, W=600 words, k=36 words/sentence = 159,040 graph
+edges incl. the s<->s phantom edges).  With N>1 each rank owns its own 32-doc
+shard (weak scaling) and the step ends with the data-parallel gradient
+all-reduce over RCCL (the path's one exchange step).  Encoders,
+graph construction and H2D copies are outside the step.  The step
+is captured once into a HIP graph and replayed.
+
+value = E_total x world_size / t_step (max over ranks of the timed region / K).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--n-iter", type=int, default=2)
+    ap.add_argument("--dropout", type=float, default=0.1)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-docs", type=int, default=4, help="docs in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def make_shard(config, rank, seed):
+    from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import synth
+    docs = synth.make_batch_docs(config, seed=seed * 1000 + rank)
+    G = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
+    return docs, G
+
+
+class Stack(torch.nn.Module):
+    """The timed unit: W2S + n_iter x (S2W, W2S) with the reference's shapes."""
+
+    def __init__(self, drop, n_iter):
+        super().__init__()
+        from hetersumgraph_amd.module.GAT import WSWGAT
+        self.word2sent = WSWGAT(300, 64, 8, drop, 512, drop, 50, "W2S")
+        self.sent2word = WSWGAT(64, 300, 6, drop, 512, drop, 50, "S2W")
+        self._TFembed = torch.nn.Embedding(10, 50)
+        self.n_iter = n_iter
+
+    def forward(self, G, Xw, Xs):
+        from hetersumgraph_amd.HiGraph import register_tfidf_table
+        register_tfidf_table(G, self._TFembed.weight)
+        w, s = Xw, self.word2sent(G, Xw, Xs)
+        for _ in range(self.n_iter):
+            w = self.sent2word(G, w, s)
+            s = self.word2sent(G, w, s)
+        return s
+
+
+def algorithmic_bytes_fwd(rel, H, D):
+    """Compulsory HBM bytes of one hsg_gat_fwd launch: read Z, sigma
+    (n_src rows), CSR + box (int32 + uint8 per edge), phantom, origin; write h, out,
+    m, l."""
+    HD = H * D
+    return (4 * rel.n_src * (HD + H) + 4 * (rel.n_dst + 1) + 5 * rel.n_typed + 4 * rel.n_dst
+            + 3 * 4 * rel.n_dst * HD + 8 * rel.n_dst * H)
+
+
+def time_fwd_kernel(G, stack, Xw, Xs, reps):
+    """Average duration of the dominant edge kernel (S2W hsg_gat_fwd), HIP events
+    recorded on the stream the kernel is launched on."""
+    import ctypes
+    from hetersumgraph_amd import _lib
+    from hetersumgraph_amd.module.GATLayer import edge_tau, head_tensors
+    lib = _lib.load()
+    rel = G.relation("S2W")
+    heads = list(stack.sent2word.layer.heads)
+    H, D = len(heads), heads[0].fc.out_features
+    with torch.no_grad():
+        W, a1, a3, wf, bf = head_tensors(heads)
+        Z = torch.nn.functional.linear(Xs, W).contiguous()
+        tau, mode = edge_tau(G, rel, a3, wf, bf)
+        sigma = Z.new_empty(rel.n_src, H)
+        h = Xw.new_empty(rel.n_dst, H * D)
+        out = torch.empty_like(h)
+        m = Z.new_empty(rel.n_dst, H)
+        l = Z.new_empty(rel.n_dst, H)
+        st = torch.cuda.current_stream()
+        relp = ctypes.byref(rel.cstruct())
+        _lib.check(lib.hsg_attn_src_logits(rel.n_src, H, D, Z.data_ptr(), a1.contiguous().data_ptr(),
+                                           sigma.data_ptr(), st.cuda_stream), "sigma")
+        args = (relp, H, D, mode, 0.01, Z.data_ptr(), sigma.data_ptr(), tau.contiguous().data_ptr(),
+                Xw.data_ptr(), h.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(), st.cuda_stream)
+        for _ in range(5):
+            _lib.check(lib.hsg_gat_fwd(*args), "fwd")
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        torch.cuda.synchronize()
+        for e0, e1 in evs:
+            e0.record(st)
+            lib.hsg_gat_fwd(*args)
+            e1.record(st)
+        torch.cuda.synchronize()
+        ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    return float(np.mean(ms)), float(np.median(ms)), algorithmic_bytes_fwd(rel, H, D)
+
+
+def cpu_baseline(docs_all, args, stack):
+    """The DGL-UDF-structured CPU port (oracle/dgl_udf.py) on a bounded sample of
+    the same workload, on this host's cores."""
+    from oracle import dgl_udf, fused
+    cores = len(os.sched_getaffinity(0))
+    threads = min(cores, 16)
+    torch.set_num_threads(threads)
+    docs = docs_all[: args.cpu_docs]
+    offs = np.cumsum([0] + [d.n_nodes for d in docs])
+    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
+    g = dgl_udf.UdfGraph(cat(lambda d, o: d.src + o), cat(lambda d, o: d.dst + o), cat(lambda d, o: d.unit),
+                         cat(lambda d, o: d.tffrac), cat(lambda d, o: d.edtype))
+    n_w, n_s = int((g.unit == 0).sum()), int((g.unit == 1).sum())
+    rng = np.random.default_rng(5)
+    Xw = torch.from_numpy((0.4 * rng.standard_normal((n_w, 300))).astype(np.float32))
+    Xs = torch.from_numpy(rng.standard_normal((n_s, 64)).astype(np.float32))
+    p1 = fused.as_params({k: v.cpu() for k, v in stack.word2sent.state_dict().items()}, torch.float32)
+    p2 = fused.as_params({k: v.cpu() for k, v in stack.sent2word.state_dict().items()}, torch.float32)
+    T = stack._TFembed.weight.detach().cpu().clone().requires_grad_()
+    E = len(g.src)
+
+    def step():
+        Xs_ = Xs.clone().requires_grad_()
+        s = dgl_udf.stack_step(g, Xw, Xs_, p1, p2, T, n_iter=args.n_iter, drop=args.dropout, training=True)
+        s.sum().backward()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = (time.perf_counter() - t0) / args.cpu_steps
+    return {"value": E / dt, "unit": "graph-edges/s", "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_docs} of the {len(docs_all)} {args.config} docs ({E} edges), "
+                      f"{args.cpu_steps} fwd+bwd steps of the same stack, fp32, torch CPU, "
+                      f"{cpu_model()}; oracle/dgl_udf.py (DGL-0.4 UDF structure)",
+            "ms_per_step": dt * 1e3}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from hetersumgraph_amd import _lib
+    _lib.load()
+
+    docs, G = make_shard(args.config, rank, args.seed)
+    E_total = G.number_of_edges()
+    G.to(dev)
+    torch.manual_seed(args.seed)                       # identical replicas on every rank
+    stack = Stack(args.dropout, args.n_iter).to(dev).train()
+    rel_w, rel_s = G.relation("W2S"), G.relation("S2W")
+    gen = torch.Generator(device=dev).manual_seed(args.seed * 7 + rank)
+    Xw = 0.4 * torch.randn(rel_s.n_dst, 300, device=dev, generator=gen)      # word embeddings (frozen)
+    Xs = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen).requires_grad_()   # encoder output
+    R = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen)
+    params = [p for p in stack.parameters() if p.requires_grad]
+    flat = None
+    if world > 1:
+        import torch.distributed as dist
+        flat = torch.zeros(sum(p.numel() for p in params), device=dev)
+
+    def step():
+        s = stack(G, Xw, Xs)
+        (s * R).sum().backward()
+
+    def allreduce():
+        import torch.distributed as dist
+        torch._utils._flatten_dense_tensors  # noqa: B018
+        off = 0
+        for p in params:
+            n = p.numel()
+            flat[off:off + n].copy_(p.grad.view(-1))
+            off += n
+        dist.all_reduce(flat)
+        flat.div_(world)
+        off = 0
+        for p in params:
+            n = p.numel()
+            p.grad.view(-1).copy_(flat[off:off + n])
+            off += n
+
+    def zero():
+        for p in params:
+            if p.grad is not None:
+                p.grad.zero_()
+        if Xs.grad is not None:
+            Xs.grad.zero_()
+
+    # eager warm-up (builds relation caches, allocator pools)
+    for _ in range(max(args.warmup, 2)):
+        zero()
+        step()
+        if world > 1:
+            allreduce()
+    torch.cuda.synchronize()
+
+    use_graph = not args.no_graph
+    graph = None
+    if use_graph:
+        try:
+            s_side = torch.cuda.Stream(dev)
+            s_side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s_side):
+                for _ in range(2):
+                    zero()
+                    step()
+            torch.cuda.current_stream(dev).wait_stream(s_side)
+            zero()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            torch.cuda.synchronize()
+        except Exception as exc:  # pragma: no cover - reported in the JSON
+            print(f"hip graph capture failed, running eager: {exc!r}", file=sys.stderr)
+            graph = None
+            use_graph = False
+
+    def run_one():
+        if graph is not None:
+            zero()
+            graph.replay()
+        else:
+            zero()
+            step()
+        if world > 1:
+            allreduce()
+
+    for _ in range(args.warmup):
+        run_one()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / args.steps * 1e3
+    value = E_total * world / (dt / args.steps)
+
+    # dominant edge kernel: average launch duration with HIP events on its stream
+    k_ms_mean, k_ms_med, k_bytes = time_fwd_kernel(G, stack, Xw.detach(), Xs.detach(), args.kernel_reps)
+    achieved = k_bytes / (k_ms_mean * 1e-3) / 1e9
+
+    out = {
+        "metric": "graph-edges/sec through WSWGAT fwd+bwd, CNN/DM-shaped batch; 1/2/4/8 GPU",
+        "value": value,
+        "unit": "graph-edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded CNN/DM-shaped graphs, random-init weights of the reference architecture)",
+        "config": {"workload": f"{args.config}: HSG WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) fwd+bwd, "
+                               "train mode, 32 docs/GPU x (N=35, W=600, k=36)",
+                   "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
+                   "typed_edges_per_direction": rel_w.n_typed,
+                   "dropout": args.dropout, "parallelism": f"dp{world}",
+                   "hip_graph": bool(use_graph)},
+        "roofline": {"kernel": "hsg_gat_fwd (S2W: sentence->word, H=6 x D=50)", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": k_bytes, "avg_launch_us": k_ms_mean * 1e3,
+                     "median_launch_us": k_ms_med * 1e3},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(docs, args, stack)
+        except Exception as exc:  # pragma: no cover
+            out["cpu_baseline"] = {"error": repr(exc)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

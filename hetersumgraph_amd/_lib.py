@@ -1,0 +1,86 @@
+"""ctypes binding of libhsg.so (the C ABI declared in include/hsg.h).
+
+The library is built in-tree (``python -m hetersumgraph_amd.build`` or
+``__graft_entry__.build()``).  There is deliberately no fallback: if the shared
+object is missing or a call fails, a ``RuntimeError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhsg.so")
+
+HSG_EINVAL = 1001
+HSG_TAU_TABLE = 0
+HSG_TAU_PER_EDGE = 1
+
+# every symbol include/hsg.h declares (checked by tests/test_abi.py)
+EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
+           "hsg_attn_src_logits", "hsg_version")
+
+
+class HsgRel(ctypes.Structure):
+    """Mirror of ``struct hsg_rel`` (include/hsg.h)."""
+
+    _fields_ = [("n_src", ctypes.c_int32), ("n_dst", ctypes.c_int32), ("n_edges", ctypes.c_int32),
+                ("indptr", ctypes.c_void_p), ("src", ctypes.c_void_p), ("tf", ctypes.c_void_p),
+                ("phantom", ctypes.c_void_p), ("cindptr", ctypes.c_void_p),
+                ("cdst", ctypes.c_void_p), ("cperm", ctypes.c_void_p)]
+
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_RELP = ctypes.POINTER(HsgRel)
+
+_SIGS = {
+    "hsg_gat_fwd": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_dst": [_RELP, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_blocks": [_RELP],
+    "hsg_gat_bwd_src": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
+    "hsg_version": [],
+}
+
+
+def load():
+    """Load libhsg.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libhsg.so not found at {LIB_PATH}: build it with `python -m hetersumgraph_amd.build` "
+            "(hetersumgraph_amd has no CPU fallback for the WSWGAT hot path)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name == "hsg_version" else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        kind = "unsupported shape" if rc == HSG_EINVAL else f"hipError {rc}"
+        raise RuntimeError(f"{what} failed: {kind}")
+
+
+def version() -> str:
+    return load().hsg_version().decode()

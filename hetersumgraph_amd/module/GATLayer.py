@@ -1,0 +1,145 @@
+"""Per-head GAT layers and the position-wise FFN (reference: module/GATLayer.py).
+
+Parameter names and shapes match the reference exactly (state_dict compatible,
+SURVEY Appendix B), but the computation is not per head: ``MultiHeadLayer``
+concatenates every head's weights and runs all heads in one fused HIP pass
+(:func:`hetersumgraph_amd.ops.gat_aggregate`).  A single head's ``forward(g, h)``
+is still available and is the same kernel with H = 1.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import LEAKY_SLOPE, gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
+from ..relation import N_BOX, ZERO_ROW
+
+# The reference asserts "no NaN" around every FFN (GATLayer.py:36, 43), a host sync
+# per call.  Same error behaviour behind a switch (default off: it would serialise
+# the stream and break HIP-graph capture).
+CHECK_NAN = os.environ.get("HSG_CHECK_NAN", "0") == "1"
+
+TFIDF_TAG = "tffrac@dtype0"
+
+
+class PositionwiseFeedForward(nn.Module):
+    """LN(x + Dropout(W2 relu(W1 x + b1) + b2)), eps 1e-5 (GATLayer.py:25-44).
+
+    Kept as two k=1 ``Conv1d`` modules for state_dict compatibility; executed as
+    row-major GEMMs on [n, d]."""
+
+    def __init__(self, d_in, d_hid, dropout=0.1):
+        super().__init__()
+        self.w_1 = nn.Conv1d(d_in, d_hid, 1)
+        self.w_2 = nn.Conv1d(d_hid, d_in, 1)
+        self.layer_norm = nn.LayerNorm(d_in)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])            # reference feeds [1, n, d] (GAT.py:58)
+        if CHECK_NAN:
+            assert not torch.any(torch.isnan(x2)), "FFN input"
+        hid = F.relu(F.linear(x2, self.w_1.weight.squeeze(-1), self.w_1.bias))
+        y = F.linear(hid, self.w_2.weight.squeeze(-1), self.w_2.bias)
+        y = self.dropout(y)
+        y = self.layer_norm(y + x2)
+        if CHECK_NAN:
+            assert not torch.any(torch.isnan(y)), "FFN output"
+        return y.reshape(shape)
+
+
+class _HeadParams(nn.Module):
+    """fc / feat_fc / attn_fc of one head (GATLayer.py:82-87, 121-126)."""
+
+    kind = None
+    feat_bias = False
+
+    def __init__(self, in_dim, out_dim, feat_embed_size):
+        super().__init__()
+        self.fc = nn.Linear(in_dim, out_dim, bias=False)
+        self.feat_fc = nn.Linear(feat_embed_size, out_dim, bias=self.feat_bias)
+        self.attn_fc = nn.Linear(3 * out_dim, 1, bias=False)
+
+    def forward(self, g, h):
+        """One head on its own (reference signature): returns [n_dst, out_dim]."""
+        return fused_heads(g, h, [self], self.kind, origin=None, dropout=None)
+
+
+class WSGATLayer(_HeadParams):
+    """Word -> sentence head (GATLayer.py:81-116): feat_fc has no bias."""
+
+    kind = "W2S"
+    feat_bias = False
+
+
+class SWGATLayer(_HeadParams):
+    """Sentence -> word head (GATLayer.py:120-152): feat_fc has a bias."""
+
+    kind = "S2W"
+    feat_bias = True
+
+
+def head_tensors(heads):
+    """Concatenate per-head parameters (autograd-tracked) for the fused pass."""
+    D = heads[0].fc.out_features
+    W = torch.cat([hd.fc.weight for hd in heads], 0)                     # [H*D, in]
+    attn = torch.cat([hd.attn_fc.weight for hd in heads], 0)             # [H, 3D]
+    a1 = attn[:, :D]                                                     # z_src weights
+    a3 = attn[:, 2 * D:]                                                 # feat weights
+    wf = torch.stack([hd.feat_fc.weight for hd in heads], 0)             # [H, D, F]
+    bf = (torch.stack([hd.feat_fc.bias for hd in heads], 0)
+          if heads[0].feat_fc.bias is not None else None)                # [H, D]
+    return W, a1, a3, wf, bf
+
+
+def edge_tau(g, rel, a3, wf, bf):
+    """tau = a3 . feat_fc(tfidfembed) per (tf-idf box | edge) and head.
+
+    Fast path: ``tfidfembed`` was written by HSumGraph.set_wnfeature as a table
+    column (``_TFembed.weight`` rows selected by ``tffrac`` on dtype-0 edges,
+    HiGraph.py:146-151) -> an [11, H] table (row 10 = never-written edges).
+    Generic path: a dense per-edge ``tfidfembed`` from a foreign caller ->
+    [E_T, H] in CSR order."""
+    from ..graph import TableColumn
+
+    col = g._eframe().cols.get("tfidfembed")
+    if col is None:
+        raise KeyError("tfidfembed")   # edges.data['tfidfembed'] in the reference UDF
+    v = torch.einsum("kd,kdf->kf", a3, wf)                               # [H, F]
+    c = (a3 * bf).sum(-1) if bf is not None else None                    # [H]
+    if isinstance(col, TableColumn) and col.tag == TFIDF_TAG and col.weight.shape[0] == N_BOX:
+        tau = F.pad(col.weight @ v.t(), (0, 0, 0, 1))                    # [11, H], row 10 = 0
+        if c is not None:
+            tau = tau + c
+        return tau, HSG_TAU_TABLE
+    dense = col.materialize() if isinstance(col, TableColumn) else col
+    eid = rel.dev["eid"]
+    tau = dense[eid].to(v.dtype) @ v.t()
+    if c is not None:
+        tau = tau + c
+    return tau, HSG_TAU_PER_EDGE
+
+
+def fused_heads(g, h, heads, kind, origin=None, dropout=None):
+    """All heads of one layer application in one pass (+ ELU/residual if origin).
+
+    ``dropout``: the MultiHeadLayer's nn.Dropout, applied to ``h`` with an
+    independent mask per head in training mode (GATStackLayer.py:56)."""
+    rel = g.relation(kind)
+    H = len(heads)
+    D = heads[0].fc.out_features
+    W, a1, a3, wf, bf = head_tensors(heads)
+    if h.shape[0] != rel.n_src:
+        raise ValueError(f"{kind}: input has {h.shape[0]} rows, graph has {rel.n_src} source nodes")
+    if dropout is not None and dropout.training and dropout.p > 0:
+        hx = F.dropout(h.unsqueeze(0).expand(H, *h.shape).contiguous(), dropout.p, True)
+        Z = torch.bmm(hx, W.view(H, D, -1).transpose(1, 2))              # [H, n, D]
+        Z = Z.transpose(0, 1).reshape(h.shape[0], H * D)
+    else:
+        Z = F.linear(h, W)
+    tau, mode = edge_tau(g, rel, a3, wf, bf)
+    return gat_aggregate(Z, a1, tau, origin, rel, H, D, LEAKY_SLOPE, mode)

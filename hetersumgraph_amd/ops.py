@@ -1,0 +1,103 @@
+"""Autograd operators over the C ABI (libhsg.so) -- the WSWGAT hot path.
+
+``gat_aggregate`` is one multi-head WSGAT/SWGAT application with the ELU +
+residual epilogue, i.e. module/GATLayer.py:104-116 (or 142-152) for every head of
+module/GATStackLayer.py:55-59 followed by module/GAT.py:56-57, expressed as the
+fused restatement of SURVEY §8a:
+
+    sigma[u,k] = <Z[u,k,:], a1_k>                        (z_src part of attn_fc)
+    s_e,k      = leaky_relu(sigma[u,k] + tau[t_e,k])     (z_dst part is 0, GATLayer.py:111)
+    alpha      = softmax over ALL in-edges of v (phantoms: e = 0, z = 0)
+    out[v]     = elu(sum_e alpha z_u) + origin[v]
+
+Everything runs on the current HIP stream; nothing synchronises, so a whole
+training step can be captured into a HIP graph.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import HSG_TAU_PER_EDGE, HSG_TAU_TABLE, check, load, ptr, stream_of
+from .relation import N_BOX
+
+LEAKY_SLOPE = 0.01   # F.leaky_relu default (GATLayer.py:92, 131)
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "hetersumgraph_amd WSWGAT runs only on a ROCm device (libhsg.so HIP kernels); "
+                f"got a tensor on {t.device}. There is no CPU fallback.")
+        if t.dtype != torch.float32:
+            raise TypeError(f"hetersumgraph_amd WSWGAT computes in fp32; got {t.dtype}")
+
+
+class _GatAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Z, a1, tau, origin, rel, H, D, slope, tau_mode):
+        lib = load()
+        Z = Z.contiguous()
+        a1 = a1.contiguous()
+        tau = tau.contiguous()
+        origin = None if origin is None else origin.contiguous()
+        n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
+        if Z.shape != (n_src, HD):
+            raise ValueError(f"Z has shape {tuple(Z.shape)}, relation expects ({n_src}, {HD})")
+        if origin is not None and origin.shape != (n_dst, HD):
+            raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
+        st = stream_of(Z)
+        relp = ctypes.byref(rel.cstruct())
+        sigma = Z.new_empty(n_src, H)
+        check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st),
+              "hsg_attn_src_logits")
+        h = Z.new_empty(n_dst, HD)
+        out = Z.new_empty(n_dst, HD) if origin is not None else None
+        m = Z.new_empty(n_dst, H)
+        l = Z.new_empty(n_dst, H)
+        check(lib.hsg_gat_fwd(relp, H, D, tau_mode, slope, ptr(Z), ptr(sigma), ptr(tau),
+                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+        ctx.save_for_backward(Z, a1, sigma, tau, h, m, l)
+        ctx.rel, ctx.H, ctx.D, ctx.slope, ctx.tau_mode = rel, H, D, slope, tau_mode
+        ctx.has_origin = origin is not None
+        return out if origin is not None else h
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = load()
+        Z, a1, sigma, tau, h, m, l = ctx.saved_tensors
+        rel, H, D, slope, mode = ctx.rel, ctx.H, ctx.D, ctx.slope, ctx.tau_mode
+        dout = dout.contiguous()
+        st = stream_of(Z)
+        relp = ctypes.byref(rel.cstruct())
+        G = torch.empty_like(h)
+        dpre = Z.new_empty(rel.n_typed, H)
+        nb = lib.hsg_gat_bwd_blocks(relp)
+        dtp = Z.new_empty(nb, N_BOX + 1, H) if mode == HSG_TAU_TABLE else None
+        check(lib.hsg_gat_bwd_dst(relp, H, D, mode, int(ctx.has_origin), slope, ptr(Z), ptr(sigma),
+                                  ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                  ptr(dtp), st), "hsg_gat_bwd_dst")
+        dZ = torch.empty_like(Z)
+        dsig = torch.empty_like(sigma)
+        check(lib.hsg_gat_bwd_src(relp, H, D, mode, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                                  ptr(G), ptr(dpre), ptr(a1), ptr(dZ), ptr(dsig), st),
+              "hsg_gat_bwd_src")
+        da1 = None
+        if ctx.needs_input_grad[1]:
+            da1 = torch.einsum("uk,ukd->kd", dsig, Z.view(-1, H, D))
+        dtau = dtp.sum(0) if mode == HSG_TAU_TABLE else dpre
+        return dZ, da1, dtau, (dout if ctx.has_origin else None), None, None, None, None, None
+
+
+def gat_aggregate(Z, a1, tau, origin, rel, H, D, slope=LEAKY_SLOPE, tau_mode=HSG_TAU_TABLE):
+    """Fused multi-head edge-softmax aggregation (+ ELU + residual when ``origin``).
+
+    Z [n_src, H*D], a1 [H, D], tau [11, H] (table) or [E_T, H] (per edge, CSR
+    order), origin [n_dst, H*D] or None.  Returns [n_dst, H*D]."""
+    _require_device(Z, a1, tau, origin)
+    return _GatAggregate.apply(Z, a1, tau, origin, rel, H, D, float(slope), int(tau_mode))

@@ -1,0 +1,101 @@
+/*
+ * hsg.h -- C ABI of the MI355X-native WSWGAT hot path (libhsg.so, gfx950).
+ *
+ * The reference (yellow-binary-tree/HeterSumGraph) has no FFI: its hot path is the
+ * Python operator WSWGAT(...).forward(g, w, s) (module/GAT.py:31-59) built from DGL
+ * UDFs (module/GATLayer.py:81-152) and a per-head Python loop
+ * (module/GATStackLayer.py:55-63).  Each entry point below replaces one piece of
+ * that call chain; the Python host layer (hetersumgraph_amd/module/) binds them
+ * with ctypes exactly as shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - All pointers are device pointers (hipMalloc'd or torch-allocated).  The
+ *     library never allocates, frees or synchronises; work is enqueued on `stream`
+ *     (a hipStream_t passed as void*), so every call is graph-capturable.
+ *   - Row-major fp32 features.  Z is [n_src, H*D], head k occupies columns
+ *     [k*D, (k+1)*D) (the torch.cat order of GATStackLayer.py:59).
+ *   - Return value: 0 on success, otherwise a hipError_t (launch error) or
+ *     HSG_EINVAL for unsupported shapes.  No global mutable state; reentrant
+ *     across streams and devices.
+ */
+#ifndef HSG_H_
+#define HSG_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HSG_EINVAL 1001
+
+/* One typed relation (W2S: word->sentence/doc, S2W: sentence/doc->word).
+ * Replaces, per layer call, DGL's filter_nodes/filter_edges
+ * (GATLayer.py:105-107, 143-145) and the in-edge set of g.pull (113, 149). */
+typedef struct hsg_rel {
+    int32_t n_src;            /* |source set|      (rows of Z, sigma)               */
+    int32_t n_dst;            /* |destination set| (rows of the output)             */
+    int32_t n_edges;          /* |typed edges| E_T                                  */
+    const int32_t *indptr;    /* [n_dst+1] CSR by destination rank                  */
+    const int32_t *src;       /* [E_T]     source rank per CSR edge                 */
+    const uint8_t *tf;        /* [E_T]     tau row per CSR edge (tf-idf box, 10=0)  */
+    const int32_t *phantom;   /* [n_dst]   untyped in-edges (e=0, z=0) per dst      */
+    const int32_t *cindptr;   /* [n_src+1] CSC by source rank                       */
+    const int32_t *cdst;      /* [E_T]     destination rank per CSC edge            */
+    const int32_t *cperm;     /* [E_T]     CSR position of each CSC edge            */
+} hsg_rel;
+
+/* tau addressing: HSG_TAU_TABLE -> tau is [11, H] indexed by rel->tf (tf-idf box
+ * table, HiGraph.py:52 + zero row); HSG_TAU_PER_EDGE -> tau is [E_T, H] in CSR order
+ * (a foreign caller wrote a dense edata['tfidfembed']). */
+#define HSG_TAU_TABLE 0
+#define HSG_TAU_PER_EDGE 1
+
+/* Forward of one multi-head WSGAT/SWGAT application, all heads fused.
+ * Replaces GATLayer.py:89-93 (edge_attention, apply_edges), 95-102
+ * (message_func/reduce_func under g.pull with degree bucketing), the head loop and
+ * concat of GATStackLayer.py:55-59 and -- when `origin` != NULL -- the ELU +
+ * residual of GAT.py:56-57:
+ *   s_e   = leaky_relu(sigma[src_e,k] + tau[t_e,k], slope)
+ *   m_v   = max(max_e s_e, 0 if phantom_v>0),  l_v = sum_e exp(s_e-m_v) + phantom_v*exp(-m_v)
+ *   h[v]  = sum_e exp(s_e-m_v)/l_v * Z[src_e, k, :]      (0 if v has no in-edges)
+ *   out   = origin ? elu(h) + origin : h
+ * Saved for backward: h, m, l ([n_dst, H] each). */
+int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
+                const float *Z, const float *sigma, const float *tau, const float *origin,
+                float *h, float *out, float *m, float *l, void *stream);
+
+/* Backward, destination-centric half: given dOut, computes
+ *   G = origin_mode ? dOut * elu'(h) : dOut                      [n_dst, H*D]
+ *   dpre[e,k] = alpha_ek (G_v.Z_u - G_v.h_v) * leaky'(pre_ek)   [E_T, H], CSR order
+ *   dtau_part[b, t, k] = per-block partial sums of dpre by tau row (table mode)
+ * dtau_part must hold hsg_gat_bwd_blocks(rel) * 11 * H floats. */
+int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_mode, float slope,
+                    const float *Z, const float *sigma, const float *tau,
+                    const float *h, const float *m, const float *l, const float *dout,
+                    float *G, float *dpre, float *dtau_part, void *stream);
+
+/* Number of partial rows hsg_gat_bwd_dst writes into dtau_part. */
+int hsg_gat_bwd_blocks(const hsg_rel *rel);
+
+/* Backward, source-centric half (CSC): for every source u
+ *   dZ[u, k, :]  = sum_{e: src_e = u} alpha_ek * G[dst_e, k, :]  (+ dsigma[u,k]*a1[k,:] if a1)
+ *   dsigma[u, k] = sum_{e: src_e = u} dpre[e, k]
+ * a1 (optional, [H, D]) folds the gradient of sigma = <Z[u,k,:], a1[k,:]> into dZ. */
+int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
+                    const float *sigma, const float *tau, const float *m, const float *l,
+                    const float *G, const float *dpre, const float *a1,
+                    float *dZ, float *dsigma, void *stream);
+
+/* sigma[u, k] = <Z[u, k, :], a1[k, :]> -- the z_src part of attn_fc
+ * (GATLayer.py:91-92 / 130-131); a1 = attn_fc.weight[0, :D] per head. */
+int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,
+                        void *stream);
+
+/* Library build identification (ABI version, gfx target). */
+const char *hsg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HSG_H_ */

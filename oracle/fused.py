@@ -1,0 +1,118 @@
+"""CPU ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, ``__graft_entry__.smoke()`` and bench.py's cpu_baseline
+leg, as the *checker*; never by the product path (hetersumgraph_amd/).
+
+A float64 PyTorch-CPU restatement of one WSWGAT application, written edge-wise
+like the reference (no tau-table shortcut, no fused kernels), so it checks both
+the HIP kernels and the algebra they rely on.  Pinned against the golden vectors
+that the reference's own module code produced (tests/golden/, see
+tests/test_oracle_golden.py).
+
+Reference lines restated:
+  typed_relation  -- GATLayer.py:105-107 / 143-145 (filters) + DGL 0.4 pull's
+                     in-edge set (113 / 149) incl. untyped "phantom" in-edges
+  wswgat_layer    -- GAT.py:45-59, GATStackLayer.py:55-59, GATLayer.py:89-102,
+                     110-116, 128-152, and PositionwiseFeedForward 35-44
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+SLOPE = 0.01
+
+
+def typed_relation(kind, src, dst, unit, tffrac, edtype):
+    """Typed edges and phantom counts of one layer type (numpy, edge-id order)."""
+    su, du = (0.0, 1.0) if kind == "W2S" else (1.0, 0.0)
+    unit = np.asarray(unit)
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    is_s, is_d = unit == su, unit == du
+    s_nodes, d_nodes = np.nonzero(is_s)[0], np.nonzero(is_d)[0]
+    s_rank = np.full(len(unit), -1)
+    s_rank[s_nodes] = np.arange(len(s_nodes))
+    d_rank = np.full(len(unit), -1)
+    d_rank[d_nodes] = np.arange(len(d_nodes))
+    typed = np.nonzero(is_s[src] & is_d[dst])[0]
+    indeg = np.bincount(dst, minlength=len(unit))[d_nodes]
+    n_typed_in = np.bincount(d_rank[dst[typed]], minlength=len(d_nodes))
+    has_tf = np.asarray(edtype)[typed] == 0        # tfidfembed written on dtype-0 edges only
+    return dict(e_src=s_rank[src[typed]], e_dst=d_rank[dst[typed]],
+                tf=np.where(has_tf, np.asarray(tffrac)[typed], -1),
+                phantom=indeg - n_typed_in, any_in=indeg > 0,
+                n_src=len(s_nodes), n_dst=len(d_nodes))
+
+
+def _heads(params, prefix, H):
+    return [dict(fc=params[f"{prefix}layer.heads.{i}.fc.weight"],
+                 feat_w=params[f"{prefix}layer.heads.{i}.feat_fc.weight"],
+                 feat_b=params.get(f"{prefix}layer.heads.{i}.feat_fc.bias"),
+                 attn=params[f"{prefix}layer.heads.{i}.attn_fc.weight"]) for i in range(H)]
+
+
+def n_heads(params, prefix=""):
+    i = 0
+    while f"{prefix}layer.heads.{i}.fc.weight" in params:
+        i += 1
+    return i
+
+
+def gat_heads(rel, X, params, T, prefix=""):
+    """Concatenated head outputs (before ELU) -- GATStackLayer.py:55-59."""
+    H = n_heads(params, prefix)
+    e_src = torch.from_numpy(rel["e_src"])
+    e_dst = torch.from_numpy(rel["e_dst"])
+    tf = torch.from_numpy(rel["tf"])
+    n_dst = rel["n_dst"]
+    phantom = torch.from_numpy(rel["phantom"]).to(X.dtype)
+    tfe = torch.where((tf >= 0).unsqueeze(1), T[tf.clamp_min(0)], torch.zeros((), dtype=X.dtype))
+    outs = []
+    for hd in _heads(params, prefix, H):
+        z = X @ hd["fc"].t()                                   # GATLayer.py:110 / 146
+        D = z.shape[1]
+        dfeat = tfe @ hd["feat_w"].t()
+        if hd["feat_b"] is not None:
+            dfeat = dfeat + hd["feat_b"]
+        zsrc = z[e_src]
+        zdst = torch.zeros_like(zsrc)                          # dst 'z' never written -> 0
+        wa = torch.cat([zsrc, zdst, dfeat], 1) @ hd["attn"].t()   # attn_fc, GATLayer.py:91-92
+        e = F.leaky_relu(wa.squeeze(1), SLOPE)
+        # softmax over ALL in-edges of each dst: typed edges + phantoms with e = 0
+        mx = torch.full((n_dst,), -torch.inf, dtype=X.dtype).scatter_reduce(0, e_dst, e, "amax")
+        mx = torch.where(phantom > 0, torch.clamp_min(mx, 0.0), mx)
+        mx = torch.where(torch.isinf(mx), torch.zeros_like(mx), mx).detach()
+        p = torch.exp(e - mx[e_dst])
+        den = torch.zeros(n_dst, dtype=X.dtype).index_add(0, e_dst, p) + phantom * torch.exp(-mx)
+        alpha = p / den[e_dst]
+        h = torch.zeros(n_dst, D, dtype=X.dtype).index_add(0, e_dst, alpha.unsqueeze(1) * zsrc)
+        outs.append(h)
+    return torch.cat(outs, 1)
+
+
+def ffn(x, params, prefix=""):
+    """PositionwiseFeedForward (GATLayer.py:35-44), eval mode."""
+    w1 = params[f"{prefix}ffn.w_1.weight"].squeeze(-1)
+    w2 = params[f"{prefix}ffn.w_2.weight"].squeeze(-1)
+    y = F.relu(x @ w1.t() + params[f"{prefix}ffn.w_1.bias"]) @ w2.t() + params[f"{prefix}ffn.w_2.bias"]
+    return F.layer_norm(y + x, (x.shape[1],), params[f"{prefix}ffn.layer_norm.weight"],
+                        params[f"{prefix}ffn.layer_norm.bias"], 1e-5)
+
+
+def wswgat_layer(kind, rel, Xw, Xs, params, T, prefix=""):
+    """WSWGAT.forward(g, w, s) (GAT.py:45-59), eval mode."""
+    origin, neighbor = (Xs, Xw) if kind == "W2S" else (Xw, Xs)
+    h = F.elu(gat_heads(rel, neighbor, params, T, prefix)) + origin
+    return ffn(h, params, prefix)
+
+
+def as_params(module_or_dict, dtype=torch.float64, requires_grad=True):
+    """name -> leaf tensor (float64) from a state_dict-like mapping."""
+    src = module_or_dict.state_dict() if hasattr(module_or_dict, "state_dict") else module_or_dict
+    out = {}
+    for k, v in src.items():
+        t = torch.as_tensor(np.asarray(v.detach().cpu() if hasattr(v, "detach") else v)).to(dtype)
+        out[k] = t.clone().requires_grad_(requires_grad)
+    return out

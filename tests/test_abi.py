@@ -1,0 +1,46 @@
+"""The C ABI: libhsg.so builds for gfx950, loads, and exports every symbol that
+include/hsg.h declares, with the struct layout the ctypes binding assumes.
+(No compute calls here -- those need a GPU and live in the -m gpu tests.)"""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "hsg.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hsg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_bound_symbols():
+    from hetersumgraph_amd import _lib
+    assert declared_functions() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    from hetersumgraph_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libhsg.so is not built (run python -m hetersumgraph_amd.build)")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert _lib.load() is not None
+    assert "gfx950" in _lib.version()
+
+
+def test_struct_layout():
+    from hetersumgraph_amd._lib import HsgRel
+    # 3 x int32 + pad to 8 + 7 pointers (x86-64 SysV)
+    assert ctypes.sizeof(HsgRel) == 16 + 7 * 8
+    assert HsgRel.indptr.offset == 16
+
+
+def test_code_object_is_gfx950():
+    from hetersumgraph_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data

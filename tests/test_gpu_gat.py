@@ -1,0 +1,212 @@
+"""GPU parity of the fused WSWGAT HIP path (libhsg.so through its C ABI).
+
+* against the reference's golden vectors (fp32 reference outputs: the 1e-4
+  contract of BASELINE.json; gradients: the fp64 reference run);
+* against the fp64 CPU oracle on seeded random graphs that exercise the edge
+  cases the reference's graphs contain (phantom-only destinations, isolated
+  words, >64-edge segments, every tf-idf box, HDSG doc nodes), other head
+  shapes, and the per-edge tfidfembed path;
+* determinism (bitwise-equal reruns) and full config-2 size.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import (build_graph, concat_arrays, gat_inputs, load_fixture, projections,
+                     seeded_gat_params, upstream)
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-4        # BASELINE.json contract (fp32 outputs vs reference CPU path)
+
+
+def max_err(a, b):
+    a = torch.as_tensor(np.asarray(a.detach().cpu() if torch.is_tensor(a) else a), dtype=torch.float64)
+    b = torch.as_tensor(np.asarray(b.detach().cpu() if torch.is_tensor(b) else b), dtype=torch.float64)
+    return (a - b).abs().max().item() if a.numel() else 0.0
+
+
+def assert_grad_close(got, ref, rtol=2e-4, max_bad_rows=0):
+    """|got - ref| <= rtol * max|ref| except in at most ``max_bad_rows`` rows
+    (fp32 vs fp64 ReLU-gate flips at near-zero pre-activations, see
+    tests/test_oracle_golden.py)."""
+    got = torch.as_tensor(np.asarray(got.detach().cpu() if torch.is_tensor(got) else got), dtype=torch.float64)
+    ref = torch.as_tensor(np.asarray(ref.detach().cpu() if torch.is_tensor(ref) else ref), dtype=torch.float64)
+    scale = max(ref.abs().max().item(), 1e-6)
+    err = (got - ref).abs()
+    if err.dim() == 1:
+        err = err.unsqueeze(1)
+    bad_rows = (err.reshape(err.shape[0], -1).max(1).values > rtol * scale).sum().item()
+    assert bad_rows <= max_bad_rows, (
+        f"{bad_rows} rows off (max err {err.max().item():.3e}, scale {scale:.3e})")
+
+
+def run_gat(z, seed, dense_tfidf=False, device="cuda"):
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    G = build_graph(z).to(device)
+    n_w, n_s = int(z["n_w"]), int(z["n_s"])
+    Xw, Xs, T = gat_inputs(seed, n_w, n_s)
+    Xw = Xw.to(device).requires_grad_()
+    Xs = Xs.to(device).requires_grad_()
+    T = T.to(device).requires_grad_()
+    if dense_tfidf:
+        idx = torch.where(G.edata["dtype"] == 0, G.edata["tffrac"], torch.full_like(G.edata["tffrac"], -1))
+        dense = torch.where((idx >= 0).unsqueeze(1), T[idx.clamp_min(0)], torch.zeros((), device=device))
+        G.edata["tfidfembed"] = dense
+    else:
+        register_tfidf_table(G, T)
+    w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
+    w2s, s2w = w2s.to(device), s2w.to(device)
+    o1 = w2s(G, Xw, Xs)
+    o2 = s2w(G, Xw, Xs)
+    R1, R2 = upstream(seed, o1.shape, o2.shape)
+    ((o1 * R1.to(device)).sum() + (o2 * R2.to(device)).sum()).backward()
+    torch.cuda.synchronize()
+    return dict(o1=o1, o2=o2, Xw=Xw, Xs=Xs, T=T, w2s=w2s, s2w=s2w)
+
+
+@pytest.mark.parametrize("name,seed,dense", [("gat_small", 1, False), ("gat_hdsg_small", 2, False),
+                                             ("gat_cfg1", 3, False), ("gat_small", 1, True),
+                                             ("gat_hdsg_small", 2, True)])
+def test_gat_vs_reference_golden(name, seed, dense):
+    z = load_fixture(name)
+    r = run_gat(z, seed, dense_tfidf=dense)
+    rows = z["rows_w"] if "rows_w" in z else slice(None)
+    assert max_err(r["o1"], z["out_w2s"]) <= OUT_TOL
+    assert max_err(r["o2"].detach().cpu()[rows], z["out_s2w"]) <= OUT_TOL
+    # tighter than the contract: the two fp32 paths differ only by summation order
+    assert max_err(r["o1"], z["out64_w2s"]) <= 1e-5
+    assert max_err(r["o2"].detach().cpu()[rows], z["out64_s2w"]) <= 1e-5
+    bad = 2 if name == "gat_cfg1" else 0
+    assert_grad_close(r["Xs"].grad, z["grad_Xs"], max_bad_rows=bad)
+    assert_grad_close(r["T"].grad, z["grad_T"], rtol=1e-3, max_bad_rows=bad)
+    if "grad_Xw" in z:
+        assert_grad_close(r["Xw"].grad, z["grad_Xw"], max_bad_rows=bad)
+    else:
+        assert_grad_close(r["Xw"].grad.cpu()[rows], z["grad_Xw_rows"], max_bad_rows=bad)
+    for tag, mod in (("w2s", r["w2s"]), ("s2w", r["s2w"])):
+        for k, p in mod.named_parameters():
+            key = f"grad.{tag}.{k}"
+            if key in z:
+                assert_grad_close(p.grad, z[key], rtol=1e-3, max_bad_rows=bad)
+            elif "proj." + key in z:
+                got = projections(p.grad, seed, key)
+                ref = z["proj." + key]
+                assert np.abs(got - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-4, key
+
+
+# ------------------------------------------------------------ vs the oracle --
+def oracle_gat(z, seed):
+    from oracle import fused
+    a = concat_arrays(z)
+    rws = fused.typed_relation("W2S", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    rsw = fused.typed_relation("S2W", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    n_w, n_s = rsw["n_dst"], rws["n_dst"]
+    Xw, Xs, T = gat_inputs(seed, n_w, n_s)
+    Xw, Xs, T = (t.double().requires_grad_() for t in (Xw, Xs, T))
+    w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
+    p1, p2 = fused.as_params(w2s), fused.as_params(s2w)
+    o1 = fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T)
+    o2 = fused.wswgat_layer("S2W", rsw, Xw, Xs, p2, T)
+    R1, R2 = upstream(seed, o1.shape, o2.shape)
+    ((o1 * R1.double()).sum() + (o2 * R2.double()).sum()).backward()
+    return dict(o1=o1, o2=o2, Xw=Xw, Xs=Xs, T=T, p1=p1, p2=p2, n_w=n_w, n_s=n_s)
+
+
+def synth_fixture(docs):
+    """Fixture-like dict from synth DocArrays (no reference outputs)."""
+    offs = np.cumsum([0] + [d.n_nodes for d in docs])
+    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
+    z = {"g_n_nodes": np.array([d.n_nodes for d in docs]), "g_n_edges": np.array([len(d.src) for d in docs]),
+         "g_unit": cat(lambda d, o: d.unit), "g_ndtype": cat(lambda d, o: d.ndtype),
+         "g_wid": cat(lambda d, o: d.wid), "g_src": cat(lambda d, o: d.src + o),
+         "g_dst": cat(lambda d, o: d.dst + o), "g_tffrac": cat(lambda d, o: d.tffrac),
+         "g_edtype": cat(lambda d, o: d.edtype)}
+    z["n_w"] = int((z["g_unit"] == 0).sum())
+    z["n_s"] = int((z["g_unit"] == 1).sum())
+    return z
+
+
+def random_docs(kind, seed):
+    from hetersumgraph_amd import synth
+    rng = np.random.default_rng(1000 + seed)
+    if kind == "hsg_edge":
+        # k up to 90 (>64-edge W2S segments), isolated words, all boxes
+        return [synth.make_hsg_doc(rng, N=int(rng.integers(1, 12)), W=int(rng.integers(20, 120)), k=30,
+                                   k_jitter=30, isolated_words=3, tf_range=(0.0, 1.0)) for _ in range(3)]
+    if kind == "hsg_hub":
+        # 70 sentences all containing the same few words (>64-edge S2W segments)
+        return [synth.make_hsg_doc(rng, N=70, W=6, k=4, tf_range=(0.0, 1.0))]
+    if kind == "hdsg":
+        return [synth.make_hdsg_example(rng, tuple(int(x) for x in rng.integers(1, 6, size=3)), W=60, k=8,
+                                        doc_words=25, tf_range=(0.0, 1.0)) for _ in range(3)]
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind,seed", [("hsg_edge", 0), ("hsg_edge", 1), ("hsg_hub", 0), ("hdsg", 0)])
+def test_gat_vs_oracle_random_graphs(kind, seed):
+    z = synth_fixture(random_docs(kind, seed))
+    r = run_gat(z, 7 + seed)
+    o = oracle_gat(z, 7 + seed)
+    assert max_err(r["o1"], o["o1"]) <= 1e-5
+    assert max_err(r["o2"], o["o2"]) <= 1e-5
+    assert_grad_close(r["Xs"].grad, o["Xs"].grad)
+    assert_grad_close(r["Xw"].grad, o["Xw"].grad)
+    assert_grad_close(r["T"].grad, o["T"].grad, rtol=1e-3)
+    for tag, mod, pd in (("w2s", r["w2s"], o["p1"]), ("s2w", r["s2w"], o["p2"])):
+        for k, p in mod.named_parameters():
+            assert_grad_close(p.grad, pd[k].grad, rtol=1e-3)
+
+
+@pytest.mark.parametrize("H,hidden", [(4, 64), (1, 64), (16, 64), (3, 48)])
+def test_other_head_shapes(H, hidden):
+    """W2S with a different n_head / hidden_size (hps flags, train.py:282-293)."""
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    from hetersumgraph_amd.module.GAT import WSWGAT
+    from oracle import fused
+    import weights
+    z = synth_fixture(random_docs("hsg_edge", 5))
+    G = build_graph(z).to("cuda")
+    a = concat_arrays(z)
+    rel = fused.typed_relation("W2S", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    Xw = torch.from_numpy(weights.feature(9, "Xw", (z["n_w"], 300), 0.4))
+    Xs = torch.from_numpy(weights.feature(9, "Xs", (z["n_s"], hidden), 1.0))
+    T = torch.from_numpy(weights.param_value(9, "T", (10, 50)))
+    m = weights.seed_module(WSWGAT(300, hidden, H, 0.1, 512, 0.1, 50, "W2S"), 77).eval()
+    p = fused.as_params(m, requires_grad=False)
+    with torch.no_grad():
+        ref = fused.wswgat_layer("W2S", rel, Xw.double(), Xs.double(), p, T.double())
+        register_tfidf_table(G, T.cuda())
+        got = m.cuda()(G, Xw.cuda(), Xs.cuda())
+    assert max_err(got, ref) <= 1e-5
+
+
+def test_deterministic_reruns():
+    z = load_fixture("gat_cfg1")
+    a = run_gat(z, 3)
+    b = run_gat(z, 3)
+    assert torch.equal(a["o1"], b["o1"]) and torch.equal(a["o2"], b["o2"])
+    assert torch.equal(a["Xw"].grad, b["Xw"].grad) and torch.equal(a["Xs"].grad, b["Xs"].grad)
+    assert torch.equal(a["T"].grad, b["T"].grad)
+
+
+def test_cpu_tensors_fail_loudly():
+    """No CPU fallback: the product path refuses host tensors."""
+    z = load_fixture("gat_small")
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        run_gat(z, 1, device="cpu")
+
+
+def test_config2_full_size_vs_oracle():
+    """BASELINE config 2 (32 docs x N=35, W=600, k=36; 159,040 edges) end to end
+    against the fp64 oracle."""
+    from hetersumgraph_amd import synth
+    docs = synth.make_batch_docs("cfg2", seed=0)
+    z = synth_fixture(docs)
+    assert int(z["g_n_edges"].sum()) == 159040
+    r = run_gat(z, 21)
+    o = oracle_gat(z, 21)
+    assert max_err(r["o1"], o["o1"]) <= 2e-5
+    assert max_err(r["o2"], o["o2"]) <= 2e-5
+    assert_grad_close(r["Xs"].grad, o["Xs"].grad, max_bad_rows=8)
+    assert_grad_close(r["Xw"].grad, o["Xw"].grad, max_bad_rows=40)

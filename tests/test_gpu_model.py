@@ -1,0 +1,97 @@
+"""Sentence-logit parity of HSumGraph / HSumDocGraph on the GPU against the
+reference's own HiGraph.py run on CPU (golden vectors, tests/golden/make_golden.py).
+
+This is the BASELINE.json contract: sentence scores within 1e-4 (fp32) of the
+reference CPU path on the same batched graph.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import weights
+from helpers import build_graph, load_fixture, projections
+
+pytestmark = pytest.mark.gpu
+
+
+class HPS:
+    def __init__(self, **kw):
+        d = dict(n_iter=2, word_emb_dim=300, feat_embed_size=50, n_feature_size=128, hidden_size=64,
+                 n_head=8, atten_dropout_prob=0.1, ffn_inner_hidden_size=512, ffn_dropout_prob=0.1,
+                 doc_max_timesteps=50, lstm_hidden_state=128, lstm_layers=2, bidirectional=True,
+                 sent_max_len=100, cuda=True, vocab_size=500)
+        d.update(kw)
+        self.__dict__.update(d)
+
+
+def build_model(cls_name, seed):
+    from hetersumgraph_amd import HiGraph
+    hps = HPS()
+    torch.manual_seed(seed)
+    embed = torch.nn.Embedding(hps.vocab_size, 300, padding_idx=0)
+    model = getattr(HiGraph, cls_name)(hps, embed)
+    weights.seed_module(model, seed)
+    return model.eval().cuda()
+
+
+@pytest.mark.parametrize("name,cls,seed", [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5)])
+def test_model_logits_match_reference(name, cls, seed):
+    from hetersumgraph_amd import graph as hg
+    z = load_fixture(name)
+    G = build_graph(z, z["sent_words"], z["sent_label"])
+    G.to(torch.device("cuda"))                      # in-place, train.py:112
+    model = build_model(cls, seed)
+    logits = model(G)
+    err = np.abs(logits.detach().cpu().double().numpy() - z["logits"]).max()
+    assert err <= 1e-4, f"logit max |diff| {err:.3e}"
+    err64 = np.abs(logits.detach().cpu().double().numpy() - z["logits64"]).max()
+    assert err64 <= 1e-4
+    # train.py:115-119 loss through the graph API, then backward
+    snode = G.filter_nodes(lambda n: n.data["dtype"] == 1)
+    label = G.ndata["label"][snode].sum(-1)
+    G.nodes[snode].data["loss"] = F.cross_entropy(logits, label, reduction="none").unsqueeze(-1)
+    loss = hg.sum_nodes(G, "loss").mean()
+    assert abs(loss.item() - float(z["loss64"])) <= 1e-4
+    loss.backward()
+    n = 0
+    for k, p in model.named_parameters():
+        key = f"grad.{k}"
+        if p.grad is None:
+            continue
+        if key in z:
+            ref = z[key].astype(np.float64)
+            got = p.grad.detach().cpu().double().numpy()
+            assert np.abs(got - ref).max() <= 2e-3 * max(np.abs(ref).max(), 1e-3), k
+            n += 1
+        elif "proj." + key in z:
+            got = projections(p.grad, seed, key)
+            ref = z["proj." + key]
+            assert np.abs(got - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-5, k
+            n += 1
+    assert n >= 90
+
+
+def test_train_step_runs_and_learns():
+    """One reference-style train step (train.py:114-135): fwd, CE, sum_nodes, bwd,
+    clip, Adam -- in train mode with dropout -- and the loss goes down."""
+    from hetersumgraph_amd import graph as hg
+    z = load_fixture("model_hsg")
+    G = build_graph(z, z["sent_words"], z["sent_label"])
+    G.to(torch.device("cuda"))
+    model = build_model("HSumGraph", 4).train()
+    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=5e-4)
+    losses = []
+    for _ in range(5):
+        out = model(G)
+        snode = G.filter_nodes(lambda n: n.data["dtype"] == 1)
+        label = G.ndata["label"][snode].sum(-1)
+        G.nodes[snode].data["loss"] = F.cross_entropy(out, label, reduction="none").unsqueeze(-1)
+        loss = hg.sum_nodes(G, "loss").mean()
+        assert torch.isfinite(loss)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0]
