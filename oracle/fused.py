@@ -116,3 +116,27 @@ def as_params(module_or_dict, dtype=torch.float64, requires_grad=True):
         t = torch.as_tensor(np.asarray(v.detach().cpu() if hasattr(v, "detach") else v)).to(dtype)
         out[k] = t.clone().requires_grad_(requires_grad)
     return out
+
+
+def gat_aggregate_ref(e_src, e_dst, tf_row, phantom, n_dst, Z, a1, tau, origin=None, slope=SLOPE):
+    """Op-level restatement of ``hetersumgraph_amd.ops.gat_aggregate`` (the fused
+    restatement of SURVEY §8a) for kernel-level checks: Z [n_src, H*D], a1 [H, D],
+    tau [rows, H] indexed by ``tf_row`` per typed edge (CSR or any order)."""
+    H, D = a1.shape
+    Zh = Z.view(Z.shape[0], H, D)
+    sigma = (Zh * a1.unsqueeze(0)).sum(-1)                          # [n_src, H]
+    e_src = torch.as_tensor(e_src, dtype=torch.long)
+    e_dst = torch.as_tensor(e_dst, dtype=torch.long)
+    tf_row = torch.as_tensor(tf_row, dtype=torch.long)
+    phantom = torch.as_tensor(phantom).to(Z.dtype)
+    s = F.leaky_relu(sigma[e_src] + tau[tf_row], slope)              # [E, H]
+    mx = torch.full((n_dst, H), -torch.inf, dtype=Z.dtype).scatter_reduce(
+        0, e_dst.unsqueeze(1).expand(-1, H), s, "amax")
+    mx = torch.where(phantom.unsqueeze(1) > 0, torch.clamp_min(mx, 0.0), mx)
+    mx = torch.where(torch.isinf(mx), torch.zeros_like(mx), mx).detach()
+    p = torch.exp(s - mx[e_dst])
+    den = torch.zeros(n_dst, H, dtype=Z.dtype).index_add(0, e_dst, p) + phantom.unsqueeze(1) * torch.exp(-mx)
+    alpha = p / den[e_dst]
+    h = torch.zeros(n_dst, H, D, dtype=Z.dtype).index_add(0, e_dst, alpha.unsqueeze(-1) * Zh[e_src])
+    h = h.view(n_dst, H * D)
+    return h if origin is None else F.elu(h) + origin

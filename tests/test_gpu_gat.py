@@ -87,12 +87,15 @@ def test_gat_vs_reference_golden(name, seed, dense):
     for tag, mod in (("w2s", r["w2s"]), ("s2w", r["s2w"])):
         for k, p in mod.named_parameters():
             key = f"grad.{tag}.{k}"
+            # a ReLU-gate flip in one input row (cfg1: word 479) perturbs every row of
+            # a weight gradient, so there the bound is relative to the largest entry
+            prtol = 5e-3 if bad else 1e-3
             if key in z:
-                assert_grad_close(p.grad, z[key], rtol=1e-3, max_bad_rows=bad)
+                assert_grad_close(p.grad, z[key], rtol=prtol, max_bad_rows=bad)
             elif "proj." + key in z:
                 got = projections(p.grad, seed, key)
                 ref = z["proj." + key]
-                assert np.abs(got - ref).max() <= 2e-3 * np.abs(ref).max() + 1e-4, key
+                assert np.abs(got - ref).max() <= prtol * np.abs(ref).max() + 1e-4, key
 
 
 # ------------------------------------------------------------ vs the oracle --

@@ -42,6 +42,10 @@ def test_model_logits_match_reference(name, cls, seed):
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))                      # in-place, train.py:112
     model = build_model(cls, seed)
+    # MIOpen (like cuDNN) has no RNN backward in eval mode; train-mode LSTM with
+    # its inter-layer dropout set to 0 is numerically the eval LSTM
+    model.lstm.train()
+    model.lstm.dropout = 0.0
     logits = model(G)
     err = np.abs(logits.detach().cpu().double().numpy() - z["logits"]).max()
     assert err <= 1e-4, f"logit max |diff| {err:.3e}"
@@ -93,5 +97,6 @@ def test_train_step_runs_and_learns():
         loss.backward()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         opt.step()
+        G.ndata.pop("loss")          # train.py gets a fresh graph every step
         losses.append(loss.item())
     assert losses[-1] < losses[0]
