@@ -105,13 +105,14 @@ def time_fwd_kernel(G, stack, Xw, Xs, reps):
     recorded on the stream the kernel is launched on."""
     import ctypes
     from hetersumgraph_amd import _lib
-    from hetersumgraph_amd.module.GATLayer import edge_tau, head_tensors
+    from hetersumgraph_amd.module.GATLayer import edge_tau
     lib = _lib.load()
     rel = G.relation("S2W")
-    heads = list(stack.sent2word.layer.heads)
-    H, D = len(heads), heads[0].fc.out_features
+    layer = stack.sent2word.layer
+    H, D = layer.num_heads, layer.head_dim
     with torch.no_grad():
-        W, a1, a3, wf, bf = head_tensors(heads)
+        W, attn, wf, bf = layer.fused_params()
+        a1, a3 = attn[:, :D], attn[:, 2 * D:]
         Z = torch.nn.functional.linear(Xs, W).contiguous()
         tau, mode = edge_tau(G, rel, a3, wf, bf)
         sigma = Z.new_empty(rel.n_src, H)

@@ -20,7 +20,12 @@ HSG_TAU_PER_EDGE = 1
 
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
-           "hsg_attn_src_logits", "hsg_version")
+           "hsg_attn_src_logits", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats",
+           "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd")
+
+HSG_EPI_STORE = 0
+HSG_EPI_RELU_BWD = 1
+HSG_EPI_ADD = 2
 
 
 class HsgRel(ctypes.Structure):
@@ -46,7 +51,13 @@ _SIGS = {
     "hsg_gat_bwd_src": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
+    "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P],
+    "hsg_gemm_workspace_floats": [_I, _I, _I, _I],
+    "hsg_ln_bwd_blocks": [_I],
+    "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
+    "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P, _P],
 }
+_RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_gemm_workspace_floats": ctypes.c_size_t}
 
 
 def load():
@@ -62,7 +73,7 @@ def load():
     for name, args in _SIGS.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_char_p if name == "hsg_version" else ctypes.c_int
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
     _lib = lib
     return lib
 

@@ -9,7 +9,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip",)]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_gemm.hip", "hsg_rows.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
 
@@ -25,7 +25,7 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(ROOT, "include", "hsg.h")]
+    deps = SOURCES + [os.path.join(ROOT, "include", "hsg.h"), os.path.join(HERE, "csrc", "hsg_rng.h")]
     return any(os.path.getmtime(s) > t for s in deps)
 
 

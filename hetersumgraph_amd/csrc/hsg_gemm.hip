@@ -1,0 +1,314 @@
+// hsg_gemm.hip -- fp32 MFMA GEMM with fused epilogues for gfx950 (MI355X).
+//
+// The dense parts of one WSWGAT application are fp32 GEMMs: the head
+// projection fc (GATLayer.py:110/146), and the position-wise FFN
+// W2 relu(W1 x + b1) + b2 (GATLayer.py:39) with its backward.  gfx950 has no
+// xf32 path, but v_mfma_f32_32x32x2_f32 computes an exact f32 fmaf chain at the
+// f32 vector peak while leaving the VALU free for the epilogue.
+//
+//   C[m][n] = epi( sum_k A(m,k) * B(k,n) )
+//     A(m,k) = a_kc ? A[m*lda + k] : A[k*lda + m]      (K-contiguous or M-contiguous)
+//     B(k,n) = b_kc ? B[n*ldb + k] : B[k*ldb + n]      (K-contiguous or N-contiguous)
+//   epi: STORE  v (+bias[n]) (relu if requested)
+//        RELU_BWD v * (aux[m][n] > 0)            -- relu' applied to dH
+//        ADD    v (+bias[n]) + aux[m][n]         -- accumulate (aux may alias C)
+//
+// Block = 256 threads (2x2 waves), tile BM x BN x 32, register-staged double
+// buffer in LDS, one barrier per K tile.  LDS images:
+//   K-contiguous operands: [rows][32+4] floats, read with ds_read_b128 (4 MFMA
+//     k-steps per read; the +4 pad makes the 16-lane b128 groups conflict-free);
+//   M/N-contiguous operands: [32][BM+4], read with ds_read_b32 (lanes on
+//     consecutive columns -> conflict-free).
+// K of one MFMA k-step s (0..15) is s for lanes 0-31 and 16+s for lanes 32-63,
+// identically for A and B, so the sum over a 32-deep tile is exact.
+// Split-K (grid.z > 1) writes fp32 partial slabs, reduced (with the epilogue) by
+// k_splitk_reduce in split order -> deterministic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hsg.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 32;
+constexpr int kPad = 4;
+
+struct GemmArgs {
+    int M, N, K;
+    const float *A;
+    int lda;
+    const float *B;
+    int ldb;
+    float *C;
+    int ldc;
+    const float *bias;
+    const float *aux;
+    int ldaux;
+    int epi;
+    int relu;
+    int k_tiles_per_split;
+    float *ws;            // split-K partials [splits][M][N]
+};
+
+__device__ __forceinline__ float epi_apply(float v, int m, int n, const GemmArgs &p) {
+    if (p.epi == HSG_EPI_RELU_BWD) return p.aux[(size_t)m * p.ldaux + n] > 0.f ? v : 0.f;
+    if (p.bias) v += p.bias[n];
+    if (p.epi == HSG_EPI_ADD) v += p.aux[(size_t)m * p.ldaux + n];
+    if (p.relu) v = fmaxf(v, 0.f);
+    return v;
+}
+
+template <bool KC, int ROWS>
+struct Stage {
+    // one operand tile: KC -> [ROWS x 32] from rows of a K-contiguous matrix;
+    // !KC -> [32 x ROWS] from 32 rows of a ROWS-contiguous matrix
+    static constexpr int LD = KC ? (kBK + kPad) : (ROWS + kPad);
+    static constexpr int NV = ROWS * kBK / 4 / 256;   // float4 per thread
+    f32x4 v[NV];
+
+    __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int r0, int nr, int k0, int nk) {
+        const bool full = KC ? (r0 + ROWS <= nr && k0 + kBK <= nk) : (k0 + kBK <= nk && r0 + ROWS <= nr);
+        if (full) {
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int idx = threadIdx.x + 256 * i;
+                int row, col;
+                if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+                else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
+                const int gr = KC ? r0 + row : k0 + row;
+                const int gc = KC ? k0 + col : r0 + col;
+                v[i] = *reinterpret_cast<const f32x4 *>(g + (size_t)gr * ld + gc);
+            }
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            int row, col;   // row in the "major" dimension of global memory, col contiguous
+            if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+            else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
+            const int gr = KC ? r0 + row : k0 + row;          // global row
+            const int gc = KC ? k0 + col : r0 + col;          // global col
+            const int lim_r = KC ? nr : nk, lim_c = KC ? nk : nr;
+            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            if (gr < lim_r) {
+                const float *src = g + (size_t)gr * ld + gc;
+                if (gc + 3 < lim_c) {
+                    x = *reinterpret_cast<const f32x4 *>(src);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (gc + e < lim_c) x[e] = src[e];
+                }
+            }
+            v[i] = x;
+        }
+    }
+
+    __device__ __forceinline__ void store(float *s) const {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            int row, col;
+            if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+            else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
+            *reinterpret_cast<f32x4 *>(s + row * LD + col) = v[i];
+        }
+    }
+};
+
+template <int BM, int BN, bool AK, bool BKC>
+__global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    using SA = Stage<AK, BM>;
+    using SB = Stage<BKC, BN>;
+    __shared__ __attribute__((aligned(16))) float sA[2][AK ? BM * SA::LD : kBK * SA::LD];
+    __shared__ __attribute__((aligned(16))) float sB[2][BKC ? BN * SB::LD : kBK * SB::LD];
+
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int li = lane & 31, h = lane >> 5;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+    const int kt_total = (p.K + kBK - 1) / kBK;
+    const int kt0 = blockIdx.z * p.k_tiles_per_split;
+    const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    SA ra;
+    SB rb;
+    int cur = 0;
+    if (kt0 < kt1) {
+        ra.load(p.A, p.lda, m0, p.M, kt0 * kBK, p.K);
+        rb.load(p.B, p.ldb, n0, p.N, kt0 * kBK, p.K);
+        ra.store(sA[0]);
+        rb.store(sB[0]);
+    }
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+        const bool more = kt + 1 < kt1;
+        if (more) {
+            ra.load(p.A, p.lda, m0, p.M, (kt + 1) * kBK, p.K);
+            rb.load(p.B, p.ldb, n0, p.N, (kt + 1) * kBK, p.K);
+        }
+        const float *a_s = sA[cur];
+        const float *b_s = sB[cur];
+        f32x4 af[2][TM], bf[2][TN];
+        auto frag = [&](f32x4 (&fa)[TM], f32x4 (&fb)[TN], int s4) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm * WM + i * 32 + li;
+                if constexpr (AK) {
+                    fa[i] = *reinterpret_cast<const f32x4 *>(a_s + row * SA::LD + h * (kBK / 2) + s4);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fa[i][q] = a_s[(h * (kBK / 2) + s4 + q) * SA::LD + row];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = wn * WN + j * 32 + li;
+                if constexpr (BKC) {
+                    fb[j] = *reinterpret_cast<const f32x4 *>(b_s + col * SB::LD + h * (kBK / 2) + s4);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) fb[j][q] = b_s[(h * (kBK / 2) + s4 + q) * SB::LD + col];
+                }
+            }
+        };
+        frag(af[0], bf[0], 0);
+#pragma unroll
+        for (int g = 0; g < kBK / 8; ++g) {
+            if (g + 1 < kBK / 8) frag(af[(g + 1) & 1], bf[(g + 1) & 1], 4 * (g + 1));
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g & 1][i][q], bf[g & 1][j][q],
+                                                                          acc[i][j], 0, 0, 0);
+        }
+        if (more) {
+            ra.store(sA[cur ^ 1]);
+            rb.store(sB[cur ^ 1]);
+        }
+        __syncthreads();
+        cur ^= 1;
+    }
+
+    // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
+    const bool split = gridDim.z > 1;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WN + j * 32 + li;
+            if (n >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m >= p.M) continue;
+                if (split) p.ws[((size_t)blockIdx.z * p.M + m) * p.N + n] = acc[i][j][r];
+                else p.C[(size_t)m * p.ldc + n] = epi_apply(acc[i][j][r], m, n, p);
+            }
+        }
+}
+
+__global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
+    const size_t total = (size_t)p.M * p.N;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        float v = 0.f;
+        for (int z = 0; z < splits; ++z) v += p.ws[(size_t)z * total + idx];
+        const int m = (int)(idx / p.N), n = (int)(idx % p.N);
+        p.C[(size_t)m * p.ldc + n] = epi_apply(v, m, n, p);
+    }
+}
+
+template <int BM, int BN>
+int launch_tiles(const GemmArgs &p, bool ak, bool bk, int splits, hipStream_t st) {
+    dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false>), grid, dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits) {
+    (void)K;
+    return splits > 1 ? (size_t)splits * M * N : 0;
+}
+
+int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                 int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
+                 int relu, int splits, float *workspace, void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
+    // float4 staging needs 16-byte aligned rows
+    if ((lda & 3) || (ldb & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)B) & 15)) return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const int kt_total = (K + kBK - 1) / kBK;
+    if (splits == 0) {
+        // automatic: split K when the output has too few tiles to fill the GPU
+        const long tiles = (long)((M + 127) / 128) * ((N + 63) / 64);
+        splits = 1;
+        if (tiles < 256 && kt_total >= 8) {
+            splits = (int)((512 + tiles - 1) / tiles);
+            if (splits > kt_total / 4) splits = kt_total / 4;
+            if (splits < 1) splits = 1;
+        }
+    }
+    if (splits < 1) splits = 1;
+    if (splits > kt_total) splits = kt_total > 0 ? kt_total : 1;
+    if (splits > 1 && !workspace) return HSG_EINVAL;
+    GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
+               (kt_total + splits - 1) / splits, workspace};
+    const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
+    // pick the tile whose block count best fills 256 CUs (blocks/CU by LDS+VGPR
+    // budget: 128x128 -> 2, 128x64 -> 3, 64x64 -> 4), favouring larger tiles
+    struct Cand { int bm, bn, per_cu; float eff; };
+    Cand cands[3] = {{128, 128, 2, 1.0f}, {128, 64, 3, 0.9f}, {64, 64, 4, 0.8f}};
+    int best = 0;
+    float best_score = -1.f;
+    for (int c = 0; c < 3; ++c) {
+        const long nb = (long)((M + cands[c].bm - 1) / cands[c].bm) * ((N + cands[c].bn - 1) / cands[c].bn) * splits;
+        const long slots = 256L * cands[c].per_cu;
+        const long rounds = (nb + slots - 1) / slots;
+        const float fill = (float)nb / (float)(rounds * slots);
+        const float score = fill * cands[c].eff;
+        if (score > best_score + 1e-3f) { best_score = score; best = c; }
+    }
+    int rc;
+    if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
+    else if (best == 1) rc = launch_tiles<128, 64>(p, ak, bk, splits, st);
+    else rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
+    if (rc || splits == 1) return rc;
+    const size_t total = (size_t)M * N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, st, p, splits);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

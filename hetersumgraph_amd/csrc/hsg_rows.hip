@@ -1,0 +1,190 @@
+// hsg_rows.hip -- row-wise epilogues of PositionwiseFeedForward for gfx950.
+//
+// Reference (module/GATLayer.py:35-44):
+//     out = LayerNorm(Dropout(W2 relu(W1 x + b1) + b2) + x),  eps 1e-5
+// The GEMMs run on MFMA (hsg_gemm.hip); this file fuses everything after the
+// second GEMM into one pass over the rows (dropout, residual add, LayerNorm) and
+// the matching backward (LayerNorm backward, dropout backward, residual split,
+// per-block dgamma/dbeta partials -- no atomics, deterministic).
+//
+// Dropout masks come from a counter-based hash of (seed, offset, element): seed is
+// read from device memory (so a HIP-graph replay can advance it), offset is a
+// per-call-site constant.  Forward and backward regenerate the same mask, so no
+// mask tensor is stored.  One wave per row; lane owns columns lane + 64*i.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hsg.h"
+#include "hsg_rng.h"
+
+namespace {
+
+constexpr int kMaxPerLane = 8;   // d <= 512
+
+__device__ __forceinline__ float wsum(float v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int NPL>
+__global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__restrict__ y,
+                                                const float *__restrict__ x, const float *__restrict__ gamma,
+                                                const float *__restrict__ beta, float eps, float p_drop,
+                                                const int64_t *__restrict__ seedp, uint32_t offset,
+                                                float *__restrict__ out, float *__restrict__ mean,
+                                                float *__restrict__ rstd) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += gridDim.x * 4) {
+        float s[NPL];
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            s[i] = 0.f;
+            if (c < d) {
+                const size_t o = (size_t)r * d + c;
+                float v = y[o];
+                if (p_drop > 0.f) v = hsg_keep(seed, offset, o, thr) ? v * scale : 0.f;
+                s[i] = v + x[o];
+                acc += s[i];
+            }
+        }
+        const float mu = wsum(acc) / d;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+            if (lane + 64 * i < d) { const float t = s[i] - mu; var = fmaf(t, t, var); }
+        const float rs = rsqrtf(wsum(var) / d + eps);
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            if (c < d) out[(size_t)r * d + c] = (s[i] - mu) * rs * gamma[c] + beta[c];
+        }
+        if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+    }
+}
+
+template <int NPL>
+__global__ __launch_bounds__(256) void k_ln_bwd(int n, int d, const float *__restrict__ dout,
+                                                const float *__restrict__ y, const float *__restrict__ x,
+                                                const float *__restrict__ gamma, const float *__restrict__ mean,
+                                                const float *__restrict__ rstd, float p_drop,
+                                                const int64_t *__restrict__ seedp, uint32_t offset,
+                                                float *__restrict__ dy, float *__restrict__ dx,
+                                                float *__restrict__ dgamma_part, float *__restrict__ dbeta_part) {
+    __shared__ float s_g[4][kMaxPerLane * 64];
+    __shared__ float s_b[4][kMaxPerLane * 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    float dg[NPL], db[NPL];
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) { dg[i] = 0.f; db[i] = 0.f; }
+    for (int r = blockIdx.x * 4 + wid; r < n; r += gridDim.x * 4) {
+        const float mu = mean[r], rs = rstd[r];
+        float xh[NPL], g[NPL];
+        bool keep[NPL];
+        float sg = 0.f, sgx = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            xh[i] = g[i] = 0.f;
+            keep[i] = true;
+            if (c < d) {
+                const size_t o = (size_t)r * d + c;
+                float v = y[o];
+                if (p_drop > 0.f) {
+                    keep[i] = hsg_keep(seed, offset, o, thr);
+                    v = keep[i] ? v * scale : 0.f;
+                }
+                xh[i] = (v + x[o] - mu) * rs;
+                const float go = dout[o];
+                g[i] = go * gamma[c];
+                sg += g[i];
+                sgx = fmaf(g[i], xh[i], sgx);
+                dg[i] = fmaf(go, xh[i], dg[i]);
+                db[i] += go;
+            }
+        }
+        const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            if (c < d) {
+                const size_t o = (size_t)r * d + c;
+                const float ds = rs * (g[i] - mg - xh[i] * mgx);
+                dx[o] = ds;
+                dy[o] = keep[i] ? ds * scale : 0.f;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NPL; ++i) { s_g[wid][lane + 64 * i] = dg[i]; s_b[wid][lane + 64 * i] = db[i]; }
+    __syncthreads();
+    for (int c = threadIdx.x; c < d; c += blockDim.x) {
+        dgamma_part[(size_t)blockIdx.x * d + c] = s_g[0][c] + s_g[1][c] + s_g[2][c] + s_g[3][c];
+        dbeta_part[(size_t)blockIdx.x * d + c] = s_b[0][c] + s_b[1][c] + s_b[2][c] + s_b[3][c];
+    }
+}
+
+int grid_rows(int n, int cap) {
+    int b = (n + 3) / 4;
+    if (b < 1) b = 1;
+    return b < cap ? b : cap;
+}
+constexpr int kLnBwdGridCap = 512;
+
+int status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsg_ln_bwd_blocks(int n) { return grid_rows(n, kLnBwdGridCap); }
+
+int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta, float eps,
+               float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
+               void *stream) {
+    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed))
+        return HSG_EINVAL;
+    if (n == 0) return 0;
+    const int npl = (d + 63) / 64;
+    dim3 grid(grid_rows(n, 8192)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+#define HSG_LNF(K)                                                                                       \
+    case K:                                                                                              \
+        hipLaunchKernelGGL(k_ln_fwd<K>, grid, block, 0, st, n, d, y, x, gamma, beta, eps, p_drop, seed, \
+                           offset, out, mean, rstd);                                                     \
+        break;
+    switch (npl) { HSG_LNF(1) HSG_LNF(2) HSG_LNF(3) HSG_LNF(4) HSG_LNF(5) HSG_LNF(6) HSG_LNF(7) HSG_LNF(8) }
+#undef HSG_LNF
+    return status();
+}
+
+int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+               const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
+               float *dy, float *dx, float *dgamma_part, float *dbeta_part, void *stream) {
+    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed))
+        return HSG_EINVAL;
+    if (n == 0) return 0;
+    const int npl = (d + 63) / 64;
+    dim3 grid(grid_rows(n, kLnBwdGridCap)), block(256);
+    hipStream_t st = (hipStream_t)stream;
+#define HSG_LNB(K)                                                                                       \
+    case K:                                                                                              \
+        hipLaunchKernelGGL(k_ln_bwd<K>, grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, \
+                           seed, offset, dy, dx, dgamma_part, dbeta_part);                               \
+        break;
+    switch (npl) { HSG_LNB(1) HSG_LNB(2) HSG_LNB(3) HSG_LNB(4) HSG_LNB(5) HSG_LNB(6) HSG_LNB(7) HSG_LNB(8) }
+#undef HSG_LNB
+    return status();
+}
+
+}  // extern "C"

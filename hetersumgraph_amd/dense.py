@@ -1,0 +1,69 @@
+"""Dense fp32 ops over libhsg.so's MFMA GEMM (hsg_gemm_f32, include/hsg.h).
+
+``gemm(A, B, a_t, b_t)`` computes ``op(A) @ op(B)`` for row-major tensors with
+``op(X) = X.T if x_t else X``, plus the fused epilogues the FFN and the head
+projection need (bias, ReLU, ReLU-backward mask, accumulate).  Everything is
+enqueued on the current stream; no host synchronisation.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr, stream_of
+
+
+def _ld(t):
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("gemm operands must be 2-D row-major with unit column stride")
+    return t.stride(0)
+
+
+def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=None, add=None,
+         splits=0, workspace=None):
+    """C = op(A) @ op(B) [+ bias] [relu] | * (relu_mask > 0) | + add.
+
+    A [M,K] (or [K,M] with a_t), B [K,N] (or [N,K] with b_t), fp32 on the GPU.
+    ``add`` may be ``out`` itself (accumulate)."""
+    lib = load()
+    if not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
+        raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
+    M, K = (A.shape[1], A.shape[0]) if a_t else (A.shape[0], A.shape[1])
+    K2, N = (B.shape[1], B.shape[0]) if b_t else (B.shape[0], B.shape[1])
+    if K != K2:
+        raise ValueError(f"gemm: inner dims {K} != {K2}")
+    if out is None:
+        out = A.new_empty(M, N)
+    epi, aux = HSG_EPI_STORE, None
+    if relu_mask is not None:
+        epi, aux = HSG_EPI_RELU_BWD, relu_mask
+    elif add is not None:
+        epi, aux = HSG_EPI_ADD, add
+    ws = None
+    if splits == 0:
+        splits = auto_splits(M, N, K)
+    if splits > 1:
+        n = lib.hsg_gemm_workspace_floats(M, N, K, splits)
+        ws = workspace if workspace is not None and workspace.numel() >= n else A.new_empty(n)
+    check(lib.hsg_gemm_f32(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), ptr(out),
+                           _ld(out), ptr(bias), ptr(aux), _ld(aux) if aux is not None else 0, epi,
+                           int(relu), int(splits), ptr(ws), stream_of(A)), "hsg_gemm_f32")
+    return out
+
+
+def auto_splits(M, N, K):
+    """Mirror of hsg_gemm_f32's splits == 0 rule (so the workspace can be sized)."""
+    kt = (K + 31) // 32
+    tiles = ((M + 127) // 128) * ((N + 63) // 64)
+    if tiles < 256 and kt >= 8:
+        return max(1, min((512 + tiles - 1) // tiles, kt // 4))
+    return 1
+
+
+def splits_for(M, N, K, n_cu=256):
+    """Split-K factor for the weight-gradient GEMMs (tiny M x N, K = rows):
+    aim at ~2 tiles per CU, at least 4 K-tiles per split."""
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    kt = (K + 31) // 32
+    s = max(1, min(kt // 4, (2 * n_cu) // max(tiles, 1)))
+    return s

@@ -1,8 +1,8 @@
 """Per-head GAT layers and the position-wise FFN (reference: module/GATLayer.py).
 
-Parameter names and shapes match the reference exactly (state_dict compatible,
-SURVEY Appendix B), but the computation is not per head: ``MultiHeadLayer``
-concatenates every head's weights and runs all heads in one fused HIP pass
+State-dict names and shapes match the reference exactly, but
+the computation is not per head: ``MultiHeadLayer`` keeps every head's weights in
+fused tensors and runs all heads in one HIP pass
 (:func:`hetersumgraph_amd.ops.gat_aggregate`).  A single head's ``forward(g, h)``
 is still available and is the same kernel with H = 1.
 """
@@ -14,8 +14,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ffn import ffn_forward
 from ..ops import LEAKY_SLOPE, gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
-from ..relation import N_BOX, ZERO_ROW
+from ..relation import N_BOX
 
 # The reference asserts "no NaN" around every FFN (GATLayer.py:36, 43), a host sync
 # per call.  Same error behaviour behind a switch (default off: it would serialise
@@ -29,7 +30,7 @@ class PositionwiseFeedForward(nn.Module):
     """LN(x + Dropout(W2 relu(W1 x + b1) + b2)), eps 1e-5 (GATLayer.py:25-44).
 
     Kept as two k=1 ``Conv1d`` modules for state_dict compatibility; executed as
-    row-major GEMMs on [n, d]."""
+    MFMA GEMMs with fused epilogues (:mod:`hetersumgraph_amd.ffn`)."""
 
     def __init__(self, d_in, d_hid, dropout=0.1):
         super().__init__()
@@ -43,17 +44,21 @@ class PositionwiseFeedForward(nn.Module):
         x2 = x.reshape(-1, shape[-1])            # reference feeds [1, n, d] (GAT.py:58)
         if CHECK_NAN:
             assert not torch.any(torch.isnan(x2)), "FFN input"
-        hid = F.relu(F.linear(x2, self.w_1.weight.squeeze(-1), self.w_1.bias))
-        y = F.linear(hid, self.w_2.weight.squeeze(-1), self.w_2.bias)
-        y = self.dropout(y)
-        y = self.layer_norm(y + x2)
+        p = self.dropout.p if self.training else 0.0
+        y = ffn_forward(x2, self.w_1.weight.squeeze(-1), self.w_1.bias, self.w_2.weight.squeeze(-1),
+                        self.w_2.bias, self.layer_norm.weight, self.layer_norm.bias, p, self.layer_norm.eps)
         if CHECK_NAN:
             assert not torch.any(torch.isnan(y)), "FFN output"
         return y.reshape(shape)
 
 
 class _HeadParams(nn.Module):
-    """fc / feat_fc / attn_fc of one head (GATLayer.py:82-87, 121-126)."""
+    """fc / feat_fc / attn_fc of one head (GATLayer.py:82-87, 121-126).
+
+    Built exactly like the reference head (so seeded initialisation matches); a
+    MultiHeadLayer then moves the values into its fused tensors and ``bind``s the
+    head, which from then on owns no parameters and reads views of the fused
+    storage."""
 
     kind = None
     feat_bias = False
@@ -63,10 +68,27 @@ class _HeadParams(nn.Module):
         self.fc = nn.Linear(in_dim, out_dim, bias=False)
         self.feat_fc = nn.Linear(feat_embed_size, out_dim, bias=self.feat_bias)
         self.attn_fc = nn.Linear(3 * out_dim, 1, bias=False)
+        self._index = 0
+
+    def bind(self, parent, index):
+        del self.fc, self.feat_fc, self.attn_fc
+        # plain (non-submodule) back-reference: survives deepcopy/pickle as a cycle
+        object.__setattr__(self, "_parent_layer", parent)
+        self._index = index
+
+    def params(self):
+        """(fc_weight [D,in], attn_weight [1,3D], feat_weight [1,D,F], feat_bias [1,D]|None)."""
+        p = self.__dict__.get("_parent_layer")
+        if p is None:
+            fb = self.feat_fc.bias.unsqueeze(0) if self.feat_fc.bias is not None else None
+            return self.fc.weight, self.attn_fc.weight, self.feat_fc.weight.unsqueeze(0), fb
+        k, D = self._index, p.head_dim
+        fb = p.feat_bias[k:k + 1] if p.feat_bias is not None else None
+        return p.fc_weight[k * D:(k + 1) * D], p.attn_weight[k:k + 1], p.feat_weight[k:k + 1], fb
 
     def forward(self, g, h):
         """One head on its own (reference signature): returns [n_dst, out_dim]."""
-        return fused_heads(g, h, [self], self.kind, origin=None, dropout=None)
+        return fused_heads(g, h, self.params(), self.kind, origin=None, dropout=None)
 
 
 class WSGATLayer(_HeadParams):
@@ -81,19 +103,6 @@ class SWGATLayer(_HeadParams):
 
     kind = "S2W"
     feat_bias = True
-
-
-def head_tensors(heads):
-    """Concatenate per-head parameters (autograd-tracked) for the fused pass."""
-    D = heads[0].fc.out_features
-    W = torch.cat([hd.fc.weight for hd in heads], 0)                     # [H*D, in]
-    attn = torch.cat([hd.attn_fc.weight for hd in heads], 0)             # [H, 3D]
-    a1 = attn[:, :D]                                                     # z_src weights
-    a3 = attn[:, 2 * D:]                                                 # feat weights
-    wf = torch.stack([hd.feat_fc.weight for hd in heads], 0)             # [H, D, F]
-    bf = (torch.stack([hd.feat_fc.bias for hd in heads], 0)
-          if heads[0].feat_fc.bias is not None else None)                # [H, D]
-    return W, a1, a3, wf, bf
 
 
 def edge_tau(g, rel, a3, wf, bf):
@@ -124,15 +133,19 @@ def edge_tau(g, rel, a3, wf, bf):
     return tau, HSG_TAU_PER_EDGE
 
 
-def fused_heads(g, h, heads, kind, origin=None, dropout=None):
+def fused_heads(g, h, params, kind, origin=None, dropout=None):
     """All heads of one layer application in one pass (+ ELU/residual if origin).
 
+    ``params``: a MultiHeadLayer (fused tensors) or a tuple (fc_weight [H*D, in],
+    attn_weight [H, 3D], feat_weight [H, D, F], feat_bias [H, D] | None).
     ``dropout``: the MultiHeadLayer's nn.Dropout, applied to ``h`` with an
     independent mask per head in training mode (GATStackLayer.py:56)."""
     rel = g.relation(kind)
-    H = len(heads)
-    D = heads[0].fc.out_features
-    W, a1, a3, wf, bf = head_tensors(heads)
+    W, attn, wf, bf = params.fused_params() if hasattr(params, "fused_params") else params
+    H = attn.shape[0]
+    D = W.shape[0] // H
+    a1 = attn[:, :D]                                                     # z_src weights
+    a3 = attn[:, 2 * D:]                                                 # feat weights (z_dst part unused)
     if h.shape[0] != rel.n_src:
         raise ValueError(f"{kind}: input has {h.shape[0]} rows, graph has {rel.n_src} source nodes")
     if dropout is not None and dropout.training and dropout.p > 0:

@@ -21,6 +21,7 @@
 #ifndef HSG_H_
 #define HSG_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -91,6 +92,45 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
  * (GATLayer.py:91-92 / 130-131); a1 = attn_fc.weight[0, :D] per head. */
 int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,
                         void *stream);
+
+/* ---- dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32) ---------------------------
+ * Replaces the torch GEMMs of the head projection fc (GATLayer.py:110 / 146) and of
+ * PositionwiseFeedForward (Conv1d k=1 = GEMM, GATLayer.py:39) plus their backward.
+ *   C[m][n] = epi( sum_k A(m,k) B(k,n) )
+ *   A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m];  B(k,n) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n]
+ * epi: HSG_EPI_STORE    v (+bias[n]) then relu if `relu`
+ *      HSG_EPI_RELU_BWD v * (aux[m][n] > 0)
+ *      HSG_EPI_ADD      v (+bias[n]) + aux[m][n]     (aux may alias C: accumulate)
+ * splits > 1: split-K over `splits` slices; needs hsg_gemm_workspace_floats() floats
+ * of workspace; the slices are reduced in order (deterministic).  splits == 0:
+ * choose automatically (split only when the output has too few tiles).
+ * Requires lda, ldb multiples of 4 and 16-byte aligned A, B. */
+#define HSG_EPI_STORE 0
+#define HSG_EPI_RELU_BWD 1
+#define HSG_EPI_ADD 2
+size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits);
+int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
+                 const float *B, int ldb, int b_kcontig, float *C, int ldc,
+                 const float *bias, const float *aux, int ldaux, int epi, int relu,
+                 int splits, float *workspace, void *stream);
+
+/* ---- PositionwiseFeedForward row epilogue (GATLayer.py:40-42) -------------------
+ * Forward:  s = dropout(y; p, seed, offset) + x;  out = (s-mean)*rstd*gamma + beta
+ *           (y = W2 relu(W1 x + b1) + b2 from hsg_gemm_f32; eps as nn.LayerNorm)
+ * Backward: dx = dLN/ds (residual branch), dy = dx * mask / (1-p),
+ *           dgamma_part/dbeta_part[b][d] = per-block column partials
+ *           (hsg_ln_bwd_blocks(n) rows; sum them in order).
+ * Dropout masks are a stateless hash of (*seed, offset, element index): *seed is
+ * read from device memory (advance it between graph replays), offset is a
+ * per-call constant; forward and backward with equal (seed, offset) agree.
+ * d <= 512; p_drop in [0, 1). */
+int hsg_ln_bwd_blocks(int n);
+int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
+               float eps, float p_drop, const int64_t *seed, uint32_t offset,
+               float *out, float *mean, float *rstd, void *stream);
+int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+               const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
+               float *dy, float *dx, float *dgamma_part, float *dbeta_part, void *stream);
 
 /* Library build identification (ABI version, gfx target). */
 const char *hsg_version(void);

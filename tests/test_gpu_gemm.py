@@ -1,0 +1,95 @@
+"""hsg_gemm_f32 (v_mfma_f32_32x32x2_f32) against an fp64 torch reference: every
+operand layout, ragged shapes, each epilogue, split-K."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(19200 // 8, 512, 300), (1000, 300, 512), (67, 45, 33), (1120, 64, 512), (300, 512, 2400),
+          (128, 128, 32), (5, 7, 3)]
+
+
+def ref(A, B, a_t, b_t):
+    a = A.double().t() if a_t else A.double()
+    b = B.double().t() if b_t else B.double()
+    return a @ b
+
+
+def mk(rows, cols):
+    # row stride padded to a multiple of 4 when needed (16-byte aligned rows)
+    ld = (cols + 3) // 4 * 4
+    return torch.randn(rows, ld, device="cuda")[:, :cols]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("a_t,b_t", [(False, False), (False, True), (True, False), (True, True)])
+def test_layouts(M, N, K, a_t, b_t):
+    from hetersumgraph_amd.dense import gemm
+    torch.manual_seed(M + N + K)
+    A = mk(K, M) if a_t else mk(M, K)
+    B = mk(N, K) if b_t else mk(K, N)
+    C = gemm(A, B, a_t, b_t)
+    R = ref(A, B, a_t, b_t)
+    err = (C.double() - R).abs().max().item()
+    assert err <= 1e-5 * max(1.0, K ** 0.5) * 4, err
+
+
+@pytest.mark.parametrize("splits", [2, 7, 16])
+def test_split_k(splits):
+    from hetersumgraph_amd.dense import gemm
+    torch.manual_seed(splits)
+    A = torch.randn(4000, 300, device="cuda")
+    B = torch.randn(4000, 512, device="cuda")
+    C = gemm(A, B, a_t=True, splits=splits)          # dW-shaped: A^T B
+    R = A.double().t() @ B.double()
+    assert (C.double() - R).abs().max().item() < 2e-3
+    C2 = gemm(A, B, a_t=True, splits=splits)
+    assert torch.equal(C, C2)                          # deterministic
+
+
+def test_epilogues():
+    from hetersumgraph_amd.dense import gemm
+    torch.manual_seed(0)
+    X = torch.randn(777, 300, device="cuda")
+    W = torch.randn(512, 300, device="cuda")
+    b = torch.randn(512, device="cuda")
+    H = gemm(X, W, b_t=True, bias=b, relu=True)
+    Hr = torch.relu(X.double() @ W.double().t() + b.double())
+    assert (H.double() - Hr).abs().max().item() < 1e-4
+    G = torch.randn(777, 300, device="cuda")
+    W2 = torch.randn(300, 512, device="cuda")
+    dH = gemm(G, W2, relu_mask=H)
+    dHr = (G.double() @ W2.double()) * (Hr > 0)
+    assert (dH.double() - dHr).abs().max().item() < 1e-4
+    acc = torch.randn(777, 300, device="cuda")
+    acc0 = acc.clone()
+    gemm(dH, W, out=acc, add=acc)
+    accr = acc0.double() + dH.double() @ W.double()
+    assert (acc.double() - accr).abs().max().item() < 2e-3
+
+
+def test_speed_smoke():
+    """Reports TFLOP/s of the dominant FFN GEMM shape (no assertion on speed)."""
+    from hetersumgraph_amd.dense import gemm
+    X = torch.randn(19200, 300, device="cuda")
+    W = torch.randn(512, 300, device="cuda")
+    b = torch.randn(512, device="cuda")
+    for _ in range(3):
+        gemm(X, W, b_t=True, bias=b, relu=True)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        gemm(X, W, b_t=True, bias=b, relu=True)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 20
+    tf = 2 * 19200 * 300 * 512 / (ms * 1e-3) / 1e12
+    print(f"ffn gemm1 19200x512x300: {ms * 1e3:.1f} us, {tf:.1f} TFLOP/s")
+    e0.record()
+    for _ in range(20):
+        torch.nn.functional.linear(X, W, b)
+    e1.record()
+    torch.cuda.synchronize()
+    ms2 = e0.elapsed_time(e1) / 20
+    print(f"torch linear same shape: {ms2 * 1e3:.1f} us, {2 * 19200 * 300 * 512 / (ms2 * 1e-3) / 1e12:.1f} TFLOP/s")
