@@ -21,7 +21,9 @@ HSG_TAU_PER_EDGE = 1
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
            "hsg_attn_src_logits", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats",
-           "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd")
+           "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
+           "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
+           "hsg_hproj_dw_chunks", "hsg_hproj_dw")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -54,10 +56,18 @@ _SIGS = {
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P],
     "hsg_gemm_workspace_floats": [_I, _I, _I, _I],
     "hsg_ln_bwd_blocks": [_I],
+    "hsg_dropmask_words": [_I, _I, _I],
+    "hsg_dropmask_scale": [_F],
+    "hsg_dropmask": [_I, _I, _I, _F, _P, ctypes.c_uint32, _P, _P],
+    "hsg_hproj_fwd": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
+    "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
+    "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
+    "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _P],
     "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P, _P],
 }
-_RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_gemm_workspace_floats": ctypes.c_size_t}
+_RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_gemm_workspace_floats": ctypes.c_size_t,
+            "hsg_dropmask_scale": ctypes.c_float}
 
 
 def load():

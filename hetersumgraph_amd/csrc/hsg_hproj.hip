@@ -1,0 +1,566 @@
+// hsg_hproj.hip -- head projection with per-head input dropout, for gfx950.
+//
+// Reference (module/GATStackLayer.py:56, GATLayer.py:110/146): in training, every
+// head k sees its own dropout of the layer input,  z_k = fc_k(dropout(h)).  Done
+// literally that is H copies of the [n, in] input (PyTorch: 8 x 19,200 x 300 for
+// W2S) and a batched GEMM.  Here:
+//   hsg_dropmask   writes the H keep-masks once as bits, 32 rows per word, words
+//                  contiguous along the input column:
+//                    bits[(k*NWI + i/32)*LDC + c] bit (i%32) = keep(i, k, c)
+//                  NWI = ceil(n/32), LDC = in rounded up to 4 (0.7 MB for W2S)
+//   hsg_hproj_fwd  Z[i, kD+d] = s * sum_c bit(i,k,c) X[i,c] W[kD+d, c]
+//   hsg_hproj_dx   dX[i, c]   = s * sum_k bit(i,k,c) sum_d dZ[i,kD+d] W[kD+d, c]
+//   hsg_hproj_dw   dW[kD+d,c] = s * sum_i dZ[i,kD+d] bit(i,k,c) X[i,c]
+// All three are f32 MFMA kernels.  The mask changes with the head, so a head's
+// outputs form their own tile ("slot" = up to 16 (fwd/dw) or DP (dx) outputs of
+// one head); the mask is applied to the MFMA operand that carries (i, c) (fwd,
+// dw) or to the per-head product before it is accumulated (dx).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hsg.h"
+#include "hsg_rng.h"
+
+namespace {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+// 16-bit uniforms, two heads per hash: drop probability resolution 2^-16.
+__device__ __forceinline__ uint32_t thr16(float p) {
+    const float t = p * 65536.f;
+    return t >= 65535.f ? 65535u : (uint32_t)t;
+}
+
+__host__ __device__ __forceinline__ int mask_ldc(int in) { return (in + 3) & ~3; }
+
+// Buffer loads: an offset past the descriptor's byte count reads 0, so edge
+// handling is a select on the OFFSET (kOOB) and the load itself is unconditional
+// -- a select on a loaded value lets the compiler sink the load into a branch and
+// serialise it.  Descriptors are built from kernel arguments (wave-uniform).
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+constexpr uint32_t kOOB = 0x80000000u;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0));
+}
+__device__ __forceinline__ uint32_t bldu(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
+__device__ __forceinline__ u32x4v bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+}
+
+// one thread = (head pair, 32-row word, column c); c fastest so stores coalesce.
+// Columns in [in, LDC) get zero words.
+__global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p, const int64_t *seedp,
+                                                  uint32_t offset, uint32_t *__restrict__ bits) {
+    const int NWI = (n + 31) / 32;
+    const int HP = (H + 1) / 2;
+    const int LDC = mask_ldc(in);
+    const uint64_t key64 = hsg_mix64((uint64_t)seedp[0] * 0x9E3779B97F4A7C15ull +
+                                     (uint64_t)offset * 0xD1B54A32D192ED03ull);
+    const uint32_t key = (uint32_t)key64 ^ (uint32_t)(key64 >> 32);
+    const uint32_t thr = thr16(p);
+    const long total = (long)HP * NWI * LDC;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        const int c = (int)(t % LDC);
+        const long r = t / LDC;
+        const int iw = (int)(r % NWI);
+        const int kp = (int)(r / NWI);
+        uint32_t b0 = 0, b1 = 0;
+        if (c < in) {
+#pragma unroll 8
+            for (int j = 0; j < 32; ++j) {
+                const int i = iw * 32 + j;
+                if (i >= n) break;
+                const uint32_t h = lowbias32(key ^ ((uint32_t)(((long)i * in + c) * HP + kp) * 0x9E3779B1u));
+                b0 |= (uint32_t)((h & 0xFFFFu) >= thr) << j;
+                b1 |= (uint32_t)((h >> 16) >= thr) << j;
+            }
+        }
+        const int k0 = 2 * kp;
+        bits[((long)k0 * NWI + iw) * LDC + c] = b0;
+        if (k0 + 1 < H) bits[((long)(k0 + 1) * NWI + iw) * LDC + c] = b1;
+    }
+}
+
+// ---------------------------------------------------------------- forward ----
+// v_mfma_f32_16x16x4_f32, no LDS.  One wave = one 16-row tile x SG slots (slot =
+// 16 outputs [d0, d0+16) of head k, zero-padded past D).  The reduction index c
+// is assigned so that every operand load is a 16-byte vector: in the 16-column
+// chunk at c0, lane (li = l&15, lk = l>>4) holds columns c0+4lk .. c0+4lk+3 and
+// feeds them to 4 consecutive MFMAs:
+//   A[i = li][kk] = bit(i, k, c) X[i0+li, c]      (X float4, mask uint4)
+//   B[kk][j = li] = W[kD + d0 + li, c]             (W row float4)
+// Loads for chunk t+1 are issued before the MFMAs of chunk t.  All loads are
+// unconditional from clamped addresses followed by a select, so the compiler can
+// keep them in flight together.  VEC: in % 4 == 0 and 16-byte aligned rows.
+template <int SG, bool VEC>
+__global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, const float *__restrict__ X,
+                                                   int ldx, const float *__restrict__ W,
+                                                   const uint32_t *__restrict__ bits, float scale,
+                                                   float *__restrict__ Z, int ldz) {
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int SPH = (D + 15) / 16, NS = H * SPH, NG = (NS + SG - 1) / SG;
+    const int lane = threadIdx.x & 63;
+    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int rt = task / NG, gq = task - rt * NG;
+    const int i0 = rt * 16;
+    if (i0 >= n) return;                          // whole wave: no barriers in this kernel
+    const int li = lane & 15, lk = lane >> 4;
+    const int i = i0 + li;
+    const int ibit = i & 31;
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rW = rsrc(W, (long)H * D * in * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const uint32_t xbase = i < n ? (uint32_t)i * ldx * 4 : kOOB;
+    uint32_t wbase[SG], mbase[SG];
+#pragma unroll
+    for (int q = 0; q < SG; ++q) {
+        const int slot = gq * SG + q;
+        const int k = min(slot, NS - 1) / SPH;
+        const int j = (min(slot, NS - 1) - k * SPH) * 16 + li;
+        wbase[q] = (slot < NS && j < D) ? (uint32_t)(k * D + j) * in * 4 : kOOB;
+        mbase[q] = (uint32_t)((k * NWI + i0 / 32) * LDC) * 4;
+    }
+    // operand quads for the 16-column chunk whose lane columns start at c
+    auto load4 = [&](__amdgpu_buffer_rsrc_t r, uint32_t base, int c) -> f32x4v {
+        if (VEC) {
+            const u32x4v v = bld4(r, (c < in && base != kOOB) ? base + c * 4 : kOOB);
+            return f32x4v{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+        }
+        f32x4v v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bld(r, (c + e < in && base != kOOB) ? base + (c + e) * 4 : kOOB);
+        return v;
+    };
+    auto loadm = [&](uint32_t base, int c) -> u32x4v { return bld4(rM, c < LDC ? base + c * 4 : kOOB); };
+    f32x4v acc[SG];
+#pragma unroll
+    for (int q = 0; q < SG; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    int c = 4 * lk;
+    f32x4v xv = load4(rX, xbase, c);
+    f32x4v wv[SG];
+    u32x4v mv[SG];
+#pragma unroll
+    for (int q = 0; q < SG; ++q) {
+        wv[q] = load4(rW, wbase[q], c);
+        mv[q] = loadm(mbase[q], c);
+    }
+    for (int c0 = 0; c0 < in; c0 += 16) {
+        const int cn = c + 16;
+        const f32x4v xn = load4(rX, xbase, cn);
+        f32x4v wn[SG];
+        u32x4v mn[SG];
+#pragma unroll
+        for (int q = 0; q < SG; ++q) {
+            wn[q] = load4(rW, wbase[q], cn);
+            mn[q] = loadm(mbase[q], cn);
+        }
+#pragma unroll
+        for (int q = 0; q < SG; ++q) {               // slots past NS carry zero W
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].x >> ibit) & 1u) ? xv[0] : 0.f, wv[q][0], acc[q],
+                                                          0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].y >> ibit) & 1u) ? xv[1] : 0.f, wv[q][1], acc[q],
+                                                          0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].z >> ibit) & 1u) ? xv[2] : 0.f, wv[q][2], acc[q],
+                                                          0, 0, 0);
+            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].w >> ibit) & 1u) ? xv[3] : 0.f, wv[q][3], acc[q],
+                                                          0, 0, 0);
+        }
+        xv = xn;
+#pragma unroll
+        for (int q = 0; q < SG; ++q) { wv[q] = wn[q]; mv[q] = mn[q]; }
+        c = cn;
+    }
+    // D layout: col = lane & 15 (slot output j), row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int q = 0; q < SG; ++q) {
+        const int slot = gq * SG + q;
+        if (slot >= NS) continue;
+        const int k = slot / SPH;
+        const int j = (slot - k * SPH) * 16 + li;
+        if (j >= D) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gi = i0 + lk * 4 + r;
+            if (gi < n) Z[(long)gi * ldz + k * D + j] = acc[q][r] * scale;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ dX ----
+// v_mfma_f32_16x16x4_f32, no LDS.  One wave = 16 rows x (16*CT) input columns.
+// Per head k the K = D product  t = dZ[i0.., kD..kD+D) W[kD.., c..]  runs on MFMA
+// (lane (li, lk) supplies d = 4s + lk), then is added to the running total under
+// the head's mask:  tot += bit(i, k, c) ? t : 0.  HF heads are in flight at once
+// (independent accumulator chains); the loads of step s+1 are issued before the
+// MFMAs of step s.  Rows/columns past the edge read clamped addresses and are
+// never stored.
+template <int CT, int HF>
+__global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                  int ldz, const float *__restrict__ W,
+                                                  const uint32_t *__restrict__ bits, float scale,
+                                                  float *__restrict__ dX, int ldx) {
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int nct = (in + 16 * CT - 1) / (16 * CT);
+    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int rt = task / nct, ctile = task - rt * nct;
+    const int i0 = rt * 16;
+    if (i0 >= n) return;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int cbase = ctile * 16 * CT;
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rW = rsrc(W, (long)H * D * in * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const int zi = i0 + li;
+    const uint32_t zbase = zi < n ? (uint32_t)zi * ldz * 4 : kOOB;
+    int cb[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) cb[t] = cbase + 16 * t + li;
+    const int DS = (D + 3) / 4;
+    f32x4v tot[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) tot[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < H; kb += HF) {
+        // mask words of this head group (used after the products)
+        uint32_t mw[HF][CT];
+#pragma unroll
+        for (int f = 0; f < HF; ++f) {
+            const uint32_t mrow = (uint32_t)(((kb + f) * NWI + i0 / 32) * LDC) * 4;
+#pragma unroll
+            for (int t = 0; t < CT; ++t) mw[f][t] = bldu(rM, (kb + f < H && cb[t] < in) ? mrow + cb[t] * 4 : kOOB);
+        }
+        f32x4v acc[HF][CT];
+#pragma unroll
+        for (int f = 0; f < HF; ++f)
+#pragma unroll
+            for (int t = 0; t < CT; ++t) acc[f][t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        float av[HF], bv[HF][CT];
+        auto fetch = [&](int s, float (&a)[HF], float (&b)[HF][CT]) {
+            const int d = 4 * s + lk;
+#pragma unroll
+            for (int f = 0; f < HF; ++f) {
+                const int k = kb + f;
+                const bool ok = d < D && k < H;
+                const int hd = k * D + d;
+                a[f] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
+#pragma unroll
+                for (int t = 0; t < CT; ++t)
+                    b[f][t] = bld(rW, (ok && cb[t] < in) ? (uint32_t)(hd * in + cb[t]) * 4 : kOOB);
+            }
+        };
+        fetch(0, av, bv);
+        for (int s = 0; s < DS; ++s) {
+            float an[HF], bn[HF][CT];
+            fetch(s + 1, an, bn);                    // past D: reads 0, never used
+#pragma unroll
+            for (int f = 0; f < HF; ++f)
+#pragma unroll
+                for (int t = 0; t < CT; ++t)
+                    acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[f], bv[f][t], acc[f][t], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < HF; ++f) {
+                av[f] = an[f];
+#pragma unroll
+                for (int t = 0; t < CT; ++t) bv[f][t] = bn[f][t];
+            }
+        }
+        // C layout: col = li (input column), row = 4 lk + r
+        const int sh = (i0 & 31) + 4 * lk;
+#pragma unroll
+        for (int f = 0; f < HF; ++f)
+#pragma unroll
+            for (int t = 0; t < CT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tot[t][r] += ((mw[f][t] >> (sh + r)) & 1u) ? acc[f][t][r] : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int gc = cbase + 16 * t + li;
+        if (gc >= in) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gi = i0 + 4 * lk + r;
+            if (gi < n) dX[(long)gi * ldx + gc] = tot[t][r] * scale;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ dW ----
+// v_mfma_f32_16x16x4_f32, reduction over rows.  Block = 64 input columns (wave w:
+// columns 16w..16w+15) x 8 slots (slot = 16 outputs of one head) x one chunk of
+// rows.  Per 32-row step, staged in LDS:
+//   Xs[32][80]       X[r, c0 .. c0+63]
+//   Zs[32][8*16+16]  dZ of the 8 slots, zero-padded to 16 per slot
+//   Ms[8][64]        the slots' mask words for these 32 rows
+// and MFMA A[c][r] = bit X[r, c], B[r][j] = dZ[r, kD+d0+j].  The next step's
+// global loads are issued before this step's MFMAs.  Each block writes its own
+// partial slab part[chunk][H*D][in]; k_sum_parts adds the chunks in order.
+constexpr int kDwSlots = 8;
+constexpr int kDwXs = 80;                         // row stride: 4 rows hit 4 disjoint bank quarters
+constexpr int kDwZs = kDwSlots * 16 + 16;
+
+struct DwGeom {
+    int ctiles, sgroups, chunks, rows;            // rows per chunk (multiple of 32)
+};
+
+DwGeom dw_geom(int n, int in, int H, int D) {
+    DwGeom g;
+    const int ns = H * ((D + 15) / 16);
+    g.ctiles = (in + 63) / 64;
+    g.sgroups = (ns + kDwSlots - 1) / kDwSlots;
+    const int steps = (n + 31) / 32 > 0 ? (n + 31) / 32 : 1;
+    int want = 512 / (g.ctiles * g.sgroups);
+    if (want < 1) want = 1;
+    if (want > steps) want = steps;
+    const int per = (steps + want - 1) / want;    // 32-row steps per chunk
+    g.rows = per * 32;
+    g.chunks = (steps + per - 1) / per;
+    return g;
+}
+
+__global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, int rows_per_chunk,
+                                                  const float *__restrict__ dZ, int ldz,
+                                                  const float *__restrict__ X, int ldx,
+                                                  const uint32_t *__restrict__ bits, float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float Xs[32][kDwXs];
+    __shared__ __attribute__((aligned(16))) float Zs[32][kDwZs];
+    __shared__ uint32_t Ms[kDwSlots][64];
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int SPH = (D + 15) / 16, NS = H * SPH;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int c0 = blockIdx.x * 64;
+    const int s0 = blockIdx.y * kDwSlots;
+    const int rb = blockIdx.z * rows_per_chunk;
+    const int rend = min(rb + rows_per_chunk, n);
+    // per-thread staging: X 2 x 4 columns, dZ 16 values, 2 mask words.  The
+    // column parts of every offset are fixed per thread; buffer loads with kOOB
+    // offsets for the edges keep all 26 loads unconditional and in flight together.
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    float xr[8], zr[16];
+    uint32_t mr[2];
+    int xcol[2], zcol[16];
+    uint32_t moff[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) xcol[u] = c0 + ((tid + 256 * u) & 15) * 4;   // 32 rows x 16 column quads
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int a = (tid + 256 * u) & 127;          // 32 rows x 128 slot columns
+        const int v = s0 + (a >> 4);
+        const int k = min(v, NS - 1) / SPH, d = (min(v, NS - 1) - k * SPH) * 16 + (a & 15);
+        zcol[u] = (v < NS && d < D) ? k * D + d : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int e = tid + 256 * u;                  // 8 slots x 64 columns
+        const int v = s0 + (e >> 6), gc = c0 + (e & 63);
+        moff[u] = (v < NS && gc < LDC) ? (uint32_t)((v / SPH) * NWI * LDC + gc) * 4 : kOOB;
+    }
+    auto fetch = [&](int r0) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int gi = r0 + ((tid + 256 * u) >> 4);
+            const bool rok = gi < rend;
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                xr[u * 4 + v] = bld(rX, (rok && xcol[u] + v < in) ? (uint32_t)(gi * ldx + xcol[u] + v) * 4 : kOOB);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int gi = r0 + ((tid + 256 * u) >> 7);
+            zr[u] = bld(rZ, (gi < rend && zcol[u] >= 0) ? (uint32_t)(gi * ldz + zcol[u]) * 4 : kOOB);
+        }
+        const uint32_t roff = (uint32_t)(r0 / 32) * LDC * 4;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) mr[u] = bldu(rM, moff[u] != kOOB ? moff[u] + roff : kOOB);
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u;
+            const int rr = e >> 4, cq = (e & 15) * 4;
+            *reinterpret_cast<f32x4v *>(&Xs[rr][cq]) = f32x4v{xr[u * 4], xr[u * 4 + 1], xr[u * 4 + 2], xr[u * 4 + 3]};
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int e = tid + 256 * u;
+            Zs[e >> 7][e & 127] = zr[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int e = tid + 256 * u;
+            Ms[e >> 6][e & 63] = mr[u];
+        }
+    };
+    f32x4v acc[kDwSlots];
+#pragma unroll
+    for (int q = 0; q < kDwSlots; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int col = wv * 16 + li;
+    if (rb < rend) fetch(rb);
+    for (int r0 = rb; r0 < rend; r0 += 32) {
+        __syncthreads();
+        stash();
+        __syncthreads();
+        if (r0 + 32 < rend) fetch(r0 + 32);
+#pragma unroll
+        for (int s4 = 0; s4 < 32; s4 += 4) {
+            const int rr = s4 + lk;
+            const float xv = Xs[rr][col];
+            // slots past NS were staged as zeros: no branch around the MFMAs (a
+            // conditional MFMA makes the compiler shuffle accumulators)
+#pragma unroll
+            for (int q = 0; q < kDwSlots; ++q) {
+                const float a = ((Ms[q][col] >> rr) & 1u) ? xv : 0.f;
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Zs[rr][q * 16 + li], acc[q], 0, 0, 0);
+            }
+        }
+    }
+    // D: col = lane & 15 -> slot output j, row = (lane >> 4) * 4 + r -> input column
+    const long base = (long)blockIdx.z * H * D * in;
+#pragma unroll
+    for (int q = 0; q < kDwSlots; ++q) {
+        const int v = s0 + q;
+        if (v >= NS) continue;
+        const int k = v / SPH, j = (v - k * SPH) * 16 + li;
+        if (j >= D) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gc = c0 + wv * 16 + lk * 4 + r;
+            if (gc < in) part[base + (long)(k * D + j) * in + gc] = acc[q][r];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_parts(long total, int chunks, float scale, const float *__restrict__ part,
+                                                   float *__restrict__ out) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        float s = 0.f;
+#pragma unroll 8
+        for (int z = 0; z < chunks; ++z) s += part[(long)z * total + e];
+        out[e] = s * scale;
+    }
+}
+
+int status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+float drop_scale(float p) {
+    const float t = p * 65536.f;
+    const float thr = (float)(uint32_t)(t >= 65535.f ? 65535.f : t);
+    return 1.f / (1.f - thr / 65536.f);
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// buffer descriptors address < 2 GiB per operand (kOOB is the first bad offset)
+bool fits_buffers(int n, int in, int H, int D, int ld_rows) {
+    const long lim = (long)kOOB;
+    return (long)n * ld_rows * 4 < lim && (long)H * D * in * 4 < lim &&
+           (long)H * ((n + 31) / 32) * mask_ldc(in) * 4 < lim;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsg_dropmask_words(int n, int in, int H) { return H * ((n + 31) / 32) * mask_ldc(in); }
+
+float hsg_dropmask_scale(float p) { return drop_scale(p); }
+
+int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t offset, uint32_t *bits,
+                 void *stream) {
+    if (n < 0 || in < 1 || H < 1 || p < 0.f || p >= 1.f || !seed || !bits) return HSG_EINVAL;
+    if ((long)n * in * ((H + 1) / 2) >= (1L << 32)) return HSG_EINVAL;   // 32-bit hash counter
+    if (n == 0) return 0;
+    const long total = (long)((H + 1) / 2) * ((n + 31) / 32) * mask_ldc(in);
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_dropmask, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, in, H, p, seed, offset,
+                       bits);
+    return status();
+}
+
+int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W, const uint32_t *bits,
+                  float p, float *Z, int ldz, void *stream) {
+    if (n < 0 || in < 1 || H < 1 || D < 1 || ldx < in || !fits_buffers(n, in, H, D, ldx)) return HSG_EINVAL;
+    if (n == 0) return 0;
+    constexpr int SG = 4;
+    const int ns = H * ((D + 15) / 16);
+    const long tasks = (long)((n + 15) / 16) * ((ns + SG - 1) / SG);
+    const bool vec = in % 4 == 0 && ldx % 4 == 0 && aligned16(X) && aligned16(W);
+    const dim3 grid((unsigned)((tasks + 3) / 4));
+    if (vec)
+        hipLaunchKernelGGL((k_hproj_fwd<SG, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx, W,
+                           bits, drop_scale(p), Z, ldz);
+    else
+        hipLaunchKernelGGL((k_hproj_fwd<SG, false>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx,
+                           W, bits, drop_scale(p), Z, ldz);
+    return status();
+}
+
+int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W, const uint32_t *bits,
+                 float p, float *dX, int ldx, void *stream) {
+    if (n < 0 || in < 1 || H < 1 || D < 1 || ldz < H * D || !fits_buffers(n, in, H, D, ldz)) return HSG_EINVAL;
+    if (n == 0) return 0;
+    const float s = drop_scale(p);
+    hipStream_t st = (hipStream_t)stream;
+    const long rtiles = (n + 15) / 16;
+    // wide wave tiles (16 x 64) when that still gives >= 2048 waves, else 16 x 16
+    const long wide = rtiles * ((in + 63) / 64);
+    if (wide >= 2048) {
+        hipLaunchKernelGGL((k_hproj_dx<4, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D, dZ,
+                           ldz, W, bits, s, dX, ldx);
+    } else {
+        const long narrow = rtiles * ((in + 15) / 16);
+        hipLaunchKernelGGL((k_hproj_dx<1, 4>), dim3((unsigned)((narrow + 3) / 4)), dim3(256), 0, st, n, in, H, D,
+                           dZ, ldz, W, bits, s, dX, ldx);
+    }
+    return status();
+}
+
+int hsg_hproj_dw_chunks(int n, int in, int H, int D) {
+    if (n < 0 || in < 1 || H < 1 || D < 1) return 0;
+    return dw_geom(n, in, H, D).chunks;
+}
+
+int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
+                 const uint32_t *bits, float p, float *part, float *dW, void *stream) {
+    if (n < 0 || in < 1 || H < 1 || D < 1 || !part || !dW || ldx < in || ldz < H * D ||
+        !fits_buffers(n, in, H, D, ldx > ldz ? ldx : ldz))
+        return HSG_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    const DwGeom g = dw_geom(n, in, H, D);
+    const long total = (long)H * D * in;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_hproj_dw, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D, g.rows,
+                           dZ, ldz, X, ldx, bits, part);
+        int rc = status();
+        if (rc) return rc;
+    }
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(k_sum_parts, dim3(blocks), dim3(256), 0, st, total, n > 0 ? g.chunks : 0, drop_scale(p),
+                       part, dW);
+    return status();
+}
+
+}  // extern "C"

@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ffn import ffn_forward
+from ..hproj import head_projection_dropout
 from ..ops import LEAKY_SLOPE, gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
 from ..relation import N_BOX
 
@@ -149,9 +150,7 @@ def fused_heads(g, h, params, kind, origin=None, dropout=None):
     if h.shape[0] != rel.n_src:
         raise ValueError(f"{kind}: input has {h.shape[0]} rows, graph has {rel.n_src} source nodes")
     if dropout is not None and dropout.training and dropout.p > 0:
-        hx = F.dropout(h.unsqueeze(0).expand(H, *h.shape).contiguous(), dropout.p, True)
-        Z = torch.bmm(hx, W.view(H, D, -1).transpose(1, 2))              # [H, n, D]
-        Z = Z.transpose(0, 1).reshape(h.shape[0], H * D)
+        Z = head_projection_dropout(h, W, H, D, dropout.p)               # per-head masks, fused
     else:
         Z = F.linear(h, W)
     tau, mode = edge_tau(g, rel, a3, wf, bf)

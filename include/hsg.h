@@ -132,6 +132,33 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                float *dy, float *dx, float *dgamma_part, float *dbeta_part, void *stream);
 
+/* ---- head projection with per-head input dropout (GATStackLayer.py:56) ----------
+ * Training-mode  z_k = fc_k(dropout_k(h))  for all heads without materialising the
+ * H dropped copies of h (reference: GATLayer.py:110 / :146 apply nn.Dropout to the
+ * layer input inside each head's forward):
+ *   hsg_dropmask: keep(i, k, c) as bits, a stateless hash of (*seed, offset, i, k, c)
+ *                 with 16-bit resolution in p; layout, NWI = ceil(n/32),
+ *                 LDC = in rounded up to 4:
+ *                   bits[(k*NWI + i/32)*LDC + c] bit (i%32)
+ *                 hsg_dropmask_words(n,in,H) uint32 words.
+ *   hsg_hproj_fwd: Z[i, kD+d]  = s * sum_c bit X[i,c] W[kD+d, c]
+ *   hsg_hproj_dx:  dX[i, c]    = s * sum_k bit sum_d dZ[i, kD+d] W[kD+d, c]
+ *   hsg_hproj_dw:  dW[kD+d, c] = s * sum_i dZ[i, kD+d] bit X[i,c]
+ *                  (part: hsg_hproj_dw_chunks(n,in,H,D) * H*D*in floats of workspace)
+ * W is the fused fc weight [H*D][in] (row-major); s = 1/(1-p_eff) =
+ * hsg_dropmask_scale(p).  Any H, D >= 1. */
+int hsg_dropmask_words(int n, int in, int H);
+float hsg_dropmask_scale(float p);
+int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t offset, uint32_t *bits,
+                 void *stream);
+int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
+                  const uint32_t *bits, float p, float *Z, int ldz, void *stream);
+int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
+                 const uint32_t *bits, float p, float *dX, int ldx, void *stream);
+int hsg_hproj_dw_chunks(int n, int in, int H, int D);
+int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
+                 const uint32_t *bits, float p, float *part, float *dW, void *stream);
+
 /* Library build identification (ABI version, gfx target). */
 const char *hsg_version(void);
 

@@ -1,0 +1,60 @@
+"""Per-head-dropout head projection kernels vs a PyTorch fp64 reference that uses
+the same keep-mask bits (fwd, dX, dW), plus mask statistics."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def unpack(bits, n):
+    """[H, NWI, in] int32 words (32 rows per word) -> bool [H, n, in]."""
+    H, NWI, d_in = bits.shape
+    b = bits.to(torch.int64) & 0xFFFFFFFF
+    j = torch.arange(32, device=bits.device)
+    m = ((b.unsqueeze(-1) >> j) & 1).bool()                   # [H, NWI, in, 32]
+    return m.permute(0, 1, 3, 2).reshape(H, NWI * 32, d_in)[:, :n]
+
+
+@pytest.mark.parametrize("n,d_in,H,D", [(19200 // 4, 300, 8, 8), (1120, 64, 6, 50), (333, 70, 3, 16),
+                                         (65, 33, 1, 64), (200, 40, 3, 5), (130, 50, 2, 75),
+                                         (97, 300, 16, 25)])
+def test_head_projection_matches_masked_reference(n, d_in, H, D):
+    from hetersumgraph_amd import _lib, rng
+    from hetersumgraph_amd.hproj import _HeadProj
+    p = 0.1
+    torch.manual_seed(n)
+    X = torch.randn(n, d_in, device="cuda", requires_grad=True)
+    W = (torch.randn(H * D, d_in, device="cuda") / d_in ** 0.5).requires_grad_()
+    r = rng.get("cuda")
+    off0 = r.offset
+    Z = _HeadProj.apply(X, W, H, D, p)
+    R = torch.randn_like(Z)
+    (Z * R).sum().backward()
+    # regenerate the same bits: same seed, same offset
+    r.offset = off0
+    from hetersumgraph_amd.hproj import dropmask_bits
+    bits = dropmask_bits(X.detach(), H, p)
+    keep = unpack(bits, n).double()                            # [H, n, d_in]
+    scale = 1.0 / (1.0 - float(int(p * 65536)) / 65536)
+    rate = 1 - keep.mean().item()
+    assert abs(rate - p) < 0.01 + 3 / (n * d_in * H) ** 0.5, rate
+    Xd = X.detach().double().requires_grad_()
+    Wd = W.detach().double().requires_grad_()
+    Zr = torch.einsum("kic,kdc->ikd", keep * Xd.unsqueeze(0) * scale, Wd.view(H, D, d_in)).reshape(n, H * D)
+    (Zr * R.double()).sum().backward()
+    assert (Z.detach().double() - Zr.detach()).abs().max().item() < 1e-4
+    assert (X.grad.double() - Xd.grad).abs().max().item() < 1e-4 * max(1, Xd.grad.abs().max().item())
+    assert (W.grad.double() - Wd.grad).abs().max().item() < 1e-4 * max(1, Wd.grad.abs().max().item())
+
+
+def test_masks_independent_across_heads_and_calls():
+    from hetersumgraph_amd.hproj import dropmask_bits
+    X = torch.randn(4096, 300, device="cuda")
+    a = unpack(dropmask_bits(X, 8, 0.1), 4096).float()
+    b = unpack(dropmask_bits(X, 8, 0.1), 4096).float()
+    # heads differ from each other and calls differ from each other
+    assert (a[0] != a[1]).float().mean().item() > 0.1
+    assert (a != b).float().mean().item() > 0.1
+    # pairwise independence: P(keep_k and keep_j) ~ (1-p)^2
+    both = (a[0] * a[1]).mean().item()
+    assert abs(both - 0.81) < 0.01
