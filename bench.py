@@ -203,37 +203,28 @@ def main():
     Xs = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen).requires_grad_()   # encoder output
     R = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen)
     params = [p for p in stack.parameters() if p.requires_grad]
-    flat = None
-    if world > 1:
-        import torch.distributed as dist
-        flat = torch.zeros(sum(p.numel() for p in params), device=dev)
+
+    from hetersumgraph_amd import rng as hsg_rng
 
     def step():
+        hsg_rng.advance_all()          # fresh dropout masks every step (device-side: replays too)
         s = stack(G, Xw, Xs)
         (s * R).sum().backward()
 
     def allreduce():
+        # data-parallel gradient exchange: one flat bucket, one RCCL all-reduce (mean)
         import torch.distributed as dist
-        torch._utils._flatten_dense_tensors  # noqa: B018
-        off = 0
-        for p in params:
-            n = p.numel()
-            flat[off:off + n].copy_(p.grad.view(-1))
-            off += n
-        dist.all_reduce(flat)
-        flat.div_(world)
-        off = 0
-        for p in params:
-            n = p.numel()
-            p.grad.view(-1).copy_(flat[off:off + n])
-            off += n
+        grads = [p.grad for p in params]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.AVG)
+        torch._foreach_copy_(grads, [t.view_as(g) for t, g in
+                                     zip(torch.split(flat, [g.numel() for g in grads]), grads)])
 
     def zero():
+        # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
         for p in params:
-            if p.grad is not None:
-                p.grad.zero_()
-        if Xs.grad is not None:
-            Xs.grad.zero_()
+            p.grad = None
+        Xs.grad = None
 
     # eager warm-up (builds relation caches, allocator pools)
     for _ in range(max(args.warmup, 2)):
@@ -265,8 +256,9 @@ def main():
             use_graph = False
 
     def run_one():
+        # replay == zero_grad(set_to_none) + forward + backward: the captured backward
+        # writes (does not accumulate into) the graph-owned .grad tensors
         if graph is not None:
-            zero()
             graph.replay()
         else:
             zero()

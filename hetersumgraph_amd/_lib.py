@@ -20,7 +20,8 @@ HSG_TAU_PER_EDGE = 1
 
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
-           "hsg_attn_src_logits", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats",
+           "hsg_gat_bwd_src_blocks", "hsg_attn_src_logits", "hsg_attn_params_fwd", "hsg_attn_params_bwd",
+           "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
            "hsg_hproj_dw_chunks", "hsg_hproj_dw")
@@ -50,11 +51,16 @@ _SIGS = {
     "hsg_gat_fwd": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gat_bwd_dst": [_RELP, _I, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gat_bwd_blocks": [_RELP],
-    "hsg_gat_bwd_src": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_src": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_src_blocks": [_RELP],
+    "hsg_attn_params_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_attn_params_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_attn_params_bwd_workspace_floats": [_I, _I],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P],
     "hsg_gemm_workspace_floats": [_I, _I, _I, _I],
+    "hsg_gemm_auto_splits": [_I, _I, _I],
     "hsg_ln_bwd_blocks": [_I],
     "hsg_dropmask_words": [_I, _I, _I],
     "hsg_dropmask_scale": [_F],
@@ -64,9 +70,10 @@ _SIGS = {
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _P],
     "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
-    "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P, _P],
+    "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
 }
 _RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_gemm_workspace_floats": ctypes.c_size_t,
+            "hsg_attn_params_bwd_workspace_floats": ctypes.c_size_t,
             "hsg_dropmask_scale": ctypes.c_float}
 
 

@@ -249,10 +249,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
                                                     const float *__restrict__ G,
                                                     const float *__restrict__ dpre,
                                                     const float *__restrict__ a1,
-                                                    float *__restrict__ dZ, float *__restrict__ dsigma) {
+                                                    const float *__restrict__ Z,
+                                                    float *__restrict__ dZ, float *__restrict__ dsigma,
+                                                    float *__restrict__ da1_part) {
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
     __shared__ int s_nb[HSG_WAVES][HSG_CHUNK];
     __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
+    __shared__ float s_da1[HSG_WAVES][64 * NF];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
@@ -262,6 +265,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
     for (int i = 0; i < NF; ++i) { int f = lane + 64 * i; fh[i] = f < HD ? f / D : 0; }
     float *sa = s_alpha[wid];
     int *sn = s_nb[wid];
+    float da1[NF];                       // this wave's share of sum_u dsigma[u,k] Z[u,k,:]
+#pragma unroll
+    for (int i = 0; i < NF; ++i) da1[i] = 0.f;
 
     for (int u = blockIdx.x * HSG_WAVES + wid; u < R.n_src; u += gridDim.x * HSG_WAVES) {
         const int beg = R.cindptr[u], end = R.cindptr[u + 1];
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
         }
         dsig = group_sum(dsig, lph);
         if (kact && l == 0) {
-            dsigma[u * H + k] = dsig;
+            if (dsigma) dsigma[u * H + k] = dsig;
             s_dsig[wid][k] = dsig;
         }
         wave_lds_sync();
@@ -305,12 +311,25 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
         for (int i = 0; i < NF; ++i) {
             const int f = lane + 64 * i;
             if (f < HD) {
+                const float ds = s_dsig[wid][fh[i]];
                 float r = acc[i];
-                if (a1) r = fmaf(s_dsig[wid][fh[i]], a1[f], r);
+                if (a1) r = fmaf(ds, a1[f], r);
                 dZ[(size_t)u * HD + f] = r;
+                if (da1_part) da1[i] = fmaf(ds, Z[(size_t)u * HD + f], da1[i]);
             }
         }
         wave_lds_sync();
+    }
+    if (da1_part) {                      // block partial of d a1 (fixed order: deterministic)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) s_da1[wid][lane + 64 * i] = da1[i];
+        __syncthreads();
+        for (int f = threadIdx.x; f < HD; f += blockDim.x) {
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < HSG_WAVES; ++w) a += s_da1[w][f];
+            da1_part[(size_t)blockIdx.x * HD + f] = a;
+        }
     }
 }
 
@@ -341,6 +360,7 @@ int grid_for(int rows, int cap) {
 }
 constexpr int kFwdGridCap = 8192;
 constexpr int kBwdDstGridCap = 1024;   // bounds the dtau partial slab
+constexpr int kBwdSrcGridCap = 2048;   // bounds the d a1 partial slab
 
 bool shape_ok(int H, int D) { return H >= 1 && H <= HSG_HMAX && D >= 1 && H * D <= 512; }
 
@@ -396,11 +416,11 @@ int ne_bucket(int ne) {
 template <int TAU>
 int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                      const float *sg, const float *tau, const float *m, const float *l, const float *G,
-                     const float *dpre, const float *a1, float *dZ, float *dsig) {
+                     const float *dpre, const float *a1, const float *Z, float *dZ, float *dsig, float *da1p) {
 #define HSG_BS(NF_)                                                                               \
     case NF_:                                                                                     \
         hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
-                           sg, tau, m, l, G, dpre, a1, dZ, dsig);                                 \
+                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                        \
         break;
     switch (nf) {
         HSG_BS(1) HSG_BS(2) HSG_BS(3) HSG_BS(4) HSG_BS(5) HSG_BS(6) HSG_BS(7) HSG_BS(8)
@@ -445,7 +465,11 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
     const RelPtrs R = rel_ptrs(rel);
     const dim3 grid(hsg_gat_bwd_blocks(rel));
     hipStream_t st = (hipStream_t)stream;
-    if (rel->n_dst == 0) return 0;
+    if (rel->n_dst == 0) {
+        if (tau_mode == HSG_TAU_TABLE && dtau_part)
+            return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
+        return 0;
+    }
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
                                                tau, h, m, l, dout, G, dpre, dtau_part);
@@ -455,21 +479,27 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
     return HSG_EINVAL;
 }
 
+int hsg_gat_bwd_src_blocks(const hsg_rel *rel) { return rel ? grid_for(rel->n_src, kBwdSrcGridCap) : 0; }
+
 int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *sigma,
                     const float *tau, const float *m, const float *l, const float *G,
-                    const float *dpre, const float *a1, float *dZ, float *dsigma, void *stream) {
-    if (!rel || !shape_ok(H, D)) return HSG_EINVAL;
-    if (rel->n_src == 0) return 0;
+                    const float *dpre, const float *a1, const float *Z, float *dZ, float *dsigma,
+                    float *da1_part, void *stream) {
+    if (!rel || !shape_ok(H, D) || (da1_part && !Z)) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
     const int nf = (H * D + 63) / 64;
-    const dim3 grid(grid_for(rel->n_src, kFwdGridCap));
+    const dim3 grid(hsg_gat_bwd_src_blocks(rel));
     hipStream_t st = (hipStream_t)stream;
+    if (rel->n_src == 0) {
+        if (da1_part) return (int)hipMemsetAsync(da1_part, 0, sizeof(float) * H * D * grid.x, st);
+        return 0;
+    }
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_src_dispatch<HSG_TAU_TABLE>(nf, grid, st, R, H, D, lanes_per_head(H), slope, sigma,
-                                               tau, m, l, G, dpre, a1, dZ, dsigma);
+                                               tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
     if (tau_mode == HSG_TAU_PER_EDGE)
         return bwd_src_dispatch<HSG_TAU_PER_EDGE>(nf, grid, st, R, H, D, lanes_per_head(H), slope,
-                                                  sigma, tau, m, l, G, dpre, a1, dZ, dsigma);
+                                                  sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
     return HSG_EINVAL;
 }
 

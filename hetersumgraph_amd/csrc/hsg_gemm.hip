@@ -25,6 +25,7 @@
 // k_splitk_reduce in split order -> deterministic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/hsg.h"
 
@@ -120,14 +121,17 @@ struct Stage {
     }
 };
 
-template <int BM, int BN, bool AK, bool BKC>
+// NBUF = 2: register-staged double buffer in LDS, one barrier per K tile.
+// NBUF = 1: one LDS buffer (half the LDS, twice the resident blocks), the next
+// tile still prefetched into registers, two barriers per K tile.
+template <int BM, int BN, bool AK, bool BKC, int NBUF>
 __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 32, TN = WN / 32;
     using SA = Stage<AK, BM>;
     using SB = Stage<BKC, BN>;
-    __shared__ __attribute__((aligned(16))) float sA[2][AK ? BM * SA::LD : kBK * SA::LD];
-    __shared__ __attribute__((aligned(16))) float sB[2][BKC ? BN * SB::LD : kBK * SB::LD];
+    __shared__ __attribute__((aligned(16))) float sA[NBUF][AK ? BM * SA::LD : kBK * SA::LD];
+    __shared__ __attribute__((aligned(16))) float sB[NBUF][BKC ? BN * SB::LD : kBK * SB::LD];
 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid >> 1, wn = wid & 1;
@@ -162,8 +166,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
             ra.load(p.A, p.lda, m0, p.M, (kt + 1) * kBK, p.K);
             rb.load(p.B, p.ldb, n0, p.N, (kt + 1) * kBK, p.K);
         }
-        const float *a_s = sA[cur];
-        const float *b_s = sB[cur];
+        const float *a_s = sA[NBUF == 2 ? cur : 0];
+        const float *b_s = sB[NBUF == 2 ? cur : 0];
         f32x4 af[2][TM], bf[2][TN];
         auto frag = [&](f32x4 (&fa)[TM], f32x4 (&fb)[TN], int s4) {
 #pragma unroll
@@ -200,12 +204,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g & 1][i][q], bf[g & 1][j][q],
                                                                           acc[i][j], 0, 0, 0);
         }
-        if (more) {
-            ra.store(sA[cur ^ 1]);
-            rb.store(sB[cur ^ 1]);
+        if constexpr (NBUF == 2) {
+            if (more) {
+                ra.store(sA[cur ^ 1]);
+                rb.store(sB[cur ^ 1]);
+            }
+            __syncthreads();
+            cur ^= 1;
+        } else {
+            __syncthreads();                  // every wave is done reading the tile
+            if (more) {
+                ra.store(sA[0]);
+                rb.store(sB[0]);
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        cur ^= 1;
     }
 
     // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
@@ -237,23 +250,48 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
     }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NBUF = 2>
 int launch_tiles(const GemmArgs &p, bool ak, bool bk, int splits, hipStream_t st) {
     dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
-    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true>), grid, dim3(256), 0, st, p);
-    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false>), grid, dim3(256), 0, st, p);
-    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false>), grid, dim3(256), 0, st, p);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false, NBUF>), grid, dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+// Plan: 64x64 tiles with a single LDS buffer (up to 8 resident blocks per CU)
+// measured fastest on the WSWGAT shapes except long-K tall GEMMs, where 128x64
+// single-buffer tiles amortise their prologue better (tools/gemm_tiles.py).
+// Split-K when the output has too few 64x64 tiles to fill the GPU (~1280 blocks).
+int plan_splits(int M, int N, int K) {
+    const int kt = (K + kBK - 1) / kBK;
+    const long tiles = (long)((M + 63) / 64) * ((N + 63) / 64);
+    int sp = 1;
+    if (tiles < 512 && kt >= 8) {
+        sp = (int)((1280 + tiles - 1) / tiles);
+        if (sp > kt / 4) sp = kt / 4;
+        if (sp < 1) sp = 1;
+    }
+    return sp;
+}
+
+int plan_tile(int M, int N, int K, int splits) {
+    const int kt = (K + kBK - 1) / kBK;
+    const long big = (long)((M + 127) / 128) * ((N + 63) / 64) * splits;
+    if (splits == 1 && kt >= 16 && big >= 512) return 4;
+    return 5;
 }
 
 }  // namespace
 
 extern "C" {
 
+int hsg_gemm_auto_splits(int M, int N, int K) { return plan_splits(M, N, K); }
+
 size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits) {
-    (void)K;
+    if (splits == 0) splits = plan_splits(M, N, K);
     return splits > 1 ? (size_t)splits * M * N : 0;
 }
 
@@ -268,40 +306,22 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     if (M == 0 || N == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     const int kt_total = (K + kBK - 1) / kBK;
-    if (splits == 0) {
-        // automatic: split K when the output has too few tiles to fill the GPU
-        const long tiles = (long)((M + 127) / 128) * ((N + 63) / 64);
-        splits = 1;
-        if (tiles < 256 && kt_total >= 8) {
-            splits = (int)((512 + tiles - 1) / tiles);
-            if (splits > kt_total / 4) splits = kt_total / 4;
-            if (splits < 1) splits = 1;
-        }
-    }
+    if (splits == 0) splits = plan_splits(M, N, K);
     if (splits < 1) splits = 1;
     if (splits > kt_total) splits = kt_total > 0 ? kt_total : 1;
     if (splits > 1 && !workspace) return HSG_EINVAL;
     GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
                (kt_total + splits - 1) / splits, workspace};
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
-    // pick the tile whose block count best fills 256 CUs (blocks/CU by LDS+VGPR
-    // budget: 128x128 -> 2, 128x64 -> 3, 64x64 -> 4), favouring larger tiles
-    struct Cand { int bm, bn, per_cu; float eff; };
-    Cand cands[3] = {{128, 128, 2, 1.0f}, {128, 64, 3, 0.9f}, {64, 64, 4, 0.8f}};
-    int best = 0;
-    float best_score = -1.f;
-    for (int c = 0; c < 3; ++c) {
-        const long nb = (long)((M + cands[c].bm - 1) / cands[c].bm) * ((N + cands[c].bn - 1) / cands[c].bn) * splits;
-        const long slots = 256L * cands[c].per_cu;
-        const long rounds = (nb + slots - 1) / slots;
-        const float fill = (float)nb / (float)(rounds * slots);
-        const float score = fill * cands[c].eff;
-        if (score > best_score + 1e-3f) { best_score = score; best = c; }
-    }
+    int best = plan_tile(M, N, K, splits);
+    if (const char *f = getenv("HSG_GEMM_TILE")) best = atoi(f);   // dev override (tools/gemm_sweep.py)
     int rc;
     if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
     else if (best == 1) rc = launch_tiles<128, 64>(p, ak, bk, splits, st);
-    else rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
+    else if (best == 2) rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
+    else if (best == 3) rc = launch_tiles<128, 128, 1>(p, ak, bk, splits, st);
+    else if (best == 4) rc = launch_tiles<128, 64, 1>(p, ak, bk, splits, st);
+    else rc = launch_tiles<64, 64, 1>(p, ak, bk, splits, st);
     if (rc || splits == 1) return rc;
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);

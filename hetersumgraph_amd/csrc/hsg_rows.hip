@@ -67,6 +67,9 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
     }
 }
 
+// Backward: one wave per row, two rows in flight per wave (their loads are
+// issued together).  Per block, column partials of dgamma, dbeta and of dy (the
+// gradient of W2's bias, b2) go to part[block][3][d].
 template <int NPL>
 __global__ __launch_bounds__(256) void k_ln_bwd(int n, int d, const float *__restrict__ dout,
                                                 const float *__restrict__ y, const float *__restrict__ x,
@@ -74,60 +77,89 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int n, int d, const float *__res
                                                 const float *__restrict__ rstd, float p_drop,
                                                 const int64_t *__restrict__ seedp, uint32_t offset,
                                                 float *__restrict__ dy, float *__restrict__ dx,
-                                                float *__restrict__ dgamma_part, float *__restrict__ dbeta_part) {
-    __shared__ float s_g[4][kMaxPerLane * 64];
-    __shared__ float s_b[4][kMaxPerLane * 64];
+                                                float *__restrict__ part) {
+    __shared__ float s_red[4][kMaxPerLane * 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
-    float dg[NPL], db[NPL];
+    float dg[NPL], db[NPL], dyb[NPL];
+    float gam[NPL];
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) { dg[i] = 0.f; db[i] = 0.f; }
-    for (int r = blockIdx.x * 4 + wid; r < n; r += gridDim.x * 4) {
-        const float mu = mean[r], rs = rstd[r];
-        float xh[NPL], g[NPL];
-        bool keep[NPL];
-        float sg = 0.f, sgx = 0.f;
+    for (int i = 0; i < NPL; ++i) {
+        dg[i] = db[i] = dyb[i] = 0.f;
+        gam[i] = lane + 64 * i < d ? gamma[lane + 64 * i] : 0.f;
+    }
+    const int stride = gridDim.x * 4;
+    for (int r0 = blockIdx.x * 4 + wid; r0 < n; r0 += 2 * stride) {
+        const int rr[2] = {r0, r0 + stride};
+        float yv[2][NPL], xv[2][NPL], gv[2][NPL], mu[2], rs[2];
 #pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-            const int c = lane + 64 * i;
-            xh[i] = g[i] = 0.f;
-            keep[i] = true;
-            if (c < d) {
-                const size_t o = (size_t)r * d + c;
-                float v = y[o];
-                if (p_drop > 0.f) {
-                    keep[i] = hsg_keep(seed, offset, o, thr);
-                    v = keep[i] ? v * scale : 0.f;
-                }
-                xh[i] = (v + x[o] - mu) * rs;
-                const float go = dout[o];
-                g[i] = go * gamma[c];
-                sg += g[i];
-                sgx = fmaf(g[i], xh[i], sgx);
-                dg[i] = fmaf(go, xh[i], dg[i]);
-                db[i] += go;
+        for (int q = 0; q < 2; ++q) {
+            const bool ok = rr[q] < n;
+            const int r = ok ? rr[q] : r0;
+            mu[q] = mean[r];
+            rs[q] = rstd[r];
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int c = lane + 64 * i;
+                const size_t o = (size_t)r * d + (c < d ? c : 0);
+                yv[q][i] = y[o];
+                xv[q][i] = x[o];
+                gv[q][i] = (ok && c < d) ? dout[o] : 0.f;
             }
         }
-        const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
 #pragma unroll
-        for (int i = 0; i < NPL; ++i) {
-            const int c = lane + 64 * i;
-            if (c < d) {
-                const size_t o = (size_t)r * d + c;
-                const float ds = rs * (g[i] - mg - xh[i] * mgx);
-                dx[o] = ds;
-                dy[o] = keep[i] ? ds * scale : 0.f;
+        for (int q = 0; q < 2; ++q) {
+            if (rr[q] >= n) break;
+            const size_t rb = (size_t)rr[q] * d;
+            float xh[NPL], g[NPL];
+            bool keep[NPL];
+            float sg = 0.f, sgx = 0.f;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int c = lane + 64 * i;
+                xh[i] = g[i] = 0.f;
+                keep[i] = true;
+                if (c < d) {
+                    float v = yv[q][i];
+                    if (p_drop > 0.f) {
+                        keep[i] = hsg_keep(seed, offset, rb + c, thr);
+                        v = keep[i] ? v * scale : 0.f;
+                    }
+                    xh[i] = (v + xv[q][i] - mu[q]) * rs[q];
+                    const float go = gv[q][i];
+                    g[i] = go * gam[i];
+                    sg += g[i];
+                    sgx = fmaf(g[i], xh[i], sgx);
+                    dg[i] = fmaf(go, xh[i], dg[i]);
+                    db[i] += go;
+                }
+            }
+            const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
+#pragma unroll
+            for (int i = 0; i < NPL; ++i) {
+                const int c = lane + 64 * i;
+                if (c < d) {
+                    const float ds = rs[q] * (g[i] - mg - xh[i] * mgx);
+                    const float dyv = keep[i] ? ds * scale : 0.f;
+                    dx[rb + c] = ds;
+                    dy[rb + c] = dyv;
+                    dyb[i] += dyv;
+                }
             }
         }
     }
+    // block partials, three passes through one LDS slab (fixed order: deterministic)
+    float *dst = part + (size_t)blockIdx.x * 3 * d;
 #pragma unroll
-    for (int i = 0; i < NPL; ++i) { s_g[wid][lane + 64 * i] = dg[i]; s_b[wid][lane + 64 * i] = db[i]; }
-    __syncthreads();
-    for (int c = threadIdx.x; c < d; c += blockDim.x) {
-        dgamma_part[(size_t)blockIdx.x * d + c] = s_g[0][c] + s_g[1][c] + s_g[2][c] + s_g[3][c];
-        dbeta_part[(size_t)blockIdx.x * d + c] = s_b[0][c] + s_b[1][c] + s_b[2][c] + s_b[3][c];
+    for (int which = 0; which < 3; ++which) {
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) s_red[wid][lane + 64 * i] = which == 0 ? dg[i] : which == 1 ? db[i] : dyb[i];
+        __syncthreads();
+        for (int c = threadIdx.x; c < d; c += blockDim.x)
+            dst[which * d + c] = s_red[0][c] + s_red[1][c] + s_red[2][c] + s_red[3][c];
+        __syncthreads();
     }
 }
 
@@ -170,17 +202,17 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
 
 int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
-               float *dy, float *dx, float *dgamma_part, float *dbeta_part, void *stream) {
-    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed))
+               float *dy, float *dx, float *part, void *stream) {
+    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) || !part)
         return HSG_EINVAL;
-    if (n == 0) return 0;
-    const int npl = (d + 63) / 64;
-    dim3 grid(grid_rows(n, kLnBwdGridCap)), block(256);
     hipStream_t st = (hipStream_t)stream;
+    dim3 grid(grid_rows(n, kLnBwdGridCap)), block(256);
+    if (n == 0) return (int)hipMemsetAsync(part, 0, sizeof(float) * 3 * d * grid.x, st);
+    const int npl = (d + 63) / 64;
 #define HSG_LNB(K)                                                                                       \
     case K:                                                                                              \
         hipLaunchKernelGGL(k_ln_bwd<K>, grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, \
-                           seed, offset, dy, dx, dgamma_part, dbeta_part);                               \
+                           seed, offset, dy, dx, part);                                                  \
         break;
     switch (npl) { HSG_LNB(1) HSG_LNB(2) HSG_LNB(3) HSG_LNB(4) HSG_LNB(5) HSG_LNB(6) HSG_LNB(7) HSG_LNB(8) }
 #undef HSG_LNB

@@ -52,12 +52,8 @@ def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=
 
 
 def auto_splits(M, N, K):
-    """Mirror of hsg_gemm_f32's splits == 0 rule (so the workspace can be sized)."""
-    kt = (K + 31) // 32
-    tiles = ((M + 127) // 128) * ((N + 63) // 64)
-    if tiles < 256 and kt >= 8:
-        return max(1, min((512 + tiles - 1) // tiles, kt // 4))
-    return 1
+    """hsg_gemm_f32's splits == 0 plan (so the workspace can be sized)."""
+    return load().hsg_gemm_auto_splits(M, N, K)
 
 
 def splits_for(M, N, K, n_cu=256):

@@ -6,10 +6,11 @@ Reference: module/GATLayer.py:35-44 --
 Forward  (3 launches): H = relu(x W1^T + b1) [GEMM, bias+ReLU epilogue];
                        y = H W2^T + b2       [GEMM, bias epilogue];
                        out = LN(dropout(y) + x) [row kernel, saves mean/rstd].
-Backward (6 launches): (dy, dx) = row kernel (LN + dropout backward, dgamma/dbeta
-                       block partials); dH = (dy W2) * (H > 0) [GEMM, relu' epilogue];
-                       dx += dH W1 [GEMM, accumulate epilogue]; dW2 = dy^T H and
-                       dW1 = dH^T x [split-K GEMMs]; bias/LN grads are column sums.
+Backward:              (dy, dx) = row kernel (LN + dropout backward, block partials
+                       of dgamma, dbeta and db2 = colsum(dy)); dH = (dy W2) * (H > 0)
+                       [GEMM, relu' epilogue]; dx += dH W1 [GEMM, accumulate
+                       epilogue]; dW2 = dy^T H and dW1 = dH^T x [split-K GEMMs];
+                       db1 = colsum(dH); one reduction of the row-kernel partials.
 """
 from __future__ import annotations
 
@@ -51,18 +52,17 @@ class _FFN(torch.autograd.Function):
         nb = lib.hsg_ln_bwd_blocks(n)
         dy = torch.empty_like(x)
         dx = torch.empty_like(x)
-        dg = x.new_empty(nb, d)
-        dbt = x.new_empty(nb, d)
+        part = x.new_empty(nb, 3, d)
         check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd),
-                             float(ctx.p_drop), ptr(ctx.seed_t), ctx.off, ptr(dy), ptr(dx), ptr(dg), ptr(dbt),
+                             float(ctx.p_drop), ptr(ctx.seed_t), ctx.off, ptr(dy), ptr(dx), ptr(part),
                              stream_of(x)), "hsg_ln_bwd")
         dH = gemm(dy, w2, relu_mask=H)                         # [n, d_hid]
         gemm(dH, w1, out=dx, add=dx)                           # dx += dH W1
         dw2 = gemm(dy, H, a_t=True)                            # [d, d_hid]
         dw1 = gemm(dH, x, a_t=True)                            # [d_hid, d]
-        db2 = dy.sum(0)
         db1 = dH.sum(0)
-        return dx, dw1, db1, dw2, db2, dg.sum(0), dbt.sum(0), None, None
+        dg, dbt, db2 = part.sum(0)                             # one reduction for three vectors
+        return dx, dw1, db1, dw2, db2, dg, dbt, None, None
 
 
 def ffn_forward(x, w1, b1, w2, b2, gamma, beta, p_drop=0.0, eps=LN_EPS):

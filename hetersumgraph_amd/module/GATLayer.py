@@ -16,7 +16,7 @@ import torch.nn.functional as F
 
 from ..ffn import ffn_forward
 from ..hproj import head_projection_dropout
-from ..ops import LEAKY_SLOPE, gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
+from ..ops import LEAKY_SLOPE, gat_aggregate, gat_heads_table, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
 from ..relation import N_BOX
 
 # The reference asserts "no NaN" around every FFN (GATLayer.py:36, 43), a host sync
@@ -153,5 +153,21 @@ def fused_heads(g, h, params, kind, origin=None, dropout=None):
         Z = head_projection_dropout(h, W, H, D, dropout.p)               # per-head masks, fused
     else:
         Z = F.linear(h, W)
+    T = table_weight(g)
+    if T is not None and T.shape[1] == wf.shape[2]:
+        return gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, LEAKY_SLOPE)
     tau, mode = edge_tau(g, rel, a3, wf, bf)
     return gat_aggregate(Z, a1, tau, origin, rel, H, D, LEAKY_SLOPE, mode)
+
+
+def table_weight(g):
+    """The [10, F] TF-IDF embedding table behind edata['tfidfembed'] when that column
+    was written by HSumGraph.set_wnfeature (HiGraph.py:146-151), else None."""
+    from ..graph import TableColumn
+
+    col = g._eframe().cols.get("tfidfembed")
+    if col is None:
+        raise KeyError("tfidfembed")   # edges.data['tfidfembed'] in the reference UDF
+    if isinstance(col, TableColumn) and col.tag == TFIDF_TAG and col.weight.shape[0] == N_BOX:
+        return col.weight
+    return None

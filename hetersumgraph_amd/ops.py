@@ -85,13 +85,99 @@ class _GatAggregate(torch.autograd.Function):
         dZ = torch.empty_like(Z)
         dsig = torch.empty_like(sigma)
         check(lib.hsg_gat_bwd_src(relp, H, D, mode, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
-                                  ptr(G), ptr(dpre), ptr(a1), ptr(dZ), ptr(dsig), st),
+                                  ptr(G), ptr(dpre), ptr(a1), None, ptr(dZ), ptr(dsig), None, st),
               "hsg_gat_bwd_src")
         da1 = None
         if ctx.needs_input_grad[1]:
             da1 = torch.einsum("uk,ukd->kd", dsig, Z.view(-1, H, D))
         dtau = dtp.sum(0) if mode == HSG_TAU_TABLE else dpre
         return dZ, da1, dtau, (dout if ctx.has_origin else None), None, None, None, None, None
+
+
+class _GatHeadsTable(torch.autograd.Function):
+    """One multi-head application whose edge-type term comes from the TF-IDF table.
+
+    Same math as ``_GatAggregate`` with ``tau`` built in-kernel from the layer's
+    attention parameters (include/hsg.h, hsg_attn_params_fwd), so forward is 3
+    launches (params, sigma, edge pass) and backward 3 (dst pass, src pass with
+    the d a1 partials, params backward) with every parameter gradient written
+    directly -- no per-parameter slicing, einsum or reduction kernels."""
+
+    @staticmethod
+    def forward(ctx, Z, attn, T, wf, bf, origin, rel, H, D, slope):
+        lib = load()
+        Z = Z.contiguous()
+        origin = None if origin is None else origin.contiguous()
+        n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
+        if Z.shape != (n_src, HD):
+            raise ValueError(f"Z has shape {tuple(Z.shape)}, relation expects ({n_src}, {HD})")
+        if origin is not None and origin.shape != (n_dst, HD):
+            raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
+        F = T.shape[1]
+        st = stream_of(Z)
+        a1 = Z.new_empty(H, D)
+        tau = Z.new_empty(N_BOX + 1, H)
+        check(lib.hsg_attn_params_fwd(H, D, F, ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(a1), ptr(tau), st),
+              "hsg_attn_params_fwd")
+        sigma = Z.new_empty(n_src, H)
+        check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
+        relp = ctypes.byref(rel.cstruct())
+        h = Z.new_empty(n_dst, HD)
+        out = Z.new_empty(n_dst, HD) if origin is not None else None
+        m = Z.new_empty(n_dst, H)
+        l = Z.new_empty(n_dst, H)
+        check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+        ctx.save_for_backward(Z, attn, T, wf, bf, a1, sigma, tau, h, m, l)
+        ctx.rel, ctx.H, ctx.D, ctx.slope = rel, H, D, slope
+        ctx.has_origin = origin is not None
+        return out if origin is not None else h
+
+    @staticmethod
+    def backward(ctx, dout):
+        lib = load()
+        Z, attn, T, wf, bf, a1, sigma, tau, h, m, l = ctx.saved_tensors
+        rel, H, D, slope = ctx.rel, ctx.H, ctx.D, ctx.slope
+        dout = dout.contiguous()
+        st = stream_of(Z)
+        relp = ctypes.byref(rel.cstruct())
+        G = torch.empty_like(h)
+        dpre = Z.new_empty(rel.n_typed, H)
+        nbd = lib.hsg_gat_bwd_blocks(relp)
+        dtp = Z.new_empty(nbd, N_BOX + 1, H)
+        check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(ctx.has_origin), slope, ptr(Z), ptr(sigma),
+                                  ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                  ptr(dtp), st), "hsg_gat_bwd_dst")
+        dZ = torch.empty_like(Z)
+        nbs = lib.hsg_gat_bwd_src_blocks(relp)
+        da1p = Z.new_empty(nbs, H * D)
+        check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                                  ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZ), None, ptr(da1p), st),
+              "hsg_gat_bwd_src")
+        dattn = torch.empty_like(attn)
+        dwf = torch.empty_like(wf)
+        dbf = torch.empty_like(bf) if bf is not None else None
+        dT = torch.empty_like(T)
+        ws = Z.new_empty(lib.hsg_attn_params_bwd_workspace_floats(H, D))
+        check(lib.hsg_attn_params_bwd(H, D, T.shape[1], nbd, ptr(dtp), nbs, ptr(da1p), ptr(attn), ptr(wf),
+                                      ptr(bf), ptr(T), ptr(dattn), ptr(dwf), ptr(dbf), ptr(dT), ptr(ws), st),
+              "hsg_attn_params_bwd")
+        need = ctx.needs_input_grad
+        return (dZ if need[0] else None, dattn if need[1] else None, dT if need[2] else None,
+                dwf if need[3] else None, dbf if need[4] else None,
+                (dout if ctx.has_origin else None), None, None, None, None)
+
+
+def gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, slope=LEAKY_SLOPE):
+    """Multi-head aggregation with the TF-IDF-table edge term (+ ELU + residual).
+
+    Z [n_src, H*D]; attn [H, 3D] (attn_fc weights [a1|a2|a3] of every head);
+    T [10, F] TF-IDF embedding table; wf [H, D, F], bf [H, D] | None (feat_fc);
+    origin [n_dst, H*D] | None.  Returns [n_dst, H*D]."""
+    _require_device(Z, attn, T, wf, bf, origin)
+    attn, T, wf = attn.contiguous(), T.contiguous(), wf.contiguous()
+    bf = bf.contiguous() if bf is not None else None
+    return _GatHeadsTable.apply(Z, attn, T, wf, bf, origin, rel, H, D, float(slope))
 
 
 def gat_aggregate(Z, a1, tau, origin, rel, H, D, slope=LEAKY_SLOPE, tau_mode=HSG_TAU_TABLE):

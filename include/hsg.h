@@ -81,17 +81,41 @@ int hsg_gat_bwd_blocks(const hsg_rel *rel);
 
 /* Backward, source-centric half (CSC): for every source u
  *   dZ[u, k, :]  = sum_{e: src_e = u} alpha_ek * G[dst_e, k, :]  (+ dsigma[u,k]*a1[k,:] if a1)
- *   dsigma[u, k] = sum_{e: src_e = u} dpre[e, k]
+ *   dsigma[u, k] = sum_{e: src_e = u} dpre[e, k]                 (written if dsigma != NULL)
+ *   da1_part[b, k*D+d] = per-block partial sums of dsigma[u,k] * Z[u,k,d]
+ *                  (if da1_part != NULL; needs Z and hsg_gat_bwd_src_blocks(rel)*H*D floats)
  * a1 (optional, [H, D]) folds the gradient of sigma = <Z[u,k,:], a1[k,:]> into dZ. */
 int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
                     const float *sigma, const float *tau, const float *m, const float *l,
-                    const float *G, const float *dpre, const float *a1,
-                    float *dZ, float *dsigma, void *stream);
+                    const float *G, const float *dpre, const float *a1, const float *Z,
+                    float *dZ, float *dsigma, float *da1_part, void *stream);
+
+/* Number of partial rows hsg_gat_bwd_src writes into da1_part. */
+int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
 
 /* sigma[u, k] = <Z[u, k, :], a1[k, :]> -- the z_src part of attn_fc
  * (GATLayer.py:91-92 / 130-131); a1 = attn_fc.weight[0, :D] per head. */
 int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,
                         void *stream);
+
+/* ---- attention parameters of one layer application (GATLayer.py:84-93, 123-131) ----
+ * attn [H][3D] = the heads' attn_fc weights [a1 | a2 | a3] (a2 multiplies the
+ * all-zero z_dst, GATLayer.py:111), wf [H][D][F] / bf [H][D] (NULL on W2S) the
+ * feat_fc weights, T [10][F] the TF-IDF embedding table (HiGraph.py:52).
+ * fwd: a1 [H][D] = attn[:, :D];  tau [11][H]: tau[t][k] = <a3_k, wf_k T[t] + bf_k>
+ *      for t < 10, tau[10][k] = <a3_k, bf_k> (edges whose tfidfembed stayed 0).
+ * bwd: reduces dtau_part (hsg_gat_bwd_dst, n_dtau_part rows of 11*H) and da1_part
+ *      (hsg_gat_bwd_src, n_da1_part rows of H*D) in a fixed order (two launches,
+ *      hsg_attn_params_bwd_workspace_floats(H, D) floats of workspace) and writes
+ *      dattn [H][3D] (= [da1 | 0 | da3]), dwf [H][D][F], dbf [H][D] (if bf and dbf),
+ *      dT [10][F].  H <= 16, H*D <= 512, F <= 256. */
+int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf, const float *bf,
+                        const float *T, float *a1, float *tau, void *stream);
+int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_part, int n_da1_part,
+                        const float *da1_part, const float *attn, const float *wf, const float *bf,
+                        const float *T, float *dattn, float *dwf, float *dbf, float *dT, float *workspace,
+                        void *stream);
+size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 
 /* ---- dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32) ---------------------------
  * Replaces the torch GEMMs of the head projection fc (GATLayer.py:110 / 146) and of
@@ -108,7 +132,8 @@ int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, fl
 #define HSG_EPI_STORE 0
 #define HSG_EPI_RELU_BWD 1
 #define HSG_EPI_ADD 2
-size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits);
+size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits);   /* splits 0: the automatic plan */
+int hsg_gemm_auto_splits(int M, int N, int K);
 int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
                  const float *B, int ldb, int b_kcontig, float *C, int ldc,
                  const float *bias, const float *aux, int ldaux, int epi, int relu,
@@ -118,8 +143,8 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
  * Forward:  s = dropout(y; p, seed, offset) + x;  out = (s-mean)*rstd*gamma + beta
  *           (y = W2 relu(W1 x + b1) + b2 from hsg_gemm_f32; eps as nn.LayerNorm)
  * Backward: dx = dLN/ds (residual branch), dy = dx * mask / (1-p),
- *           dgamma_part/dbeta_part[b][d] = per-block column partials
- *           (hsg_ln_bwd_blocks(n) rows; sum them in order).
+ *           part[b][3][d] = per-block column partials of dgamma, dbeta and dy
+ *           (= the bias gradient of W2); hsg_ln_bwd_blocks(n) blocks, sum in order.
  * Dropout masks are a stateless hash of (*seed, offset, element index): *seed is
  * read from device memory (advance it between graph replays), offset is a
  * per-call constant; forward and backward with equal (seed, offset) agree.
@@ -130,7 +155,7 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
                float *out, float *mean, float *rstd, void *stream);
 int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
-               float *dy, float *dx, float *dgamma_part, float *dbeta_part, void *stream);
+               float *dy, float *dx, float *part, void *stream);
 
 /* ---- head projection with per-head input dropout (GATStackLayer.py:56) ----------
  * Training-mode  z_k = fc_k(dropout_k(h))  for all heads without materialising the

@@ -58,3 +58,54 @@ def test_gat_aggregate_matches_op_restatement(H, D, max_deg, origin, per_edge):
     for name, got, want in zip(("Z", "a1", "tau", "origin"), dl, leaves):
         scale = want.grad.abs().max().item() + 1e-6
         assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
+
+
+def tau_table_ref(attn, T, wf, bf, D):
+    """fp64 restatement of the edge-type term (GATLayer.py:84-93 / 123-131):
+    tau[t, k] = attn_fc_k[2D:] . feat_fc_k(T[t]) for t < 10, row 10 = feat_fc_k(0)."""
+    a3 = attn[:, 2 * D:]
+    feat = torch.einsum("kdf,tf->tkd", wf, T)                       # [10, H, D]
+    if bf is not None:
+        feat = feat + bf
+    rows = (feat * a3).sum(-1)                                      # [10, H]
+    zero = (a3 * bf).sum(-1, keepdim=True).t() if bf is not None else torch.zeros(1, attn.shape[0],
+                                                                                   dtype=attn.dtype)
+    return torch.cat([rows, zero], 0)
+
+
+@pytest.mark.parametrize("H,D,F,max_deg,bias", [(8, 8, 50, 40, False), (6, 50, 50, 5, True),
+                                                 (3, 16, 20, 12, True), (16, 4, 7, 30, False)])
+def test_gat_heads_table_matches_restatement(H, D, F, max_deg, bias):
+    """The fused table path (hsg_attn_params_fwd/bwd + edge kernels) against the fp64
+    composition tau_table_ref -> gat_aggregate_ref, outputs and every gradient."""
+    from hetersumgraph_amd.ops import gat_heads_table
+    from oracle.fused import gat_aggregate_ref
+    rng = np.random.default_rng(7 * H + D + F)
+    n_src, n_dst = 211, 77
+    rel, e_src, e_dst, tf, phantom = random_relation(rng, n_src, n_dst, max_deg)
+    reld = rel.to("cuda")
+    f64 = dict(dtype=torch.float64)
+    Z = torch.randn(n_src, H * D, **f64)
+    attn = torch.randn(H, 3 * D, **f64) * 0.3
+    T = torch.randn(10, F, **f64)
+    wf = torch.randn(H, D, F, **f64) / F ** 0.5
+    bf = torch.randn(H, D, **f64) * 0.2 if bias else None
+    org = torch.randn(n_dst, H * D, **f64)
+    R = torch.randn(n_dst, H * D, **f64)
+    ins = [Z, attn, T, wf, bf, org]
+    leaves = [t.clone().requires_grad_() if t is not None else None for t in ins]
+    Zr, attnr, Tr, wfr, bfr, orgr = leaves
+    tau = tau_table_ref(attnr, Tr, wfr, bfr, D)
+    ref = gat_aggregate_ref(e_src, e_dst, tf, phantom, n_dst, Zr, attnr[:, :D], tau, orgr)
+    (ref * R).sum().backward()
+    dl = [t.float().cuda().requires_grad_() if t is not None else None for t in ins]
+    out = gat_heads_table(dl[0], dl[1], dl[2], dl[3], dl[4], dl[5], reld, H, D)
+    (out * R.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    err = lambda a, b: (a.detach().cpu().double() - b.detach()).abs().max().item()
+    assert err(out, ref) < 2e-5
+    for name, got, want in zip(("Z", "attn", "T", "wf", "bf", "origin"), dl, leaves):
+        if want is None:
+            continue
+        scale = want.grad.abs().max().item() + 1e-6
+        assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
