@@ -14,7 +14,8 @@ all-reduce over RCCL (the path's one exchange step).  Encoders,
 graph construction and H2D copies are outside the step.  The step
 is captured once into a HIP graph and replayed.
 
-value = E_total x world_size / t_step (max over ranks of the timed region / K).
+value = E_global / t_step: all ranks' graph edges over the max-over-ranks time of
+one step (timed region / K).
 """
 from __future__ import annotations
 
@@ -62,12 +63,18 @@ def cpu_model():
     return platform.processor()
 
 
-def make_shard(config, rank, seed):
+def make_shard(config, rank, world, seed):
+    """The global batch (32 docs per GPU, seeded) split by document across ranks
+    (hetersumgraph_amd.parallel.shard_documents); returns this rank's docs, its
+    batched graph and the global edge count."""
     from hetersumgraph_amd import graph as hg
     from hetersumgraph_amd import synth
-    docs = synth.make_batch_docs(config, seed=seed * 1000 + rank)
+    from hetersumgraph_amd.parallel import shard_documents
+    per_gpu = synth.CONFIGS[config][1]
+    docs_all = synth.make_batch_docs(config, seed=seed, n_docs=per_gpu * world)
+    docs = shard_documents(docs_all, rank, world)
     G = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
-    return docs, G
+    return docs, G, int(sum(len(d.src) for d in docs_all))
 
 
 class Stack(torch.nn.Module):
@@ -139,6 +146,40 @@ def time_fwd_kernel(G, stack, Xw, Xs, reps):
     return float(np.mean(ms)), float(np.median(ms)), algorithmic_bytes_fwd(rel, H, D)
 
 
+def time_dense_kernel(stack, n_rows, reps):
+    """Average duration of the dominant dense kernel: the S2W FFN first GEMM
+    (x W1^T + b1, ReLU; [n_w, 300] x [300, 512]) on the stack's own weights, HIP
+    events on the launching stream.  Returns (ms, flops per launch)."""
+    from hetersumgraph_amd.dense import gemm
+    ffn = stack.sent2word.ffn
+    w1, b1 = ffn.w_1.weight.detach().squeeze(-1).contiguous(), ffn.w_1.bias.detach()
+    x = torch.randn(n_rows, w1.shape[1], device=w1.device)
+    out = x.new_empty(n_rows, w1.shape[0])
+    st = torch.cuda.current_stream()
+    for _ in range(5):
+        gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    torch.cuda.synchronize()
+    for e0, e1 in evs:
+        e0.record(st)
+        gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
+        e1.record(st)
+    torch.cuda.synchronize()
+    ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    return ms, 2.0 * n_rows * w1.shape[0] * w1.shape[1]
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py), or None."""
+    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            return json.load(fh)["traffic_bytes"], os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
 def cpu_baseline(docs_all, args, stack):
     """The DGL-UDF-structured CPU port (oracle/dgl_udf.py) on a bounded sample of
     the same workload, on this host's cores."""
@@ -192,7 +233,7 @@ def main():
     from hetersumgraph_amd import _lib
     _lib.load()
 
-    docs, G = make_shard(args.config, rank, args.seed)
+    docs, G, E_global = make_shard(args.config, rank, world, args.seed)
     E_total = G.number_of_edges()
     G.to(dev)
     torch.manual_seed(args.seed)                       # identical replicas on every rank
@@ -212,13 +253,9 @@ def main():
         (s * R).sum().backward()
 
     def allreduce():
-        # data-parallel gradient exchange: one flat bucket, one RCCL all-reduce (mean)
-        import torch.distributed as dist
-        grads = [p.grad for p in params]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat, op=dist.ReduceOp.AVG)
-        torch._foreach_copy_(grads, [t.view_as(g) for t, g in
-                                     zip(torch.split(flat, [g.numel() for g in grads]), grads)])
+        # the data-parallel exchange: bucketed mean all-reduce over RCCL
+        from hetersumgraph_amd.parallel import allreduce_gradients
+        allreduce_gradients(params)
 
     def zero():
         # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
@@ -284,11 +321,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
-    value = E_total * world / (dt / args.steps)
+    value = E_global / (dt / args.steps)
 
     # dominant edge kernel: average launch duration with HIP events on its stream
     k_ms_mean, k_ms_med, k_bytes = time_fwd_kernel(G, stack, Xw.detach(), Xs.detach(), args.kernel_reps)
     achieved = k_bytes / (k_ms_mean * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic()
+    d_ms, d_flops = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
+    d_tf = d_flops / (d_ms * 1e-3) / 1e12
 
     out = {
         "metric": "graph-edges/sec through WSWGAT fwd+bwd, CNN/DM-shaped batch; 1/2/4/8 GPU",
@@ -311,9 +351,15 @@ def main():
                    "hip_graph": bool(use_graph)},
         "roofline": {"kernel": "hsg_gat_fwd (S2W: sentence->word, H=6 x D=50)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": k_bytes, "avg_launch_us": k_ms_mean * 1e3,
                      "median_launch_us": k_ms_med * 1e3},
+        "roofline_dense": {"kernel": "hsg_gemm_f32 (S2W FFN x W1^T + b1, ReLU; "
+                                     f"{rel_s.n_dst}x300 @ 300x512)", "bound": "mfma",
+                           "achieved": d_tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                           "frac": d_tf / FP32_MFMA_PEAK_TFLOPS, "flops_per_launch": d_flops,
+                           "avg_launch_us": d_ms * 1e3},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
