@@ -12,7 +12,7 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhsg.so")
+LIB_PATH = os.environ.get("HSG_LIB_PATH") or os.path.join(_HERE, "libhsg.so")   # override: dev A/B builds
 
 HSG_EINVAL = 1001
 HSG_TAU_TABLE = 0

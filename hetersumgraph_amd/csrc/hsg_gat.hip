@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/hsg.h"
 
@@ -74,8 +75,50 @@ __device__ __forceinline__ int tau_row(const RelPtrs &R, int e) {
     else return e;
 }
 
+// Work assignment.  WPN waves cooperate on one node: WPN = 1 -> a wave owns whole
+// nodes (short edge segments, many nodes); WPN = 4 -> the block owns a node and
+// wave w takes the w-th contiguous quarter of its segment (long segments, few
+// nodes: the W2S destinations and S2W sources at config 2).  With WPN > 1 the node
+// loop is block-uniform (it contains barriers) and partial results are combined
+// through LDS in wave order (deterministic).
+__device__ __forceinline__ void subrange(int beg, int end, int part, int wpn, int &eb, int &ee) {
+    const int q = (end - beg + wpn - 1) / wpn;
+    eb = min(end, beg + part * q);
+    ee = min(end, eb + q);
+}
+
+// acc[i] += sum_j w[j][fh[i]] * X[rows[j], fo[i]] over the n staged edges of a
+// chunk.  Rows are fetched GR at a time into registers before any is used, so a
+// group's loads are in flight together; row indices past n are clamped and
+// their weight is 0.  All loads are unconditional (no per-lane branches).
+template <int NF>
+__device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD, int n, const int *rows,
+                                            const float *w, int H, const int (&fh)[NF], const int (&fo)[NF],
+                                            float (&acc)[NF]) {
+    // measured on the config-2 passes: grouping pays for narrow rows (NF <= 2);
+    // for wide rows the extra registers cost more occupancy than they buy
+    constexpr int GR = NF <= 2 ? 4 : 1;
+    for (int j0 = 0; j0 < n; j0 += GR) {
+        float xv[GR][NF];
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {
+            const float *xr = X + (size_t)rows[min(j0 + q, n - 1)] * HD;
+#pragma unroll
+            for (int i = 0; i < NF; ++i) xv[q][i] = xr[fo[i]];
+        }
+#pragma unroll
+        for (int q = 0; q < GR; ++q) {
+            const int j = j0 + q;
+            if (j < n) {
+#pragma unroll
+                for (int i = 0; i < NF; ++i) acc[i] = fmaf(w[j * H + fh[i]], xv[q][i], acc[i]);
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- forward ----
-template <int NF, int TAU_MODE>
+template <int NF, int TAU_MODE, int WPN>
 __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
@@ -83,27 +126,49 @@ __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lp
                                                 const float *__restrict__ origin,
                                                 float *__restrict__ hout, float *__restrict__ out,
                                                 float *__restrict__ mout, float *__restrict__ lout) {
+    constexpr int NPB = HSG_WAVES / WPN;
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
     __shared__ int s_nb[HSG_WAVES][HSG_CHUNK];
+    __shared__ float s_ml[HSG_WAVES][2 * HSG_HMAX];
+    __shared__ float s_acc[WPN > 1 ? HSG_WAVES : 1][WPN > 1 ? 64 * NF : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
     const bool kact = k < H;
-    int fh[NF];
+    const int part = wid % WPN, w0 = wid - part;
+    const bool writer = part == 0;
+    // fh: head of feature f; fo: f clamped into the row, so every gather load is
+    // unconditional (lanes past H*D compute values that are never stored) and the
+    // compiler can keep a chunk's loads in flight together
+    int fh[NF], fo[NF];
 #pragma unroll
-    for (int i = 0; i < NF; ++i) { int f = lane + 64 * i; fh[i] = f < HD ? f / D : 0; }
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        fh[i] = f < HD ? f / D : 0;
+        fo[i] = f < HD ? f : HD - 1;
+    }
     float *sa = s_alpha[wid];
     int *sn = s_nb[wid];
 
-    for (int v = blockIdx.x * HSG_WAVES + wid; v < R.n_dst; v += gridDim.x * HSG_WAVES) {
+    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += gridDim.x * NPB) {
+        const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
         const int beg = R.indptr[v], end = R.indptr[v + 1];
         const int c = R.phantom[v];
+        int eb, ee;
+        subrange(beg, end, part, WPN, eb, ee);
+        const int n1 = ee - eb;
+        const bool single = n1 <= HSG_CHUNK;      // scores stay in LDS between the phases
         // phase 1: online (max, sum) of this head's scores over edges j = l (mod lph)
         float mx = -INFINITY, sm = 0.f;
         if (kact) {
-            for (int e = beg + l; e < end; e += lph) {
+            for (int j = l; j < n1; j += lph) {
+                const int e = eb + j;
                 const int u = R.src[e];
                 const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                if (single) {
+                    sa[j * H + k] = s;
+                    if (k == 0) sn[j] = u;
+                }
                 if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
                 else sm += __expf(s - mx);
             }
@@ -112,56 +177,179 @@ __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lp
             const float om = __shfl_xor(mx, o), os = __shfl_xor(sm, o);
             lse_merge(mx, sm, om, os);
         }
+        if constexpr (WPN > 1) {
+            if (kact && l == 0) { s_ml[wid][k] = mx; s_ml[wid][HSG_HMAX + k] = sm; }
+            __syncthreads();
+            mx = -INFINITY;
+            sm = 0.f;
+            if (kact) {
+#pragma unroll
+                for (int p = 0; p < WPN; ++p) lse_merge(mx, sm, s_ml[w0 + p][k], s_ml[w0 + p][HSG_HMAX + k]);
+            }
+        }
         if (c > 0) lse_merge(mx, sm, 0.f, (float)c);     // phantom in-edges: e = 0
         const bool any = end > beg;
         const float inv = any ? 1.f / sm : 0.f;
+        // the residual row: independent of the gathers below
+        float org[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
 
-        // phase 2: stage alphas per 64-edge chunk, then flat-mapped aggregation
+        // phase 2: alphas per 64-edge chunk, then flat-mapped aggregation
         float acc[NF];
 #pragma unroll
         for (int i = 0; i < NF; ++i) acc[i] = 0.f;
-        for (int cb = beg; cb < end; cb += HSG_CHUNK) {
-            const int n = min(HSG_CHUNK, end - cb);
+        for (int cb = eb; cb < ee; cb += HSG_CHUNK) {
+            const int n = min(HSG_CHUNK, ee - cb);
             if (kact) {
                 for (int j = l; j < n; j += lph) {
-                    const int e = cb + j;
-                    const int u = R.src[e];
-                    const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                    float s;
+                    if (single) {
+                        s = sa[j * H + k];                 // written by this same lane
+                    } else {
+                        const int e = cb + j;
+                        const int u = R.src[e];
+                        s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                        if (k == 0) sn[j] = u;
+                    }
                     sa[j * H + k] = __expf(s - mx) * inv;
-                    if (k == 0) sn[j] = u;
                 }
             }
             wave_lds_sync();
-#pragma unroll 4
-            for (int j = 0; j < n; ++j) {
-                const float *zr = Z + (size_t)sn[j] * HD;
+            gather_rows<NF>(Z, HD, n, sn, sa, H, fh, fo, acc);
+            wave_lds_sync();
+        }
+        if constexpr (WPN > 1) {
+#pragma unroll
+            for (int i = 0; i < NF; ++i) s_acc[wid][lane + 64 * i] = acc[i];
+            __syncthreads();
+            if (writer) {
 #pragma unroll
                 for (int i = 0; i < NF; ++i) {
-                    const int f = lane + 64 * i;
-                    if (f < HD) acc[i] = fmaf(sa[j * H + fh[i]], zr[f], acc[i]);
+                    float a = 0.f;
+#pragma unroll
+                    for (int p = 0; p < WPN; ++p) a += s_acc[w0 + p][lane + 64 * i];
+                    acc[i] = a;
                 }
             }
-            wave_lds_sync();
         }
         // epilogue: h, and elu(h) + origin (GAT.py:56-57)
+        if (writer) {
 #pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            const int f = lane + 64 * i;
-            if (f < HD) {
-                const size_t o = (size_t)v * HD + f;
-                const float hv = acc[i];
-                hout[o] = hv;
-                if (origin) out[o] = (hv > 0.f ? hv : expm1f(hv)) + origin[o];
+            for (int i = 0; i < NF; ++i) {
+                const int f = lane + 64 * i;
+                if (f < HD) {
+                    const size_t o = (size_t)v * HD + f;
+                    const float hv = acc[i];
+                    hout[o] = hv;
+                    if (origin) out[o] = (hv > 0.f ? hv : expm1f(hv)) + org[i];
+                }
+            }
+            if (kact && l == 0) {
+                mout[v * H + k] = any ? mx : 0.f;
+                lout[v * H + k] = any ? sm : 1.f;
             }
         }
-        if (kact && l == 0) {
-            mout[v * H + k] = any ? mx : 0.f;
-            lout[v * H + k] = any ? sm : 1.f;
-        }
+        if constexpr (WPN > 1) __syncthreads();          // s_ml / s_acc are reused
     }
 }
 
 // ---------------------------------------------------- backward: dst-centric ----
+// Shared by both variants:  G = origin_mode ? dOut * elu'(h) : dOut,  rho = G.h,
+//   dpre[e,k] = alpha (G_v.Z_u - rho) * leaky'(pre),  dtau partials per block.
+//
+// Edge-parallel variant (D <= 16): every lane of head k holds the whole G_v,k
+// (DV registers) and handles its own edges e = l (mod lph) end to end -- no
+// shuffles per edge, independent loads.  The d tau contributions go to 11
+// per-lane registers (one per tau row), reduced once at the end.
+template <int DV, int TAU_MODE, int WPN>
+__global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D, int lph, int origin_mode,
+                                                       float slope,
+                                                       const float *__restrict__ Z,
+                                                       const float *__restrict__ sigma,
+                                                       const float *__restrict__ tau,
+                                                       const float *__restrict__ hsv,
+                                                       const float *__restrict__ mv,
+                                                       const float *__restrict__ lv,
+                                                       const float *__restrict__ dout,
+                                                       float *__restrict__ G, float *__restrict__ dpre,
+                                                       float *__restrict__ dtau_part) {
+    constexpr int NPB = HSG_WAVES / WPN;
+    __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const int k = lane / lph, l = lane - (lane / lph) * lph;
+    const bool kact = k < H;
+    const int part = wid % WPN;
+    float dt[HSG_NT];
+#pragma unroll
+    for (int t = 0; t < HSG_NT; ++t) dt[t] = 0.f;
+
+    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += gridDim.x * NPB) {
+        const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
+        const int beg = R.indptr[v], end = R.indptr[v + 1];
+        float g[DV];
+        float rho = 0.f;
+        const int kc = kact ? k : H - 1;
+#pragma unroll
+        for (int d = 0; d < DV; ++d) {           // clamped, unconditional loads; masked values
+            const size_t o = (size_t)v * HD + kc * D + min(d, D - 1);
+            const float hv = hsv[o], dv = dout[o];
+            const bool ok = kact && d < D;
+            const float gv = ok ? (origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv) : 0.f;
+            g[d] = gv;
+            rho = fmaf(gv, hv, rho);
+        }
+        if (part == 0 && kact) {
+#pragma unroll
+            for (int d = 0; d < DV; ++d)
+                if (d < D && d % lph == l) G[(size_t)v * HD + k * D + d] = g[d];
+        }
+        if (end == beg || !kact) continue;
+        const float M = mv[v * H + k];
+        const float inv = 1.f / lv[v * H + k];
+        int eb, ee;
+        subrange(beg, end, part, WPN, eb, ee);
+#pragma unroll 2
+        for (int e = eb + l; e < ee; e += lph) {
+            const int u = R.src[e];
+            const int t = tau_row<TAU_MODE>(R, e);
+            const float *zr = Z + (size_t)u * HD + k * D;
+            float dot = 0.f;
+#pragma unroll
+            for (int d = 0; d < DV; ++d) dot = fmaf(g[d], zr[min(d, D - 1)], dot);   // g[d] = 0 past D
+            const float pre = sigma[u * H + k] + tau[t * H + k];
+            const float alpha = __expf(leaky(pre, slope) - M) * inv;
+            const float ds = alpha * (dot - rho);
+            const float dp = pre > 0.f ? ds : ds * slope;
+            dpre[(size_t)e * H + k] = dp;
+            if constexpr (TAU_MODE == HSG_TAU_TABLE) {
+#pragma unroll
+                for (int tt = 0; tt < HSG_NT; ++tt) dt[tt] += t == tt ? dp : 0.f;
+            }
+        }
+    }
+    if constexpr (TAU_MODE == HSG_TAU_TABLE) {
+#pragma unroll
+        for (int tt = 0; tt < HSG_NT; ++tt) {
+            const float a = group_sum(dt[tt], lph);
+            if (kact && l == 0) s_dtau[wid][tt * H + k] = a;
+        }
+        __syncthreads();
+        const int nt = HSG_NT * H;
+        for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < HSG_WAVES; ++w) a += s_dtau[w][i];
+            dtau_part[(size_t)blockIdx.x * nt + i] = a;
+        }
+    }
+}
+
+// Feature-split variant (any D <= 512, short segments): lane l of head k owns
+// features d = l + lph*i; per edge the G.Z dot is a group sum.  The first lph
+// edges' (src, pre) are loaded before the G/h/dOut rows so that chain overlaps
+// them, then broadcast to the head group with a lane shuffle.
 template <int NE, int TAU_MODE>
 __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
@@ -185,40 +373,55 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
         wave_lds_sync();
     }
 
-    for (int v = blockIdx.x * HSG_WAVES + wid; v < R.n_dst; v += gridDim.x * HSG_WAVES) {
+    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += gridDim.x * HSG_WAVES) {
+        const int v = __builtin_amdgcn_readfirstlane(v_);
         const int beg = R.indptr[v], end = R.indptr[v + 1];
+        // prefetch edge j = l of this head: source rank, tau row and pre-activation
+        int u0 = 0, t0 = 0;
+        float pre0 = 0.f;
+        if (kact && beg + l < end) {
+            u0 = R.src[beg + l];
+            t0 = tau_row<TAU_MODE>(R, beg + l);
+            pre0 = sigma[u0 * H + k] + tau[t0 * H + k];
+        }
         float g[NE];
         float rho = 0.f;
+        const int kc = kact ? k : H - 1;
 #pragma unroll
-        for (int i = 0; i < NE; ++i) {
+        for (int i = 0; i < NE; ++i) {           // clamped, unconditional loads; masked values
             const int d = l + lph * i;
-            g[i] = 0.f;
-            if (kact && d < D) {
-                const size_t o = (size_t)v * HD + k * D + d;
-                const float hv = hsv[o], dv = dout[o];
-                const float gv = origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv;
-                G[o] = gv;
-                g[i] = gv;
-                rho = fmaf(gv, hv, rho);
-            }
+            const size_t o = (size_t)v * HD + kc * D + min(d, D - 1);
+            const float hv = hsv[o], dv = dout[o];
+            const bool ok = kact && d < D;
+            const float gv = ok ? (origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv) : 0.f;
+            if (ok) G[o] = gv;
+            g[i] = gv;
+            rho = fmaf(gv, hv, rho);
         }
         if (end == beg) continue;   // uniform per wave: no typed in-edge, no gradient
         rho = group_sum(rho, lph);
         const float M = kact ? mv[v * H + k] : 0.f;
         const float inv = kact ? 1.f / lv[v * H + k] : 0.f;
+        const int gl = k * lph;                         // first lane of this head group
         for (int e = beg; e < end; ++e) {
-            const int u = R.src[e];
-            const float *zr = Z + (size_t)u * HD + k * D;
+            const int j = e - beg;
+            int u, t;
+            float pre;
+            if (j < lph) {                              // wave-uniform branch
+                u = __shfl(u0, gl + j);
+                t = __shfl(t0, gl + j);
+                pre = __shfl(pre0, gl + j);
+            } else {
+                u = R.src[e];
+                t = tau_row<TAU_MODE>(R, e);
+                pre = kact ? sigma[u * H + k] + tau[t * H + k] : 0.f;
+            }
+            const float *zr = Z + (size_t)u * HD + kc * D;
             float dot = 0.f;
 #pragma unroll
-            for (int i = 0; i < NE; ++i) {
-                const int d = l + lph * i;
-                if (kact && d < D) dot = fmaf(g[i], zr[d], dot);
-            }
+            for (int i = 0; i < NE; ++i) dot = fmaf(g[i], zr[min(l + lph * i, D - 1)], dot);   // g = 0 past D
             dot = group_sum(dot, lph);
             if (kact && l == 0) {
-                const int t = tau_row<TAU_MODE>(R, e);
-                const float pre = sigma[u * H + k] + tau[t * H + k];
                 const float alpha = __expf(leaky(pre, slope) - M) * inv;
                 const float ds = alpha * (dot - rho);
                 const float dp = pre > 0.f ? ds : ds * slope;
@@ -240,7 +443,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
 }
 
 // ---------------------------------------------------- backward: src-centric ----
-template <int NF, int TAU_MODE>
+template <int NF, int TAU_MODE, int WPN>
 __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, int lph, float slope,
                                                     const float *__restrict__ sigma,
                                                     const float *__restrict__ tau,
@@ -252,32 +455,50 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
                                                     const float *__restrict__ Z,
                                                     float *__restrict__ dZ, float *__restrict__ dsigma,
                                                     float *__restrict__ da1_part) {
+    constexpr int NPB = HSG_WAVES / WPN;
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
     __shared__ int s_nb[HSG_WAVES][HSG_CHUNK];
     __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
+    __shared__ float s_dsum[HSG_WAVES][HSG_HMAX];
     __shared__ float s_da1[HSG_WAVES][64 * NF];
+    __shared__ float s_acc[WPN > 1 ? HSG_WAVES : 1][WPN > 1 ? 64 * NF : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
     const bool kact = k < H;
-    int fh[NF];
+    const int part = wid % WPN, w0 = wid - part;
+    const bool writer = part == 0;
+    int fh[NF], fo[NF];
 #pragma unroll
-    for (int i = 0; i < NF; ++i) { int f = lane + 64 * i; fh[i] = f < HD ? f / D : 0; }
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        fh[i] = f < HD ? f / D : 0;
+        fo[i] = f < HD ? f : HD - 1;
+    }
     float *sa = s_alpha[wid];
     int *sn = s_nb[wid];
     float da1[NF];                       // this wave's share of sum_u dsigma[u,k] Z[u,k,:]
 #pragma unroll
     for (int i = 0; i < NF; ++i) da1[i] = 0.f;
 
-    for (int u = blockIdx.x * HSG_WAVES + wid; u < R.n_src; u += gridDim.x * HSG_WAVES) {
+    for (int u_ = blockIdx.x * NPB + wid / WPN; u_ < R.n_src; u_ += gridDim.x * NPB) {
+        const int u = __builtin_amdgcn_readfirstlane(u_);
         const int beg = R.cindptr[u], end = R.cindptr[u + 1];
+        int eb, ee;
+        subrange(beg, end, part, WPN, eb, ee);
         const float sig = kact ? sigma[u * H + k] : 0.f;
+        float zrow[NF];                  // Z row for d a1, issued early
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int f = lane + 64 * i;
+            zrow[i] = (da1_part && writer && f < HD) ? Z[(size_t)u * HD + fo[i]] : 0.f;
+        }
         float dsig = 0.f;
         float acc[NF];
 #pragma unroll
         for (int i = 0; i < NF; ++i) acc[i] = 0.f;
-        for (int cb = beg; cb < end; cb += HSG_CHUNK) {
-            const int n = min(HSG_CHUNK, end - cb);
+        for (int cb = eb; cb < ee; cb += HSG_CHUNK) {
+            const int n = min(HSG_CHUNK, ee - cb);
             if (kact) {
                 for (int j = l; j < n; j += lph) {
                     const int p = cb + j;
@@ -290,35 +511,50 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
                 }
             }
             wave_lds_sync();
-#pragma unroll 4
-            for (int j = 0; j < n; ++j) {
-                const float *gr = G + (size_t)sn[j] * HD;
-#pragma unroll
-                for (int i = 0; i < NF; ++i) {
-                    const int f = lane + 64 * i;
-                    if (f < HD) acc[i] = fmaf(sa[j * H + fh[i]], gr[f], acc[i]);
-                }
-            }
+            gather_rows<NF>(G, HD, n, sn, sa, H, fh, fo, acc);
             wave_lds_sync();
         }
         dsig = group_sum(dsig, lph);
-        if (kact && l == 0) {
-            if (dsigma) dsigma[u * H + k] = dsig;
-            s_dsig[wid][k] = dsig;
+        if (kact && l == 0) s_dsig[wid][k] = dsig;
+        if constexpr (WPN > 1) {
+#pragma unroll
+            for (int i = 0; i < NF; ++i) s_acc[wid][lane + 64 * i] = acc[i];
+            __syncthreads();
+            if (writer) {
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int p = 0; p < WPN; ++p) a += s_acc[w0 + p][lane + 64 * i];
+                    acc[i] = a;
+                }
+                if (kact && l == 0) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int p = 0; p < WPN; ++p) a += s_dsig[w0 + p][k];
+                    s_dsum[wid][k] = a;
+                }
+            }
+        } else {
+            if (kact && l == 0) s_dsum[wid][k] = dsig;
         }
         wave_lds_sync();
+        if (writer) {
+            if (dsigma && kact && l == 0) dsigma[u * H + k] = s_dsum[wid][k];
 #pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            const int f = lane + 64 * i;
-            if (f < HD) {
-                const float ds = s_dsig[wid][fh[i]];
-                float r = acc[i];
-                if (a1) r = fmaf(ds, a1[f], r);
-                dZ[(size_t)u * HD + f] = r;
-                if (da1_part) da1[i] = fmaf(ds, Z[(size_t)u * HD + f], da1[i]);
+            for (int i = 0; i < NF; ++i) {
+                const int f = lane + 64 * i;
+                if (f < HD) {
+                    const float ds = s_dsum[wid][fh[i]];
+                    float r = acc[i];
+                    if (a1) r = fmaf(ds, a1[f], r);
+                    dZ[(size_t)u * HD + f] = r;
+                    if (da1_part) da1[i] = fmaf(ds, zrow[i], da1[i]);
+                }
             }
         }
-        wave_lds_sync();
+        if constexpr (WPN > 1) __syncthreads();
+        else wave_lds_sync();
     }
     if (da1_part) {                      // block partial of d a1 (fixed order: deterministic)
 #pragma unroll
@@ -353,14 +589,20 @@ __global__ __launch_bounds__(256) void k_attn_src_logits(int n, int H, int D, in
 // ------------------------------------------------------------ host helpers ----
 int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 int lanes_per_head(int H) { return 64 / next_pow2(H); }
-int grid_for(int rows, int cap) {
-    int b = (rows + HSG_WAVES - 1) / HSG_WAVES;
-    if (b < 1) b = 1;
-    return b < cap ? b : cap;
-}
 constexpr int kFwdGridCap = 8192;
 constexpr int kBwdDstGridCap = 1024;   // bounds the dtau partial slab
 constexpr int kBwdSrcGridCap = 2048;   // bounds the d a1 partial slab
+constexpr int kLongSegment = 16;       // mean segment length from which 4 waves share a node
+
+// waves per node for a set of n nodes sharing n_edges edges
+int wpn_for(int n, int n_edges) { return n > 0 && n_edges >= kLongSegment * n ? 4 : 1; }
+int grid_nodes(int n, int wpn, int cap) {
+    if (const char *e = getenv("HSG_GAT_CAP")) cap = atoi(e) < cap ? atoi(e) : cap;   // dev sweep
+    int b = wpn == 4 ? n : (n + HSG_WAVES - 1) / HSG_WAVES;
+    if (b < 1) b = 1;
+    return b < cap ? b : cap;
+}
+int grid_for(int rows, int cap) { return grid_nodes(rows, 1, cap); }
 
 bool shape_ok(int H, int D) { return H >= 1 && H <= HSG_HMAX && D >= 1 && H * D <= 512; }
 
@@ -369,20 +611,34 @@ int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int TAU>
+template <int TAU, int WPN>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
                  float *out, float *m, float *l) {
-#define HSG_FWD(NF_)                                                                           \
-    case NF_:                                                                                  \
-        hipLaunchKernelGGL((k_gat_fwd<NF_, TAU>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
-                           sg, tau, org, h, out, m, l);                                        \
+#define HSG_FWD(NF_)                                                                                \
+    case NF_:                                                                                       \
+        hipLaunchKernelGGL((k_gat_fwd<NF_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
+                           sg, tau, org, h, out, m, l);                                             \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
         default: return HSG_EINVAL;
     }
 #undef HSG_FWD
+    return launch_status();
+}
+
+template <int TAU, int WPN>
+int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int lph, int om, float slope,
+                        const float *Z, const float *sg, const float *tau, const float *h, const float *m,
+                        const float *l, const float *dout, float *G, float *dpre, float *dtp) {
+#define HSG_EP(DV_)                                                                                    \
+    hipLaunchKernelGGL((k_gat_bwd_dst_ep<DV_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, om, slope, \
+                       Z, sg, tau, h, m, l, dout, G, dpre, dtp)
+    if (D <= 4) HSG_EP(4);
+    else if (D <= 8) HSG_EP(8);
+    else HSG_EP(16);
+#undef HSG_EP
     return launch_status();
 }
 
@@ -413,14 +669,14 @@ int ne_bucket(int ne) {
     return -1;
 }
 
-template <int TAU>
+template <int TAU, int WPN>
 int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                      const float *sg, const float *tau, const float *m, const float *l, const float *G,
                      const float *dpre, const float *a1, const float *Z, float *dZ, float *dsig, float *da1p) {
-#define HSG_BS(NF_)                                                                               \
-    case NF_:                                                                                     \
-        hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
-                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                        \
+#define HSG_BS(NF_)                                                                                   \
+    case NF_:                                                                                         \
+        hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
+                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                            \
         break;
     switch (nf) {
         HSG_BS(1) HSG_BS(2) HSG_BS(3) HSG_BS(4) HSG_BS(5) HSG_BS(6) HSG_BS(7) HSG_BS(8)
@@ -430,6 +686,10 @@ int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
     return launch_status();
 }
 
+// dst-side launch shape (fwd and bwd_dst share it; the d tau slab has one row per block)
+int dst_wpn(const hsg_rel *r) { return wpn_for(r->n_dst, r->n_edges); }
+int src_wpn(const hsg_rel *r) { return wpn_for(r->n_src, r->n_edges); }
+
 }  // namespace
 
 extern "C" {
@@ -438,30 +698,32 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
                 const float *sigma, const float *tau, const float *origin, float *h, float *out,
                 float *m, float *l, void *stream) {
     if (!rel || !shape_ok(H, D) || (origin && !out)) return HSG_EINVAL;
+    if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     if (rel->n_dst == 0) return 0;
     const RelPtrs R = rel_ptrs(rel);
     const int nf = (H * D + 63) / 64;
-    const dim3 grid(grid_for(rel->n_dst, kFwdGridCap));
+    const int wpn = dst_wpn(rel);
+    const dim3 grid(grid_nodes(rel->n_dst, wpn, kFwdGridCap));
     hipStream_t st = (hipStream_t)stream;
-    if (tau_mode == HSG_TAU_TABLE)
-        return fwd_dispatch<HSG_TAU_TABLE>(nf, grid, st, R, H, D, lanes_per_head(H), slope, Z, sigma,
-                                           tau, origin, h, out, m, l);
-    if (tau_mode == HSG_TAU_PER_EDGE)
-        return fwd_dispatch<HSG_TAU_PER_EDGE>(nf, grid, st, R, H, D, lanes_per_head(H), slope, Z,
-                                              sigma, tau, origin, h, out, m, l);
-    return HSG_EINVAL;
+    const int lph = lanes_per_head(H);
+#define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
+    if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_F(HSG_TAU_TABLE, 4) : HSG_F(HSG_TAU_TABLE, 1);
+    return wpn == 4 ? HSG_F(HSG_TAU_PER_EDGE, 4) : HSG_F(HSG_TAU_PER_EDGE, 1);
+#undef HSG_F
 }
 
-int hsg_gat_bwd_blocks(const hsg_rel *rel) { return rel ? grid_for(rel->n_dst, kBwdDstGridCap) : 0; }
+int hsg_gat_bwd_blocks(const hsg_rel *rel) {
+    if (!rel) return 0;
+    return grid_nodes(rel->n_dst, dst_wpn(rel), kBwdDstGridCap);
+}
 
 int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_mode, float slope,
                     const float *Z, const float *sigma, const float *tau, const float *h,
                     const float *m, const float *l, const float *dout, float *G, float *dpre,
                     float *dtau_part, void *stream) {
     if (!rel || !shape_ok(H, D)) return HSG_EINVAL;
+    if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     const int lph = lanes_per_head(H);
-    const int ne = ne_bucket((D + lph - 1) / lph);
-    if (ne < 0) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
     const dim3 grid(hsg_gat_bwd_blocks(rel));
     hipStream_t st = (hipStream_t)stream;
@@ -470,22 +732,36 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
             return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
         return 0;
     }
+    const int wpn = dst_wpn(rel);
+    if (D <= 16) {                       // edge-parallel: whole G_v,k per lane
+#define HSG_E(TAU, W) bwd_dst_ep_dispatch<TAU, W>(D, grid, st, R, H, lph, origin_mode, slope, Z, sigma, tau, h, \
+                                                  m, l, dout, G, dpre, dtau_part)
+        if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_E(HSG_TAU_TABLE, 4) : HSG_E(HSG_TAU_TABLE, 1);
+        return wpn == 4 ? HSG_E(HSG_TAU_PER_EDGE, 4) : HSG_E(HSG_TAU_PER_EDGE, 1);
+#undef HSG_E
+    }
+    // feature-split variant (one wave per destination; with long segments it runs on
+    // the same grid as above, the d tau slab's row count, with some idle waves)
+    const int ne = ne_bucket((D + lph - 1) / lph);
+    if (ne < 0) return HSG_EINVAL;
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
                                                tau, h, m, l, dout, G, dpre, dtau_part);
-    if (tau_mode == HSG_TAU_PER_EDGE)
-        return bwd_dst_dispatch<HSG_TAU_PER_EDGE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
-                                                  sigma, tau, h, m, l, dout, G, dpre, dtau_part);
-    return HSG_EINVAL;
+    return bwd_dst_dispatch<HSG_TAU_PER_EDGE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
+                                              sigma, tau, h, m, l, dout, G, dpre, dtau_part);
 }
 
-int hsg_gat_bwd_src_blocks(const hsg_rel *rel) { return rel ? grid_for(rel->n_src, kBwdSrcGridCap) : 0; }
+int hsg_gat_bwd_src_blocks(const hsg_rel *rel) {
+    if (!rel) return 0;
+    return grid_nodes(rel->n_src, src_wpn(rel), kBwdSrcGridCap);
+}
 
 int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *sigma,
                     const float *tau, const float *m, const float *l, const float *G,
                     const float *dpre, const float *a1, const float *Z, float *dZ, float *dsigma,
                     float *da1_part, void *stream) {
     if (!rel || !shape_ok(H, D) || (da1_part && !Z)) return HSG_EINVAL;
+    if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
     const int nf = (H * D + 63) / 64;
     const dim3 grid(hsg_gat_bwd_src_blocks(rel));
@@ -494,13 +770,12 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
         if (da1_part) return (int)hipMemsetAsync(da1_part, 0, sizeof(float) * H * D * grid.x, st);
         return 0;
     }
-    if (tau_mode == HSG_TAU_TABLE)
-        return bwd_src_dispatch<HSG_TAU_TABLE>(nf, grid, st, R, H, D, lanes_per_head(H), slope, sigma,
-                                               tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
-    if (tau_mode == HSG_TAU_PER_EDGE)
-        return bwd_src_dispatch<HSG_TAU_PER_EDGE>(nf, grid, st, R, H, D, lanes_per_head(H), slope,
-                                                  sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
-    return HSG_EINVAL;
+    const int wpn = src_wpn(rel), lph = lanes_per_head(H);
+#define HSG_S(TAU, W) bwd_src_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G, dpre, a1, \
+                                               Z, dZ, dsigma, da1_part)
+    if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_S(HSG_TAU_TABLE, 4) : HSG_S(HSG_TAU_TABLE, 1);
+    return wpn == 4 ? HSG_S(HSG_TAU_PER_EDGE, 4) : HSG_S(HSG_TAU_PER_EDGE, 1);
+#undef HSG_S
 }
 
 int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,
