@@ -10,7 +10,8 @@
 //   tau[t][k] = <a3_k, W_f,k T[t] + b_f,k>   (t < 10),   tau[10][k] = <a3_k, b_f,k>
 // hsg_attn_params_fwd builds that table (and a contiguous copy of a1 for the
 // sigma kernel); hsg_attn_params_bwd reduces the per-block partials the edge
-// kernels wrote (d tau, d a1) and produces every parameter gradient:
+// kernels wrote (d tau, d a1; a 64-range stage kernel, then one workgroup per
+// head plus one for dT) and produces every parameter gradient:
 //   v[k][f]   = sum_d a3[k][d] W_f[k][d][f]
 //   dv[k][f]  = sum_{t<10} dtau[t][k] T[t][f],   dc[k] = sum_{t<=10} dtau[t][k]
 //   dT[t][f]  = sum_k dtau[t][k] v[k][f]
@@ -30,41 +31,63 @@ constexpr int kHMax = 16;
 constexpr int kFMax = 256;
 constexpr int kDMax = 512;     // H*D bound of the edge kernels
 
-__global__ __launch_bounds__(1024) void k_attn_params_fwd(int H, int D, int F, const float *__restrict__ attn,
+constexpr int kWfLds = 8192;   // head slice W_f,k [D][F] staged in LDS when it fits
+
+// v_k[f] = sum_d a3_k[d] W_f,k[d][f] for one head, all f (threads over f), with
+// W_f,k staged in LDS (coalesced fill) when D*F fits, else read from global.
+__device__ void head_v(int k, int D, int F, const float *__restrict__ attn, const float *__restrict__ wf,
+                       float *wlds, float *a3s, float *vout) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const float *wk = wf + (size_t)k * D * F;
+    const bool staged = D * F <= kWfLds;
+    __syncthreads();
+    if (staged)
+        for (int i = tid; i < D * F; i += nt) wlds[i] = wk[i];
+    for (int d = tid; d < D; d += nt) a3s[d] = attn[k * 3 * D + 2 * D + d];
+    __syncthreads();
+    const float *W = staged ? wlds : wk;
+    for (int f = tid; f < F; f += nt) {
+        float s = 0.f;
+        for (int d = 0; d < D; ++d) s = fmaf(a3s[d], W[d * F + f], s);
+        vout[f] = s;
+    }
+    __syncthreads();
+}
+
+// one workgroup per head k: v_k (W_f,k staged in LDS), then tau[:, k]; block 0
+// also writes the contiguous a1 copy
+__global__ __launch_bounds__(256) void k_attn_params_fwd(int H, int D, int F, const float *__restrict__ attn,
                                                          const float *__restrict__ wf,
                                                          const float *__restrict__ bf,
                                                          const float *__restrict__ T, float *__restrict__ a1,
                                                          float *__restrict__ tau) {
-    __shared__ float v[kHMax * kFMax];
-    __shared__ float c[kHMax];
-    const int tid = threadIdx.x;
-    const int D3 = 3 * D;
-    for (int i = tid; i < H * F; i += blockDim.x) {
-        const int k = i / F, f = i - (i / F) * F;
-        float s = 0.f;
-        #pragma unroll 8
-        for (int d = 0; d < D; ++d) s = fmaf(attn[k * D3 + 2 * D + d], wf[((size_t)k * D + d) * F + f], s);
-        v[i] = s;
-    }
-    for (int k = tid; k < H; k += blockDim.x) {
-        float s = 0.f;
-        if (bf)
-            #pragma unroll 8
-            for (int d = 0; d < D; ++d) s = fmaf(attn[k * D3 + 2 * D + d], bf[k * D + d], s);
-        c[k] = s;
-    }
-    for (int i = tid; i < H * D; i += blockDim.x) {
-        const int k = i / D, d = i - (i / D) * D;
-        a1[i] = attn[k * D3 + d];
-    }
-    __syncthreads();
-    for (int i = tid; i < kNT * H; i += blockDim.x) {
-        const int t = i / H, k = i - (i / H) * H;
+    __shared__ float wlds[kWfLds];
+    __shared__ float a3s[kDMax];
+    __shared__ float v[kFMax];
+    __shared__ float part[kNT][33];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int k = blockIdx.x;
+    if (k == 0)
+        for (int i = tid; i < H * D; i += nt) {
+            const int kk = i / D, d = i - (i / D) * D;
+            a1[i] = attn[kk * 3 * D + d];
+        }
+    head_v(k, D, F, attn, wf, wlds, a3s, v);
+    // tau[t][k] = <T[t], v_k> + <a3_k, bf_k>: 11 rows x 32 lanes, fixed-order sums
+    const int ln = tid & 31;
+    for (int t = tid >> 5; t < kNT; t += nt >> 5) {
         float s = 0.f;
         if (t < kNT - 1)
-            #pragma unroll 8
-            for (int f = 0; f < F; ++f) s = fmaf(T[t * F + f], v[k * F + f], s);
-        tau[i] = s + c[k];
+            for (int f = ln; f < F; f += 32) s = fmaf(T[t * F + f], v[f], s);
+        if (bf)
+            for (int d = ln; d < D; d += 32) s = fmaf(a3s[d], bf[k * D + d], s);
+        part[t][ln] = s;
+    }
+    __syncthreads();
+    if (tid < kNT) {
+        float s = 0.f;
+        for (int q = 0; q < 32; ++q) s += part[tid][q];
+        tau[tid * H + k] = s;
     }
 }
 
@@ -95,85 +118,83 @@ __global__ __launch_bounds__(256) void k_colsum_stage(int rows0, int cols0, cons
     }
 }
 
-// column sums of a [rows][cols] partial slab (cols <= blockDim.x) with the whole
-// block: thread (g, c) sums rows g, g+ng, ... of column c, then the ng partials
-// are added in g order -- a fixed order, so the result is deterministic.
-__device__ void colsum(const float *__restrict__ part, int rows, int cols, float *out, float *scratch) {
-    const int tid = threadIdx.x;
-    const int ng = blockDim.x / cols;
-    const int g = tid / cols, c = tid - (tid / cols) * cols;
-    if (g < ng) {
-        float s = 0.f;
-        for (int r = g; r < rows; r += ng) s += part[(size_t)r * cols + c];
-        scratch[tid] = s;
-    }
-    __syncthreads();
-    for (int i = tid; i < cols; i += blockDim.x) {
-        float a = 0.f;
-        for (int q = 0; q < ng; ++q) a += scratch[q * cols + i];
-        out[i] = a;
-    }
-    __syncthreads();
-}
-
-__global__ __launch_bounds__(1024) void k_attn_params_bwd(int H, int D, int F, int nbd,
-                                                          const float *__restrict__ dtau_part, int nbs,
-                                                          const float *__restrict__ da1_part,
-                                                          const float *__restrict__ attn,
-                                                          const float *__restrict__ wf,
-                                                          const float *__restrict__ bf,
-                                                          const float *__restrict__ T, float *__restrict__ dattn,
-                                                          float *__restrict__ dwf, float *__restrict__ dbf,
-                                                          float *__restrict__ dT) {
-    __shared__ float scratch[1024];
+// blocks 0..H-1: one head each (d attn row, dW_f,k, db_f,k); block H: dT
+__global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
+                                                         const float *__restrict__ dtau_st,   // [kStage][11*H]
+                                                         const float *__restrict__ da1_st,    // [kStage][H*D]
+                                                         const float *__restrict__ attn,
+                                                         const float *__restrict__ wf,
+                                                         const float *__restrict__ bf,
+                                                         const float *__restrict__ T, float *__restrict__ dattn,
+                                                         float *__restrict__ dwf, float *__restrict__ dbf,
+                                                         float *__restrict__ dT) {
+    __shared__ float wlds[kWfLds];
+    __shared__ float a3s[kDMax];
+    __shared__ float dv[kFMax];
     __shared__ float dtau[kNT * kHMax];
-    __shared__ float da1[kDMax];
-    __shared__ float v[kHMax * kFMax];
-    __shared__ float dv[kHMax * kFMax];
-    __shared__ float dc[kHMax];
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int D3 = 3 * D;
-    colsum(dtau_part, nbd, kNT * H, dtau, scratch);       // nbd, nbs = kStage (stage-1 rows)
-    colsum(da1_part, nbs, H * D, da1, scratch);
-    for (int i = tid; i < H * F; i += nt) {
-        const int k = i / F, f = i - (i / F) * F;
-        float s = 0.f, t = 0.f;
-        #pragma unroll 8
-        for (int d = 0; d < D; ++d) s = fmaf(attn[k * D3 + 2 * D + d], wf[((size_t)k * D + d) * F + f], s);
-        #pragma unroll 8
-        for (int r = 0; r < kNT - 1; ++r) t = fmaf(dtau[r * H + k], T[r * F + f], t);
-        v[i] = s;
-        dv[i] = t;
-    }
-    for (int k = tid; k < H; k += nt) {
+    const int NTH = kNT * H;
+    // d tau [11][H], summed over the stage rows in order
+    for (int i = tid; i < NTH; i += nt) {
         float s = 0.f;
-        for (int r = 0; r < kNT; ++r) s += dtau[r * H + k];
-        dc[k] = s;
+#pragma unroll 16
+        for (int r = 0; r < kStage; ++r) s += dtau_st[r * NTH + i];
+        dtau[i] = s;
     }
     __syncthreads();
-    for (int i = tid; i < (kNT - 1) * F; i += nt) {
-        const int r = i / F, f = i - (i / F) * F;
-        float s = 0.f;
-        for (int k = 0; k < H; ++k) s = fmaf(dtau[r * H + k], v[k * F + f], s);
-        dT[i] = s;
-    }
-    for (int i = tid; i < H * D; i += nt) {
-        const int k = i / D, d = i - (i / D) * D;
-        const float a3 = attn[k * D3 + 2 * D + d];
-        float s = 0.f;
-        #pragma unroll 8
-        for (int f = 0; f < F; ++f) s = fmaf(dv[k * F + f], wf[((size_t)k * D + d) * F + f], s);
-        if (bf) {
-            s = fmaf(dc[k], bf[k * D + d], s);
-            if (dbf) dbf[i] = a3 * dc[k];
+    const int k = blockIdx.x;
+    if (k == H) {                                  // dT[t][f] = sum_k dtau[t][k] v_k[f]
+        float *vall = wlds;                        // [H][F] (H*F <= 16*256 <= kWfLds)
+        for (int i = tid; i < H * F; i += nt) {
+            const int kk = i / F, f = i - (i / F) * F;
+            const float *wk = wf + (size_t)kk * D * F;
+            float s = 0.f;
+#pragma unroll 8
+            for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
+            vall[i] = s;
         }
-        dattn[k * D3 + d] = da1[i];
+        __syncthreads();
+        for (int i = tid; i < (kNT - 1) * F; i += nt) {
+            const int t = i / F, f = i - (i / F) * F;
+            float s = 0.f;
+            for (int kk = 0; kk < H; ++kk) s = fmaf(dtau[t * H + kk], vall[kk * F + f], s);
+            dT[i] = s;
+        }
+        return;
+    }
+    // head k
+    const float *wk = wf + (size_t)k * D * F;
+    const bool staged = D * F <= kWfLds;
+    if (staged)
+        for (int i = tid; i < D * F; i += nt) wlds[i] = wk[i];
+    for (int d = tid; d < D; d += nt) a3s[d] = attn[k * 3 * D + 2 * D + d];
+    for (int f = tid; f < F; f += nt) {
+        float s = 0.f;
+        for (int t = 0; t < kNT - 1; ++t) s = fmaf(dtau[t * H + k], T[t * F + f], s);
+        dv[f] = s;
+    }
+    float dc = 0.f;
+    for (int t = 0; t < kNT; ++t) dc += dtau[t * H + k];
+    __syncthreads();
+    const float *W = staged ? wlds : wk;
+    const int D3 = 3 * D;
+    for (int d = tid; d < D; d += nt) {
+        float s = 0.f;
+        for (int f = 0; f < F; ++f) s = fmaf(dv[f], W[d * F + f], s);
+        if (bf) {
+            s = fmaf(dc, bf[k * D + d], s);
+            if (dbf) dbf[k * D + d] = a3s[d] * dc;
+        }
+        float g = 0.f;                             // d a1: stage rows in order
+#pragma unroll 16
+        for (int r = 0; r < kStage; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
+        dattn[k * D3 + d] = g;
         dattn[k * D3 + D + d] = 0.f;
         dattn[k * D3 + 2 * D + d] = s;
     }
-    for (int i = tid; i < H * D * F; i += nt) {
-        const int f = i % F, kd = i / F, k = kd / D;
-        dwf[i] = attn[k * D3 + 2 * D + (kd - k * D)] * dv[k * F + f];
+    for (int i = tid; i < D * F; i += nt) {
+        const int d = i / F, f = i - (i / F) * F;
+        dwf[(size_t)k * D * F + i] = a3s[d] * dv[f];
     }
 }
 
@@ -191,7 +212,7 @@ extern "C" {
 int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf, const float *bf, const float *T,
                         float *a1, float *tau, void *stream) {
     if (!dims_ok(H, D, F) || !attn || !wf || !T || !a1 || !tau) return HSG_EINVAL;
-    hipLaunchKernelGGL(k_attn_params_fwd, dim3(1), dim3(1024), 0, (hipStream_t)stream, H, D, F, attn, wf, bf, T,
+    hipLaunchKernelGGL(k_attn_params_fwd, dim3(H), dim3(256), 0, (hipStream_t)stream, H, D, F, attn, wf, bf, T,
                        a1, tau);
     return status();
 }
@@ -210,8 +231,8 @@ int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_
                        n_da1_part, H * D, da1_part, s0, s1);
     int rc = status();
     if (rc) return rc;
-    hipLaunchKernelGGL(k_attn_params_bwd, dim3(1), dim3(1024), 0, st, H, D, F, kStage, s0, kStage, s1, attn, wf,
-                       bf, T, dattn, dwf, dbf, dT);
+    hipLaunchKernelGGL(k_attn_params_bwd, dim3(H + 1), dim3(256), 0, st, H, D, F, s0, s1, attn, wf, bf, T, dattn,
+                       dwf, dbf, dT);
     return status();
 }
 

@@ -52,6 +52,7 @@ struct GemmArgs {
     int relu;
     int k_tiles_per_split;
     float *ws;            // split-K partials [splits][M][N]
+    float *colpart;       // optional: per-block-row column sums of C, [ceil(M/BM)][N]
 };
 
 __device__ __forceinline__ float epi_apply(float v, int m, int n, const GemmArgs &p) {
@@ -62,22 +63,22 @@ __device__ __forceinline__ float epi_apply(float v, int m, int n, const GemmArgs
     return v;
 }
 
-template <bool KC, int ROWS>
+template <bool KC, int ROWS, int BK>
 struct Stage {
     // one operand tile: KC -> [ROWS x 32] from rows of a K-contiguous matrix;
     // !KC -> [32 x ROWS] from 32 rows of a ROWS-contiguous matrix
-    static constexpr int LD = KC ? (kBK + kPad) : (ROWS + kPad);
-    static constexpr int NV = ROWS * kBK / 4 / 256;   // float4 per thread
+    static constexpr int LD = KC ? (BK + kPad) : (ROWS + kPad);
+    static constexpr int NV = ROWS * BK / 4 / 256;   // float4 per thread
     f32x4 v[NV];
 
     __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int r0, int nr, int k0, int nk) {
-        const bool full = KC ? (r0 + ROWS <= nr && k0 + kBK <= nk) : (k0 + kBK <= nk && r0 + ROWS <= nr);
+        const bool full = KC ? (r0 + ROWS <= nr && k0 + BK <= nk) : (k0 + BK <= nk && r0 + ROWS <= nr);
         if (full) {
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
                 const int idx = threadIdx.x + 256 * i;
                 int row, col;
-                if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+                if constexpr (KC) { row = idx / (BK / 4); col = (idx % (BK / 4)) * 4; }
                 else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
                 const int gr = KC ? r0 + row : k0 + row;
                 const int gc = KC ? k0 + col : r0 + col;
@@ -89,7 +90,7 @@ struct Stage {
         for (int i = 0; i < NV; ++i) {
             const int idx = threadIdx.x + 256 * i;
             int row, col;   // row in the "major" dimension of global memory, col contiguous
-            if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+            if constexpr (KC) { row = idx / (BK / 4); col = (idx % (BK / 4)) * 4; }
             else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
             const int gr = KC ? r0 + row : k0 + row;          // global row
             const int gc = KC ? k0 + col : r0 + col;          // global col
@@ -114,7 +115,7 @@ struct Stage {
         for (int i = 0; i < NV; ++i) {
             const int idx = threadIdx.x + 256 * i;
             int row, col;
-            if constexpr (KC) { row = idx / (kBK / 4); col = (idx % (kBK / 4)) * 4; }
+            if constexpr (KC) { row = idx / (BK / 4); col = (idx % (BK / 4)) * 4; }
             else { row = idx / (ROWS / 4); col = (idx % (ROWS / 4)) * 4; }
             *reinterpret_cast<f32x4 *>(s + row * LD + col) = v[i];
         }
@@ -124,21 +125,21 @@ struct Stage {
 // NBUF = 2: register-staged double buffer in LDS, one barrier per K tile.
 // NBUF = 1: one LDS buffer (half the LDS, twice the resident blocks), the next
 // tile still prefetched into registers, two barriers per K tile.
-template <int BM, int BN, bool AK, bool BKC, int NBUF>
+template <int BM, int BN, bool AK, bool BKC, int NBUF, int BK>
 __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 32, TN = WN / 32;
-    using SA = Stage<AK, BM>;
-    using SB = Stage<BKC, BN>;
-    __shared__ __attribute__((aligned(16))) float sA[NBUF][AK ? BM * SA::LD : kBK * SA::LD];
-    __shared__ __attribute__((aligned(16))) float sB[NBUF][BKC ? BN * SB::LD : kBK * SB::LD];
+    using SA = Stage<AK, BM, BK>;
+    using SB = Stage<BKC, BN, BK>;
+    __shared__ __attribute__((aligned(16))) float sA[NBUF][AK ? BM * SA::LD : BK * SA::LD];
+    __shared__ __attribute__((aligned(16))) float sB[NBUF][BKC ? BN * SB::LD : BK * SB::LD];
 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     const int li = lane & 31, h = lane >> 5;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
 
-    const int kt_total = (p.K + kBK - 1) / kBK;
+    const int kt_total = (p.K + BK - 1) / BK;
     const int kt0 = blockIdx.z * p.k_tiles_per_split;
     const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
 
@@ -154,8 +155,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     SB rb;
     int cur = 0;
     if (kt0 < kt1) {
-        ra.load(p.A, p.lda, m0, p.M, kt0 * kBK, p.K);
-        rb.load(p.B, p.ldb, n0, p.N, kt0 * kBK, p.K);
+        ra.load(p.A, p.lda, m0, p.M, kt0 * BK, p.K);
+        rb.load(p.B, p.ldb, n0, p.N, kt0 * BK, p.K);
         ra.store(sA[0]);
         rb.store(sB[0]);
     }
@@ -163,8 +164,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     for (int kt = kt0; kt < kt1; ++kt) {
         const bool more = kt + 1 < kt1;
         if (more) {
-            ra.load(p.A, p.lda, m0, p.M, (kt + 1) * kBK, p.K);
-            rb.load(p.B, p.ldb, n0, p.N, (kt + 1) * kBK, p.K);
+            ra.load(p.A, p.lda, m0, p.M, (kt + 1) * BK, p.K);
+            rb.load(p.B, p.ldb, n0, p.N, (kt + 1) * BK, p.K);
         }
         const float *a_s = sA[NBUF == 2 ? cur : 0];
         const float *b_s = sB[NBUF == 2 ? cur : 0];
@@ -174,27 +175,27 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
             for (int i = 0; i < TM; ++i) {
                 const int row = wm * WM + i * 32 + li;
                 if constexpr (AK) {
-                    fa[i] = *reinterpret_cast<const f32x4 *>(a_s + row * SA::LD + h * (kBK / 2) + s4);
+                    fa[i] = *reinterpret_cast<const f32x4 *>(a_s + row * SA::LD + h * (BK / 2) + s4);
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) fa[i][q] = a_s[(h * (kBK / 2) + s4 + q) * SA::LD + row];
+                    for (int q = 0; q < 4; ++q) fa[i][q] = a_s[(h * (BK / 2) + s4 + q) * SA::LD + row];
                 }
             }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = wn * WN + j * 32 + li;
                 if constexpr (BKC) {
-                    fb[j] = *reinterpret_cast<const f32x4 *>(b_s + col * SB::LD + h * (kBK / 2) + s4);
+                    fb[j] = *reinterpret_cast<const f32x4 *>(b_s + col * SB::LD + h * (BK / 2) + s4);
                 } else {
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) fb[j][q] = b_s[(h * (kBK / 2) + s4 + q) * SB::LD + col];
+                    for (int q = 0; q < 4; ++q) fb[j][q] = b_s[(h * (BK / 2) + s4 + q) * SB::LD + col];
                 }
             }
         };
         frag(af[0], bf[0], 0);
 #pragma unroll
-        for (int g = 0; g < kBK / 8; ++g) {
-            if (g + 1 < kBK / 8) frag(af[(g + 1) & 1], bf[(g + 1) & 1], 4 * (g + 1));
+        for (int g = 0; g < BK / 8; ++g) {
+            if (g + 1 < BK / 8) frag(af[(g + 1) & 1], bf[(g + 1) & 1], 4 * (g + 1));
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -223,6 +224,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
 
     // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
     const bool split = gridDim.z > 1;
+    float csum[TN];                       // column sums of this wave's stored values (colpart)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) csum[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -233,10 +237,31 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
             for (int r = 0; r < 16; ++r) {
                 const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m >= p.M) continue;
-                if (split) p.ws[((size_t)blockIdx.z * p.M + m) * p.N + n] = acc[i][j][r];
-                else p.C[(size_t)m * p.ldc + n] = epi_apply(acc[i][j][r], m, n, p);
+                if (split) {
+                    p.ws[((size_t)blockIdx.z * p.M + m) * p.N + n] = acc[i][j][r];
+                } else {
+                    const float v = epi_apply(acc[i][j][r], m, n, p);
+                    p.C[(size_t)m * p.ldc + n] = v;
+                    csum[j] += v;
+                }
             }
         }
+    if (p.colpart && !split) {           // block-uniform: fixed-order block partial per column
+        // lanes li and li+32 hold the two row halves of the same column
+#pragma unroll
+        for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
+        __syncthreads();                  // the tiles in LDS are no longer read
+        float *red = sA[0];
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + li] = csum[j];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < BN; c += 256) {
+            const int n = n0 + c;
+            if (n < p.N) p.colpart[(size_t)blockIdx.y * p.N + n] = red[c] + red[BN + c];
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
@@ -250,13 +275,15 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
     }
 }
 
-template <int BM, int BN, int NBUF = 2>
-int launch_tiles(const GemmArgs &p, bool ak, bool bk, int splits, hipStream_t st) {
+template <int BM, int BN, int NBUF = 2, int BK = kBK>
+int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
+    const int kt_total = (p.K + BK - 1) / BK;
+    p.k_tiles_per_split = (kt_total + splits - 1) / splits;
     dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
-    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF>), grid, dim3(256), 0, st, p);
-    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF>), grid, dim3(256), 0, st, p);
-    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false, NBUF>), grid, dim3(256), 0, st, p);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF, BK>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF, BK>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false, NBUF, BK>), grid, dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -295,9 +322,16 @@ size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits) {
     return splits > 1 ? (size_t)splits * M * N : 0;
 }
 
+int hsg_gemm_row_tiles(int M, int N, int K, int splits) {
+    if (splits == 0) splits = plan_splits(M, N, K);
+    const int t = plan_tile(M, N, K, splits < 1 ? 1 : splits);
+    const int bm = (t == 0 || t == 1 || t == 3 || t == 4 || t == 7 || t == 9) ? 128 : 64;
+    return (M + bm - 1) / bm;
+}
+
 int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
                  int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
-                 int relu, int splits, float *workspace, void *stream) {
+                 int relu, int splits, float *workspace, float *colsum_part, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
@@ -310,18 +344,24 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     if (splits < 1) splits = 1;
     if (splits > kt_total) splits = kt_total > 0 ? kt_total : 1;
     if (splits > 1 && !workspace) return HSG_EINVAL;
+    if (splits > 1 && colsum_part) return HSG_EINVAL;     // column partials need the unsplit epilogue
     GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
-               (kt_total + splits - 1) / splits, workspace};
+               (kt_total + splits - 1) / splits, workspace, colsum_part};
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
     int best = plan_tile(M, N, K, splits);
-    if (const char *f = getenv("HSG_GEMM_TILE")) best = atoi(f);   // dev override (tools/gemm_sweep.py)
+    if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
+        if (!colsum_part) best = atoi(f);
     int rc;
     if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
     else if (best == 1) rc = launch_tiles<128, 64>(p, ak, bk, splits, st);
     else if (best == 2) rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
     else if (best == 3) rc = launch_tiles<128, 128, 1>(p, ak, bk, splits, st);
     else if (best == 4) rc = launch_tiles<128, 64, 1>(p, ak, bk, splits, st);
-    else rc = launch_tiles<64, 64, 1>(p, ak, bk, splits, st);
+    else if (best == 5) rc = launch_tiles<64, 64, 1>(p, ak, bk, splits, st);
+    else if (best == 6) rc = launch_tiles<64, 64, 1, 64>(p, ak, bk, splits, st);
+    else if (best == 7) rc = launch_tiles<128, 64, 1, 64>(p, ak, bk, splits, st);
+    else if (best == 8) rc = launch_tiles<64, 64, 2, 64>(p, ak, bk, splits, st);
+    else rc = launch_tiles<128, 128, 1, 64>(p, ak, bk, splits, st);
     if (rc || splits == 1) return rc;
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);

@@ -64,7 +64,11 @@ __device__ __forceinline__ u32x4v bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 }
 
 // one thread = (head pair, 32-row word, column c); c fastest so stores coalesce.
-// Columns in [in, LDC) get zero words.
+// Columns in [in, LDC) get zero words.  The thread's 64 16-bit uniforms (32 rows
+// x 2 heads) come from one lowbias32 hash of (key, word index) that seeds a
+// xorshift64 stream (shifts and xors only: 32-bit integer multiplies run at a
+// quarter of the VALU rate on CDNA, and one hash per word instead of per row
+// removes most of them).
 __global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p, const int64_t *seedp,
                                                   uint32_t offset, uint32_t *__restrict__ bits) {
     const int NWI = (n + 31) / 32;
@@ -82,13 +86,26 @@ __global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p,
         const int kp = (int)(r / NWI);
         uint32_t b0 = 0, b1 = 0;
         if (c < in) {
-#pragma unroll 8
-            for (int j = 0; j < 32; ++j) {
-                const int i = iw * 32 + j;
-                if (i >= n) break;
-                const uint32_t h = lowbias32(key ^ ((uint32_t)(((long)i * in + c) * HP + kp) * 0x9E3779B1u));
-                b0 |= (uint32_t)((h & 0xFFFFu) >= thr) << j;
-                b1 |= (uint32_t)((h >> 16) >= thr) << j;
+            const uint32_t w = (uint32_t)(((long)kp * NWI + iw) * in + c);
+            uint64_t x = ((uint64_t)lowbias32(key ^ (w * 0x9E3779B1u)) << 32) |
+                         lowbias32(key + 0x7F4A7C15u + w * 0x85EBCA6Bu);
+            x |= 1ull;                                     // xorshift state must be non-zero
+            const int jmax = min(32, n - iw * 32);
+#pragma unroll
+            for (int j0 = 0; j0 < 32; j0 += 2) {
+                x ^= x << 13;
+                x ^= x >> 7;
+                x ^= x << 17;
+                // 4 x 16 bits: rows j0, j0+1 for heads 2kp, 2kp+1
+                const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+                if (j0 < jmax) {
+                    b0 |= (uint32_t)((lo & 0xFFFFu) >= thr) << j0;
+                    b1 |= (uint32_t)((lo >> 16) >= thr) << j0;
+                }
+                if (j0 + 1 < jmax) {
+                    b0 |= (uint32_t)((hi & 0xFFFFu) >= thr) << (j0 + 1);
+                    b1 |= (uint32_t)((hi >> 16) >= thr) << (j0 + 1);
+                }
             }
         }
         const int k0 = 2 * kp;

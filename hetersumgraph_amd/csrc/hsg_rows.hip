@@ -163,6 +163,40 @@ __global__ __launch_bounds__(256) void k_ln_bwd(int n, int d, const float *__res
     }
 }
 
+// Column sums of up to two [rows][cols] partial slabs in one launch (block-row
+// partials of the FFN: GEMM colsum_part and hsg_ln_bwd's part).  Block =
+// (32 columns) x (8 row groups); group g sums rows g, g+8, ... in order, then
+// the 8 group sums are added in order -> deterministic.
+__global__ __launch_bounds__(256) void k_colsum2(int rows0, int cols0, const float *__restrict__ p0,
+                                                 float *__restrict__ o0, int rows1, int cols1,
+                                                 const float *__restrict__ p1, float *__restrict__ o1, int nb0) {
+    __shared__ float red[8][33];
+    const bool second = (int)blockIdx.x >= nb0;
+    const int rows = second ? rows1 : rows0, cols = second ? cols1 : cols0;
+    const float *P = second ? p1 : p0;
+    float *O = second ? o1 : o0;
+    const int cb = (second ? (int)blockIdx.x - nb0 : (int)blockIdx.x) * 32;
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = cb + cl;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < cols) {
+        int r = g;
+        for (; r + 24 < rows; r += 32) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s[q] += P[(size_t)(r + 8 * q) * cols + c];
+        }
+        for (; r < rows; r += 8) s[0] += P[(size_t)r * cols + c];
+    }
+    red[g][cl] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (g == 0 && c < cols) {
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += red[q][cl];
+        O[c] = a;
+    }
+}
+
 int grid_rows(int n, int cap) {
     int b = (n + 3) / 4;
     if (b < 1) b = 1;
@@ -216,6 +250,17 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
         break;
     switch (npl) { HSG_LNB(1) HSG_LNB(2) HSG_LNB(3) HSG_LNB(4) HSG_LNB(5) HSG_LNB(6) HSG_LNB(7) HSG_LNB(8) }
 #undef HSG_LNB
+    return status();
+}
+
+int hsg_colsum2(int rows0, int cols0, const float *part0, float *out0, int rows1, int cols1, const float *part1,
+                float *out1, void *stream) {
+    if (rows0 < 0 || cols0 < 0 || rows1 < 0 || cols1 < 0) return HSG_EINVAL;
+    if ((cols0 && (!part0 || !out0)) || (cols1 && (!part1 || !out1))) return HSG_EINVAL;
+    const int nb0 = (cols0 + 31) / 32, nb1 = (cols1 + 31) / 32;
+    if (nb0 + nb1 == 0) return 0;
+    hipLaunchKernelGGL(k_colsum2, dim3(nb0 + nb1), dim3(256), 0, (hipStream_t)stream, rows0, cols0, part0, out0,
+                       rows1, cols1, part1, out1, nb0);
     return status();
 }
 

@@ -20,11 +20,13 @@ def _ld(t):
 
 
 def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=None, add=None,
-         splits=0, workspace=None):
+         splits=0, workspace=None, colsum_part=None):
     """C = op(A) @ op(B) [+ bias] [relu] | * (relu_mask > 0) | + add.
 
     A [M,K] (or [K,M] with a_t), B [K,N] (or [N,K] with b_t), fp32 on the GPU.
-    ``add`` may be ``out`` itself (accumulate)."""
+    ``add`` may be ``out`` itself (accumulate).  ``colsum_part``: a tensor of
+    ``row_tiles(M, N, K) * N`` floats that receives per-tile-row column sums of C
+    (unsplit GEMMs)."""
     lib = load()
     if not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
         raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
@@ -41,19 +43,24 @@ def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=
         epi, aux = HSG_EPI_ADD, add
     ws = None
     if splits == 0:
-        splits = auto_splits(M, N, K)
+        splits = 1 if colsum_part is not None else auto_splits(M, N, K)
     if splits > 1:
         n = lib.hsg_gemm_workspace_floats(M, N, K, splits)
         ws = workspace if workspace is not None and workspace.numel() >= n else A.new_empty(n)
     check(lib.hsg_gemm_f32(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), ptr(out),
                            _ld(out), ptr(bias), ptr(aux), _ld(aux) if aux is not None else 0, epi,
-                           int(relu), int(splits), ptr(ws), stream_of(A)), "hsg_gemm_f32")
+                           int(relu), int(splits), ptr(ws), ptr(colsum_part), stream_of(A)), "hsg_gemm_f32")
     return out
 
 
 def auto_splits(M, N, K):
     """hsg_gemm_f32's splits == 0 plan (so the workspace can be sized)."""
     return load().hsg_gemm_auto_splits(M, N, K)
+
+
+def row_tiles(M, N, K, splits=1):
+    """Rows of hsg_gemm_f32's colsum_part slab for this shape."""
+    return load().hsg_gemm_row_tiles(M, N, K, splits)
 
 
 def splits_for(M, N, K, n_cu=256):

@@ -10,7 +10,8 @@ Backward:              (dy, dx) = row kernel (LN + dropout backward, block parti
                        of dgamma, dbeta and db2 = colsum(dy)); dH = (dy W2) * (H > 0)
                        [GEMM, relu' epilogue]; dx += dH W1 [GEMM, accumulate
                        epilogue]; dW2 = dy^T H and dW1 = dH^T x [split-K GEMMs];
-                       db1 = colsum(dH); one reduction of the row-kernel partials.
+                       db1 from the dH GEMM's column-sum epilogue; one launch
+                       reduces both partial slabs.
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm
+from .dense import gemm, row_tiles
 
 LN_EPS = 1e-5
 
@@ -50,18 +51,24 @@ class _FFN(torch.autograd.Function):
         dout = dout.contiguous()
         n, d = x.shape
         nb = lib.hsg_ln_bwd_blocks(n)
+        d_hid = H.shape[1]
         dy = torch.empty_like(x)
         dx = torch.empty_like(x)
         part = x.new_empty(nb, 3, d)
         check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd),
                              float(ctx.p_drop), ptr(ctx.seed_t), ctx.off, ptr(dy), ptr(dx), ptr(part),
                              stream_of(x)), "hsg_ln_bwd")
-        dH = gemm(dy, w2, relu_mask=H)                         # [n, d_hid]
+        rt = row_tiles(n, d_hid, d)
+        hpart = x.new_empty(rt, d_hid)
+        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
         gemm(dH, w1, out=dx, add=dx)                           # dx += dH W1
         dw2 = gemm(dy, H, a_t=True)                            # [d, d_hid]
         dw1 = gemm(dH, x, a_t=True)                            # [d_hid, d]
-        db1 = dH.sum(0)
-        dg, dbt, db2 = part.sum(0)                             # one reduction for three vectors
+        db1 = x.new_empty(d_hid)
+        red = x.new_empty(3, d)                                # dgamma, dbeta, db2
+        check(lib.hsg_colsum2(rt, d_hid, ptr(hpart), ptr(db1), nb, 3 * d, ptr(part), ptr(red), stream_of(x)),
+              "hsg_colsum2")
+        dg, dbt, db2 = red
         return dx, dw1, db1, dw2, db2, dg, dbt, None, None
 
 
