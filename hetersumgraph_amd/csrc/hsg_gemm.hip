@@ -53,6 +53,7 @@ struct GemmArgs {
     int k_tiles_per_split;
     float *ws;            // split-K partials [splits][M][N]
     float *colpart;       // optional: per-block-row column sums of C, [ceil(M/BM)][N]
+    int splits;           // K slices (tile ids run over splits x tiles_m x tiles_n)
 };
 
 __device__ __forceinline__ float epi_apply(float v, int m, int n, const GemmArgs &p) {
@@ -125,8 +126,15 @@ struct Stage {
 // NBUF = 2: register-staged double buffer in LDS, one barrier per K tile.
 // NBUF = 1: one LDS buffer (half the LDS, twice the resident blocks), the next
 // tile still prefetched into registers, two barriers per K tile.
+#ifdef HSG_GEMM_CENSUS
+__device__ unsigned long long g_census[16384 * 4];
+#endif
+
 template <int BM, int BN, bool AK, bool BKC, int NBUF, int BK>
 __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
+#ifdef HSG_GEMM_CENSUS
+    const unsigned long long c_t0 = __builtin_readcyclecounter();
+#endif
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 32, TN = WN / 32;
     using SA = Stage<AK, BM, BK>;
@@ -137,10 +145,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     const int li = lane & 31, h = lane >> 5;
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_mn = tiles_n * tiles_m;
     const int kt_total = (p.K + BK - 1) / BK;
-    const int kt0 = blockIdx.z * p.k_tiles_per_split;
+    // persistent over output tiles (grid may be smaller than the tile count)
+    for (int t = blockIdx.x; t < tiles_mn * p.splits; t += gridDim.x) {
+    const int tx = t % tiles_n, ty = (t / tiles_n) % tiles_m, tz = t / tiles_mn;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int kt0 = tz * p.k_tiles_per_split;
     const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
 
     f32x16 acc[TM][TN];
@@ -223,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     }
 
     // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
-    const bool split = gridDim.z > 1;
+    const bool split = p.splits > 1;
     float csum[TN];                       // column sums of this wave's stored values (colpart)
 #pragma unroll
     for (int j = 0; j < TN; ++j) csum[j] = 0.f;
@@ -238,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
                 const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
                 if (m >= p.M) continue;
                 if (split) {
-                    p.ws[((size_t)blockIdx.z * p.M + m) * p.N + n] = acc[i][j][r];
+                    p.ws[((size_t)tz * p.M + m) * p.N + n] = acc[i][j][r];
                 } else {
                     const float v = epi_apply(acc[i][j][r], m, n, p);
                     p.C[(size_t)m * p.ldc + n] = v;
@@ -259,9 +271,22 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
         __syncthreads();
         for (int c = threadIdx.x; c < BN; c += 256) {
             const int n = n0 + c;
-            if (n < p.N) p.colpart[(size_t)blockIdx.y * p.N + n] = red[c] + red[BN + c];
+            if (n < p.N) p.colpart[(size_t)ty * p.N + n] = red[c] + red[BN + c];
         }
     }
+    __syncthreads();                      // LDS is refilled by the next tile's prologue
+    }
+#ifdef HSG_GEMM_CENSUS
+    if (threadIdx.x == 0 && blockIdx.x < 16384) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        g_census[blockIdx.x * 4 + 0] = hw;
+        g_census[blockIdx.x * 4 + 1] = xcc;
+        g_census[blockIdx.x * 4 + 2] = c_t0;
+        g_census[blockIdx.x * 4 + 3] = __builtin_readcyclecounter();
+    }
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
@@ -279,7 +304,11 @@ template <int BM, int BN, int NBUF = 2, int BK = kBK>
 int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     const int kt_total = (p.K + BK - 1) / BK;
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
-    dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+    p.splits = splits;
+    const long tiles = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
+    long g = tiles;
+    if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
+    dim3 grid((unsigned)g);
     if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK>), grid, dim3(256), 0, st, p);
     else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF, BK>), grid, dim3(256), 0, st, p);
     else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF, BK>), grid, dim3(256), 0, st, p);
@@ -346,7 +375,7 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     if (splits > 1 && !workspace) return HSG_EINVAL;
     if (splits > 1 && colsum_part) return HSG_EINVAL;     // column partials need the unsplit epilogue
     GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
-               (kt_total + splits - 1) / splits, workspace, colsum_part};
+               (kt_total + splits - 1) / splits, workspace, colsum_part, splits};
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
     int best = plan_tile(M, N, K, splits);
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
@@ -370,5 +399,11 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
+
+#ifdef HSG_GEMM_CENSUS
+int hsg_gemm_census_read(unsigned long long *host, int n) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_census), sizeof(unsigned long long) * 4 * n);
+}
+#endif
 
 }  // extern "C"

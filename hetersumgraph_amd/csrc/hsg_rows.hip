@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
 // issued together).  Per block, column partials of dgamma, dbeta and of dy (the
 // gradient of W2's bias, b2) go to part[block][3][d].
 template <int NPL>
-__global__ __launch_bounds__(256) void k_ln_bwd(int n, int d, const float *__restrict__ dout,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 6 : (NPL <= 4 ? 4 : 2), 8))) void k_ln_bwd(int n, int d, const float *__restrict__ dout,
                                                 const float *__restrict__ y, const float *__restrict__ x,
                                                 const float *__restrict__ gamma, const float *__restrict__ mean,
                                                 const float *__restrict__ rstd, float p_drop,
