@@ -288,6 +288,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
     for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += gridDim.x * NPB) {
         const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
         const int beg = R.indptr[v], end = R.indptr[v + 1];
+        const float M = kact ? mv[v * H + k] : 0.f;             // issued early: independent
+        const float lvv = kact ? lv[v * H + k] : 1.f;
         float g[DV];
         float rho = 0.f;
         const int kc = kact ? k : H - 1;
@@ -306,8 +308,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
                 if (d < D && d % lph == l) G[(size_t)v * HD + k * D + d] = g[d];
         }
         if (end == beg || !kact) continue;
-        const float M = mv[v * H + k];
-        const float inv = 1.f / lv[v * H + k];
+        const float inv = 1.f / lvv;
         int eb, ee;
         subrange(beg, end, part, WPN, eb, ee);
 #pragma unroll 2
@@ -376,6 +377,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
     for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += gridDim.x * HSG_WAVES) {
         const int v = __builtin_amdgcn_readfirstlane(v_);
         const int beg = R.indptr[v], end = R.indptr[v + 1];
+        // softmax state of v: independent of everything below, issued first
+        const float M = kact ? mv[v * H + k] : 0.f;
+        const float lvv = kact ? lv[v * H + k] : 1.f;
         // prefetch edge j = l of this head: source rank, tau row and pre-activation
         int u0 = 0, t0 = 0;
         float pre0 = 0.f;
@@ -400,33 +404,51 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
         }
         if (end == beg) continue;   // uniform per wave: no typed in-edge, no gradient
         rho = group_sum(rho, lph);
-        const float M = kact ? mv[v * H + k] : 0.f;
-        const float inv = kact ? 1.f / lv[v * H + k] : 0.f;
+        const float inv = kact ? 1.f / lvv : 0.f;
         const int gl = k * lph;                         // first lane of this head group
-        for (int e = beg; e < end; ++e) {
-            const int j = e - beg;
-            int u, t;
-            float pre;
-            if (j < lph) {                              // wave-uniform branch
-                u = __shfl(u0, gl + j);
-                t = __shfl(t0, gl + j);
-                pre = __shfl(pre0, gl + j);
-            } else {
-                u = R.src[e];
-                t = tau_row<TAU_MODE>(R, e);
-                pre = kact ? sigma[u * H + k] + tau[t * H + k] : 0.f;
-            }
-            const float *zr = Z + (size_t)u * HD + kc * D;
-            float dot = 0.f;
+        // edges in pairs: both Z rows are fetched before either dot is reduced
+        for (int e0 = beg; e0 < end; e0 += 2) {
+            int u[2], t[2];
+            float pre[2];
 #pragma unroll
-            for (int i = 0; i < NE; ++i) dot = fmaf(g[i], zr[min(l + lph * i, D - 1)], dot);   // g = 0 past D
-            dot = group_sum(dot, lph);
-            if (kact && l == 0) {
-                const float alpha = __expf(leaky(pre, slope) - M) * inv;
-                const float ds = alpha * (dot - rho);
-                const float dp = pre > 0.f ? ds : ds * slope;
-                dpre[(size_t)e * H + k] = dp;
-                if constexpr (TAU_MODE == HSG_TAU_TABLE) sd[t * H + k] += dp;
+            for (int q = 0; q < 2; ++q) {
+                const int e = min(e0 + q, end - 1);
+                const int j = e - beg;
+                if (j < lph) {                          // wave-uniform branch
+                    u[q] = __shfl(u0, gl + j);
+                    t[q] = __shfl(t0, gl + j);
+                    pre[q] = __shfl(pre0, gl + j);
+                } else {
+                    u[q] = R.src[e];
+                    t[q] = tau_row<TAU_MODE>(R, e);
+                    pre[q] = kact ? sigma[u[q] * H + k] + tau[t[q] * H + k] : 0.f;
+                }
+            }
+            float zv[2][NE];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float *zr = Z + (size_t)u[q] * HD + kc * D;
+#pragma unroll
+                for (int i = 0; i < NE; ++i) zv[q][i] = zr[min(l + lph * i, D - 1)];
+            }
+            float dot[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                dot[q] = 0.f;
+#pragma unroll
+                for (int i = 0; i < NE; ++i) dot[q] = fmaf(g[i], zv[q][i], dot[q]);   // g = 0 past D
+                dot[q] = group_sum(dot[q], lph);
+            }
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int e = e0 + q;
+                if (e < end && kact && l == 0) {
+                    const float alpha = __expf(leaky(pre[q], slope) - M) * inv;
+                    const float ds = alpha * (dot[q] - rho);
+                    const float dp = pre[q] > 0.f ? ds : ds * slope;
+                    dpre[(size_t)e * H + k] = dp;
+                    if constexpr (TAU_MODE == HSG_TAU_TABLE) sd[t[q] * H + k] += dp;
+                }
             }
         }
     }

@@ -27,6 +27,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 #include "../../include/hsg.h"
 
 namespace {
@@ -148,12 +150,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
     const int tiles_mn = tiles_n * tiles_m;
     const int kt_total = (p.K + BK - 1) / BK;
+    const int total = tiles_mn * p.splits;
+    SA ra;
+    SB rb;
+    // first K slice of tile t into registers (single-buffer kernels prefetch the next
+    // tile's first slice during the current tile's last K step)
+    auto load_first = [&](int t) {
+        const int tx_ = t % tiles_n, ty_ = (t / tiles_n) % tiles_m, tz_ = t / tiles_mn;
+        const int k0 = tz_ * p.k_tiles_per_split * BK;
+        ra.load(p.A, p.lda, ty_ * BM, p.M, k0, p.K);
+        rb.load(p.B, p.ldb, tx_ * BN, p.N, k0, p.K);
+    };
+    if (NBUF == 1 && (int)blockIdx.x < total) load_first(blockIdx.x);
     // persistent over output tiles (grid may be smaller than the tile count)
-    for (int t = blockIdx.x; t < tiles_mn * p.splits; t += gridDim.x) {
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {
     const int tx = t % tiles_n, ty = (t / tiles_n) % tiles_m, tz = t / tiles_mn;
     const int m0 = ty * BM, n0 = tx * BN;
     const int kt0 = tz * p.k_tiles_per_split;
     const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
+    const int tn = t + gridDim.x;
+    bool prefetched = false;
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -163,10 +179,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    SA ra;
-    SB rb;
     int cur = 0;
-    if (kt0 < kt1) {
+    if constexpr (NBUF == 1) {
+        ra.store(sA[0]);                  // registers hold this tile's first slice
+        rb.store(sB[0]);
+    } else if (kt0 < kt1) {
         ra.load(p.A, p.lda, m0, p.M, kt0 * BK, p.K);
         rb.load(p.B, p.ldb, n0, p.N, kt0 * BK, p.K);
         ra.store(sA[0]);
@@ -178,6 +195,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
         if (more) {
             ra.load(p.A, p.lda, m0, p.M, (kt + 1) * BK, p.K);
             rb.load(p.B, p.ldb, n0, p.N, (kt + 1) * BK, p.K);
+        } else if (NBUF == 1 && tn < total) {
+            load_first(tn);               // overlaps this step's MFMAs and the epilogue
+            prefetched = true;
         }
         const float *a_s = sA[NBUF == 2 ? cur : 0];
         const float *b_s = sB[NBUF == 2 ? cur : 0];
@@ -234,6 +254,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
         }
     }
 
+    if (NBUF == 1 && !prefetched && tn < total) load_first(tn);   // empty K range
     // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
     const bool split = p.splits > 1;
     float csum[TN];                       // column sums of this wave's stored values (colpart)
@@ -300,13 +321,43 @@ __global__ __launch_bounds__(256) void k_splitk_reduce(GemmArgs p, int splits) {
     }
 }
 
+// resident 256-thread blocks of a kernel on the whole device (occupancy API x CUs);
+// the per-kernel blocks-per-CU answer is cached (it depends on the code object only)
+template <class F>
+long resident_blocks(bool a, int b, F kernel_of) {
+    static std::atomic<int> per_cu[4] = {{-1}, {-1}, {-1}, {-1}};
+    const int slot = (a ? 2 : 0) + (b ? 1 : 0);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    int per = per_cu[slot].load(std::memory_order_relaxed);
+    if (per < 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel_of(a ? 1 : 0, b), 256, 0) != hipSuccess)
+            return 0;
+        per_cu[slot].store(per, std::memory_order_relaxed);
+    }
+    return (long)cus * per;
+}
+
 template <int BM, int BN, int NBUF = 2, int BK = kBK>
 int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     const int kt_total = (p.K + BK - 1) / BK;
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
     p.splits = splits;
     const long tiles = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
+    // persistent grid: the resident block count (occupancy API x CUs), so tile
+    // phases desynchronise and each block overlaps a tile's epilogue with the next
+    // tile's first loads
     long g = tiles;
+    if (NBUF == 1) {
+        const long cap = resident_blocks(ak, bk ? 1 : 0, [&](int a, int b) -> const void * {
+            if (a && b) return (const void *)k_gemm<BM, BN, true, true, NBUF, BK>;
+            if (a) return (const void *)k_gemm<BM, BN, true, false, NBUF, BK>;
+            if (b) return (const void *)k_gemm<BM, BN, false, true, NBUF, BK>;
+            return (const void *)k_gemm<BM, BN, false, false, NBUF, BK>;
+        });
+        if (cap > 0 && cap < g) g = cap;
+    }
     if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
     if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK>), grid, dim3(256), 0, st, p);

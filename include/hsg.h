@@ -137,7 +137,11 @@ int hsg_gemm_auto_splits(int M, int N, int K);
 int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
                  const float *B, int ldb, int b_kcontig, float *C, int ldc,
                  const float *bias, const float *aux, int ldaux, int epi, int relu,
-                 int splits, float *workspace, void *stream);
+                 int splits, float *workspace, float *colsum_part, void *stream);
+/* colsum_part (optional, unsplit GEMMs only): per-tile-row column sums of the stored
+ * C, [hsg_gemm_row_tiles(M,N,K,splits)][N] -- e.g. the bias gradient of the FFN's
+ * first layer taken from the dH epilogue instead of a second pass over dH. */
+int hsg_gemm_row_tiles(int M, int N, int K, int splits);
 
 /* ---- PositionwiseFeedForward row epilogue (GATLayer.py:40-42) -------------------
  * Forward:  s = dropout(y; p, seed, offset) + x;  out = (s-mean)*rstd*gamma + beta
@@ -150,6 +154,10 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
  * per-call constant; forward and backward with equal (seed, offset) agree.
  * d <= 512; p_drop in [0, 1). */
 int hsg_ln_bwd_blocks(int n);
+/* out0[c] = sum_r part0[r][c] (and the same for slab 1) in a fixed order, one launch:
+ * the reduction of the FFN's block-row partials (GEMM colsum_part, hsg_ln_bwd part). */
+int hsg_colsum2(int rows0, int cols0, const float *part0, float *out0, int rows1, int cols1,
+                const float *part1, float *out1, void *stream);
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
                float eps, float p_drop, const int64_t *seed, uint32_t offset,
                float *out, float *mean, float *rstd, void *stream);
