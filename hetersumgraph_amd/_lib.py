@@ -24,7 +24,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_colsum2",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
-           "hsg_hproj_dw_chunks", "hsg_hproj_dw")
+           "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -71,12 +71,15 @@ _SIGS = {
     "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _P],
+    "hsg_rel_build_workspace_bytes": [_I, _I],
+    "hsg_rel_build": [_F, _F, _I, _I] + [_P] * 17 + [ctypes.c_size_t, _P],
     "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
 }
 _RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_gemm_workspace_floats": ctypes.c_size_t,
             "hsg_attn_params_bwd_workspace_floats": ctypes.c_size_t,
-            "hsg_dropmask_scale": ctypes.c_float}
+            "hsg_dropmask_scale": ctypes.c_float,
+            "hsg_rel_build_workspace_bytes": ctypes.c_size_t}
 
 
 def load():

@@ -9,7 +9,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
 

@@ -47,8 +47,26 @@ class Relation:
         self.dev = None
         self._cstruct = None
 
+    @classmethod
+    def on_device(cls, kind, n_src, n_dst, dev_arrays, n_edges_total):
+        """A relation whose arrays were built on the device (no host copy)."""
+        r = cls.__new__(cls)
+        r.kind = kind
+        r.n_src, r.n_dst = int(n_src), int(n_dst)
+        r.n_typed = int(dev_arrays["src"].shape[0])
+        r.n_edges_total = int(n_edges_total)
+        r.host = None
+        r.dev = dev_arrays
+        r.device = dev_arrays["indptr"].device
+        r._cstruct = None
+        return r
+
     def to(self, device):
         device = torch.device(device)
+        if self.host is None:
+            if device != self.device:
+                raise RuntimeError("device-built relation: rebuild it on the new device")
+            return self
         r = Relation.__new__(Relation)
         r.__dict__.update(self.__dict__)
         r.device = device
@@ -57,10 +75,11 @@ class Relation:
         return r
 
     def degree_stats(self):
-        deg = np.diff(self.host["indptr"])
-        cdeg = np.diff(self.host["cindptr"])
+        arr = (lambda k: self.host[k]) if self.host is not None else (lambda k: self.dev[k].cpu().numpy())
+        deg = np.diff(arr("indptr"))
+        cdeg = np.diff(arr("cindptr"))
         return dict(max_in=int(deg.max(initial=0)), mean_in=float(deg.mean()) if len(deg) else 0.0,
-                    max_out=int(cdeg.max(initial=0)), phantom_max=int(self.host["phantom"].max(initial=0)))
+                    max_out=int(cdeg.max(initial=0)), phantom_max=int(arr("phantom").max(initial=0)))
 
     def cstruct(self):
         """ctypes ``hsg_rel`` (include/hsg.h) pointing at the device arrays."""
@@ -76,88 +95,81 @@ class Relation:
 
 
 def build_relation(kind, src, dst, unit, tffrac=None, edtype=None):
-    """Host construction of a :class:`Relation` from COO edges (numpy).
+    """Device construction of a :class:`Relation` through ``hsg_rel_build``
+    (include/hsg.h; csrc/hsg_relbuild.hip).
 
     Restates GATLayer.py:105-107 / 143-145 (node and edge filters) and DGL 0.4's
-    ``pull`` in-edge set (113 / 149) as index arrays.  ``tffrac``/``edtype`` give the
+    ``pull`` in-edge set (113 / 149) as index arrays; ``tffrac``/``edtype`` give the
     tf-idf box per edge following HiGraph.py:146-151: rows of ``_TFembed`` for dtype-0
-    edges, :data:`ZERO_ROW` for any other typed edge (never written -> zeros)."""
+    edges, :data:`ZERO_ROW` for any other typed edge (never written -> zeros).
+    All inputs are tensors on one ROCm device; one 5-int readback gives the sizes."""
+    from . import _lib
+
     s_unit, d_unit = KINDS[kind]
-    unit = np.asarray(unit)
-    src = np.asarray(src, np.int64)
-    dst = np.asarray(dst, np.int64)
-    n = len(unit)
-    is_src = unit == s_unit
-    is_dst = unit == d_unit
-    src_nodes = np.nonzero(is_src)[0]
-    dst_nodes = np.nonzero(is_dst)[0]
-    src_rank = np.full(n, -1, np.int64)
-    src_rank[src_nodes] = np.arange(len(src_nodes))
-    dst_rank = np.full(n, -1, np.int64)
-    dst_rank[dst_nodes] = np.arange(len(dst_nodes))
-
-    typed = is_src[src] & is_dst[dst]
-    te = np.nonzero(typed)[0]
-    # stable sort by destination keeps DGL's edge-id order inside each mailbox
-    order = np.argsort(dst_rank[dst[te]], kind="stable")
-    eid = te[order]
-    e_dst = dst_rank[dst[eid]]
-    e_src = src_rank[src[eid]]
-    n_dst = len(dst_nodes)
-    n_src = len(src_nodes)
-    typed_cnt = np.bincount(e_dst, minlength=n_dst)
-    indptr = np.zeros(n_dst + 1, np.int64)
-    np.cumsum(typed_cnt, out=indptr[1:])
-    indeg_all = np.bincount(dst, minlength=n)
-    phantom = indeg_all[dst_nodes] - typed_cnt
-
-    if tffrac is None:
-        tf = np.full(len(eid), ZERO_ROW, np.uint8)
-    else:
-        tffrac = np.asarray(tffrac, np.int64)
-        et = np.zeros(len(src)) if edtype is None else np.asarray(edtype)
-        box = tffrac[eid]
-        has = et[eid] == 0
-        if has.any() and (box[has].min() < 0 or box[has].max() >= N_BOX):
-            # nn.Embedding(10, ...) would raise on the same input (HiGraph.py:52, 151)
-            raise IndexError("tffrac outside the 10 tf-idf boxes")
-        tf = np.where(has, box, ZERO_ROW).astype(np.uint8)
-
-    corder = np.argsort(e_src, kind="stable")
-    cperm = corder
-    cdst = e_dst[corder]
-    ccnt = np.bincount(e_src, minlength=n_src)
-    cindptr = np.zeros(n_src + 1, np.int64)
-    np.cumsum(ccnt, out=cindptr[1:])
-    i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)
-    return Relation(kind, n_src, n_dst, src_nodes, dst_nodes, i32(indptr), i32(e_src), tf,
-                    eid.astype(np.int64), i32(phantom), i32(cindptr), i32(cdst), i32(cperm),
-                    len(src))
+    dev = src.device
+    if dev.type != "cuda":
+        raise RuntimeError("build_relation runs only on a ROCm device (hsg_rel_build); no CPU fallback")
+    lib = _lib.load()
+    src = src.to(torch.int64).contiguous()
+    dst = dst.to(device=dev, dtype=torch.int64).contiguous()
+    unit = unit.to(device=dev, dtype=torch.float32).contiguous()
+    if tffrac is not None:
+        tffrac = tffrac.to(device=dev, dtype=torch.int64).contiguous()
+    if edtype is not None:
+        edtype = edtype.to(device=dev, dtype=torch.float32).contiguous()
+    n, E = int(unit.shape[0]), int(src.shape[0])
+    i32 = lambda k: torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+    i64 = lambda k: torch.empty(max(k, 1), dtype=torch.int64, device=dev)
+    counts = torch.zeros(5, dtype=torch.int32, device=dev)
+    indptr, cindptr, phantom = i32(n + 1), i32(n + 1), i32(n)
+    esrc, cdst, cperm = i32(E), i32(E), i32(E)
+    tf = torch.empty(max(E, 1), dtype=torch.uint8, device=dev)
+    eid, src_nodes, dst_nodes = i64(E), i64(n), i64(n)
+    wsb = lib.hsg_rel_build_workspace_bytes(n, E)
+    if wsb == 0:
+        raise RuntimeError("hsg_rel_build_workspace_bytes failed")
+    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(lib.hsg_rel_build(s_unit, d_unit, n, E, _lib.ptr(src), _lib.ptr(dst), _lib.ptr(unit),
+                                     _lib.ptr(tffrac), _lib.ptr(edtype), _lib.ptr(counts), _lib.ptr(indptr),
+                                     _lib.ptr(esrc), _lib.ptr(tf), _lib.ptr(eid), _lib.ptr(phantom),
+                                     _lib.ptr(cindptr), _lib.ptr(cdst), _lib.ptr(cperm), _lib.ptr(src_nodes),
+                                     _lib.ptr(dst_nodes), _lib.ptr(ws), wsb, _lib.stream_of(src)),
+                   "hsg_rel_build")
+        n_src, n_dst, n_typed, bad_tf, bad_id = counts.tolist()
+    if bad_id:
+        raise IndexError(f"{bad_id} edges reference a node id outside [0, {n})")
+    if bad_tf:
+        # nn.Embedding(10, ...) would raise on the same input (HiGraph.py:52, 151)
+        raise IndexError("tffrac outside the 10 tf-idf boxes")
+    d = dict(src_nodes=src_nodes[:n_src], dst_nodes=dst_nodes[:n_dst], indptr=indptr[:n_dst + 1],
+             src=esrc[:n_typed], tf=tf[:n_typed], eid=eid[:n_typed], phantom=phantom[:n_dst],
+             cindptr=cindptr[:n_src + 1], cdst=cdst[:n_typed], cperm=cperm[:n_typed])
+    return Relation.on_device(kind, n_src, n_dst, d, E)
 
 
-def _host_relation(g, kind):
-    key = ("rel_host", kind)
-    if key not in g._rel_cache:
-        g._flush()
-        unit = g.host_column("unit")
-        if unit is None:
-            raise KeyError("graph has no 'unit' node column (dataloader.py:216)")
-        g._rel_cache[key] = build_relation(kind, g._src, g._dst, unit,
-                                           g.host_column("tffrac"), g.host_column("edtype"))
-    return g._rel_cache[key]
+def _structure(g):
+    """Device tensors of the structural columns (src, dst, unit, tffrac, edtype)."""
+    from .graph import TableColumn
+
+    g._flush()
+    nf, ef = g._nframe.cols, g._eframe().cols
+    if "unit" not in nf:
+        raise KeyError("graph has no 'unit' node column (dataloader.py:216)")
+    col = lambda c: None if c is None or isinstance(c, TableColumn) else c
+    return g._src_t(), g._dst_t(), nf["unit"], col(ef.get("tffrac")), col(ef.get("dtype"))
 
 
 def get_relation(g, kind):
     """Relation of ``kind`` on the graph's current device (cached per batch)."""
     key = ("rel", kind, str(g.device))
     if key not in g._rel_cache:
-        g._rel_cache[key] = _host_relation(g, kind).to(g.device)
+        g._rel_cache[key] = build_relation(kind, *_structure(g))
     return g._rel_cache[key]
 
 
 def prefetch_relations(g, device):
-    """Called by ``DGLGraph.to``: build both relations while the structural columns
-    are still on the host, and upload them with the frames."""
+    """Called by ``DGLGraph.to``: build both relations once per batch, on the device."""
     if "unit" not in g._nframe.cols:
         return
     for kind in KINDS:

@@ -192,6 +192,29 @@ int hsg_hproj_dw_chunks(int n, int in, int H, int D);
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
                  const uint32_t *bits, float p, float *part, float *dW, void *stream);
 
+/* Device construction of one typed relation from the batched graph's COO edges.
+ * Replaces DGL's per-call filter_nodes/filter_edges (GATLayer.py:105-107, 143-145),
+ * the in-edge set of g.pull (113, 149) and the tffrac -> _TFembed row selection of
+ * HSumGraph.set_wnfeature (HiGraph.py:146-151); runs once per batch.
+ *   src, dst   [E] int64 node ids;  unit [n] float (dataloader.py:216-217, 0 word / 1 sentence|doc)
+ *   tffrac     [E] int64 (nullable -> tau row 10 everywhere); edtype [E] float (nullable -> all 0)
+ * Sources are nodes with unit == src_unit, destinations unit == dst_unit, typed edges
+ * go source -> destination.  Outputs are sized by the upper bounds n and E; the true
+ * sizes land in counts[0..2] = n_src, n_dst, n_typed (device).  counts[3] = typed
+ * dtype-0 edges whose tffrac is outside the 10 boxes (nn.Embedding would raise),
+ * counts[4] = edges with a node id outside [0, n): the caller raises on either.
+ *   indptr [n+1] (first n_dst+1 valid), esrc/tf/eid [E] (first n_typed), phantom [n],
+ *   cindptr [n+1] (first n_src+1), cdst/cperm [E], src_nodes/dst_nodes [n] int64.
+ * CSR edges of one destination keep edge-id order (the DGL mailbox order); CSC edges of
+ * one source keep CSR order.  workspace >= hsg_rel_build_workspace_bytes(n, E). */
+size_t hsg_rel_build_workspace_bytes(int n_nodes, int n_edges);
+int hsg_rel_build(float src_unit, float dst_unit, int n_nodes, int n_edges, const int64_t *src,
+                  const int64_t *dst, const float *unit, const int64_t *tffrac, const float *edtype,
+                  int32_t *counts, int32_t *indptr, int32_t *esrc, uint8_t *tf, int64_t *eid,
+                  int32_t *phantom, int32_t *cindptr, int32_t *cdst, int32_t *cperm,
+                  int64_t *src_nodes, int64_t *dst_nodes, void *workspace, size_t workspace_bytes,
+                  void *stream);
+
 /* Library build identification (ABI version, gfx target). */
 const char *hsg_version(void);
 
