@@ -1,17 +1,22 @@
 """In-tree build of libhsg.so for gfx950 (``python -m hetersumgraph_amd.build``).
 
 hipcc cross-compiles without a GPU; the .so lands next to this file so that it
-travels with the repository snapshot to the GPU box.
+travels with the repository snapshot to the GPU box.  Each source compiles to its
+own object in parallel (no cross-file device symbols, so no -fgpu-rdc), then one
+link step.
 """
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
+OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
+HEADERS = [os.path.join(ROOT, "include", "hsg.h"), os.path.join(HERE, "csrc", "hsg_rng.h")]
 
 
 def hipcc():
@@ -25,15 +30,40 @@ def needs_build():
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(ROOT, "include", "hsg.h"), os.path.join(HERE, "csrc", "hsg_rng.h")]
-    return any(os.path.getmtime(s) > t for s in deps)
+    return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
+
+
+def _flags():
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+            "-I", os.path.join(ROOT, "include")]
+
+
+def _obj(src):
+    return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+
+
+def _compile(src, force, verbose):
+    obj = _obj(src)
+    if not force and os.path.exists(obj):
+        t = os.path.getmtime(obj)
+        if os.path.getmtime(src) <= t and all(os.path.getmtime(h) <= t for h in HEADERS):
+            return obj
+    cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(obj + ".tmp", obj)
+    return obj
 
 
 def build(force=False, verbose=True):
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-Wno-unused-function", "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SOURCES
+    os.makedirs(OBJDIR, exist_ok=True)
+    jobs = min(len(SOURCES), os.cpu_count() or 1, 8)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -254,6 +254,109 @@ __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lp
     }
 }
 
+// Grouped forward for short segments and wide rows (S2W: ~2 in-edges per word,
+// H*D = 300): a wave carries 64/LPN destinations at once, one per LPN-lane group,
+// so each wave has that many independent index -> score -> gather chains in flight
+// and the grid needs 64/LPN times fewer waves.  Same arithmetic as k_gat_fwd with
+// WPN = 1, group-local everything: lane = k*lph + l inside the group (lph =
+// LPN / nextpow2(H)), features f = gl + LPN*i (LPN*4-byte contiguous segments per
+// row), LDS chunk of kGrpChunk edges per group.
+constexpr int kGrpChunk = 32;
+template <int NF, int TAU_MODE, int LPN>
+__global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, int lph, float slope,
+                                                    const float *__restrict__ Z,
+                                                    const float *__restrict__ sigma,
+                                                    const float *__restrict__ tau,
+                                                    const float *__restrict__ origin,
+                                                    float *__restrict__ hout, float *__restrict__ out,
+                                                    float *__restrict__ mout, float *__restrict__ lout) {
+    constexpr int NG = 256 / LPN;                       // groups per block
+    __shared__ float s_alpha[NG][kGrpChunk * HSG_HMAX];
+    __shared__ int s_nb[NG][kGrpChunk];
+    const int grp = threadIdx.x / LPN, gl = threadIdx.x % LPN;
+    const int HD = H * D;
+    const int k = gl / lph, l = gl - (gl / lph) * lph;
+    const bool kact = k < H;
+    int fh[NF], fo[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = gl + LPN * i;
+        fh[i] = f < HD ? f / D : 0;
+        fo[i] = f < HD ? f : HD - 1;
+    }
+    float *sa = s_alpha[grp];
+    int *sn = s_nb[grp];
+
+    for (int v = blockIdx.x * NG + grp; v < R.n_dst; v += gridDim.x * NG) {
+        const int beg = R.indptr[v], end = R.indptr[v + 1];
+        const int c = R.phantom[v];
+        // the residual row: independent of everything else, issued first
+        float org[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
+        const int n1 = end - beg;
+        const bool single = n1 <= kGrpChunk;
+        float mx = -INFINITY, sm = 0.f;
+        if (kact) {
+            for (int j = l; j < n1; j += lph) {
+                const int e = beg + j;
+                const int u = R.src[e];
+                const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                if (single) {
+                    sa[j * H + k] = s;
+                    if (k == 0) sn[j] = u;
+                }
+                if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
+                else sm += __expf(s - mx);
+            }
+        }
+        for (int o = lph >> 1; o >= 1; o >>= 1) {
+            const float om = __shfl_xor(mx, o), os = __shfl_xor(sm, o);
+            lse_merge(mx, sm, om, os);
+        }
+        if (c > 0) lse_merge(mx, sm, 0.f, (float)c);
+        const bool any = end > beg;
+        const float inv = any ? 1.f / sm : 0.f;
+        float acc[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) acc[i] = 0.f;
+        for (int cb = beg; cb < end; cb += kGrpChunk) {
+            const int n = min(kGrpChunk, end - cb);
+            if (kact) {
+                for (int j = l; j < n; j += lph) {
+                    float s;
+                    if (single) {
+                        s = sa[j * H + k];
+                    } else {
+                        const int e = cb + j;
+                        const int u = R.src[e];
+                        s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                        if (k == 0) sn[j] = u;
+                    }
+                    sa[j * H + k] = __expf(s - mx) * inv;
+                }
+            }
+            wave_lds_sync();
+            gather_rows<NF>(Z, HD, n, sn, sa, H, fh, fo, acc);
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int f = gl + LPN * i;
+            if (f < HD) {
+                const size_t o = (size_t)v * HD + f;
+                const float hv = acc[i];
+                hout[o] = hv;
+                if (origin) out[o] = (hv > 0.f ? hv : expm1f(hv)) + org[i];
+            }
+        }
+        if (kact && l == 0) {
+            mout[v * H + k] = any ? mx : 0.f;
+            lout[v * H + k] = any ? sm : 1.f;
+        }
+    }
+}
+
 // ---------------------------------------------------- backward: dst-centric ----
 // Shared by both variants:  G = origin_mode ? dOut * elu'(h) : dOut,  rho = G.h,
 //   dpre[e,k] = alpha (G_v.Z_u - rho) * leaky'(pre),  dtau partials per block.
@@ -650,6 +753,54 @@ int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int
     return launch_status();
 }
 
+// grouped forward: NF rounded up to an instantiated bucket (extra features are
+// clamped loads that are never stored)
+int grp_nf_bucket(int nf, int lpn) {
+    static const int b32[] = {2, 4, 8, 10, 12, 16}, b16[] = {4, 8, 12, 16, 20, 32};
+    const int *b = lpn == 32 ? b32 : b16;
+    for (int i = 0; i < 6; ++i)
+        if (nf <= b[i]) return b[i];
+    return -1;
+}
+
+template <int TAU, int LPN>
+int fwd_grp_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
+                     const float *Z, const float *sg, const float *tau, const float *org, float *h, float *out,
+                     float *m, float *l) {
+#define HSG_FG(NF_)                                                                                      \
+    case NF_:                                                                                            \
+        hipLaunchKernelGGL((k_gat_fwd_grp<NF_, TAU, LPN>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
+                           sg, tau, org, h, out, m, l);                                                  \
+        break;
+    if constexpr (LPN == 32) {
+        switch (grp_nf_bucket(nf, LPN)) {
+            HSG_FG(2) HSG_FG(4) HSG_FG(8) HSG_FG(10) HSG_FG(12) HSG_FG(16)
+            default: return HSG_EINVAL;
+        }
+    } else {
+        switch (grp_nf_bucket(nf, LPN)) {
+            HSG_FG(4) HSG_FG(8) HSG_FG(12) HSG_FG(16) HSG_FG(20) HSG_FG(32)
+            default: return HSG_EINVAL;
+        }
+    }
+#undef HSG_FG
+    return launch_status();
+}
+
+// lanes per destination for the forward: 64 (k_gat_fwd, one destination per
+// wave) by default.  HSG_GAT_LPN=32/16 selects the grouped kernel; on the cfg2
+// S2W pass (2.1 in-edges per word, H*D = 300) it measured 24.3 / 31.6 us against
+// 23.5 us for one destination per wave (tools/gat_fwd_lpn.py), so more
+// destinations per wave do not buy memory-level parallelism there.
+int fwd_lanes_per_node(const hsg_rel *r, int H, int D) {
+    int lpn = 64;
+    const int HD = H * D;
+    if (const char *e = getenv("HSG_GAT_LPN")) lpn = atoi(e);
+    if (lpn != 16 && lpn != 32) lpn = 64;
+    if (lpn < 64 && (grp_nf_bucket((HD + lpn - 1) / lpn, lpn) < 0 || next_pow2(H) > lpn)) lpn = 64;
+    return lpn;
+}
+
 template <int TAU, int WPN>
 int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int lph, int om, float slope,
                         const float *Z, const float *sg, const float *tau, const float *h, const float *m,
@@ -723,10 +874,21 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     if (rel->n_dst == 0) return 0;
     const RelPtrs R = rel_ptrs(rel);
+    hipStream_t st = (hipStream_t)stream;
+    const int lpn = fwd_lanes_per_node(rel, H, D);
+    if (lpn < 64) {
+        const int ng = 256 / lpn;
+        int b = (rel->n_dst + ng - 1) / ng;
+        const dim3 g(b < kFwdGridCap ? b : kFwdGridCap);
+        const int nfg = (H * D + lpn - 1) / lpn, lphg = lpn / next_pow2(H);
+#define HSG_G(TAU, L) fwd_grp_dispatch<TAU, L>(nfg, g, st, R, H, D, lphg, slope, Z, sigma, tau, origin, h, out, m, l)
+        if (tau_mode == HSG_TAU_TABLE) return lpn == 32 ? HSG_G(HSG_TAU_TABLE, 32) : HSG_G(HSG_TAU_TABLE, 16);
+        return lpn == 32 ? HSG_G(HSG_TAU_PER_EDGE, 32) : HSG_G(HSG_TAU_PER_EDGE, 16);
+#undef HSG_G
+    }
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
     const dim3 grid(grid_nodes(rel->n_dst, wpn, kFwdGridCap));
-    hipStream_t st = (hipStream_t)stream;
     const int lph = lanes_per_head(H);
 #define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
     if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_F(HSG_TAU_TABLE, 4) : HSG_F(HSG_TAU_TABLE, 1);

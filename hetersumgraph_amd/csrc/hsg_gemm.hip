@@ -56,7 +56,18 @@ struct GemmArgs {
     float *ws;            // split-K partials [splits][M][N]
     float *colpart;       // optional: per-block-row column sums of C, [ceil(M/BM)][N]
     int splits;           // K slices (tile ids run over splits x tiles_m x tiles_n)
+    int xcd;              // 1: XCD-aware tile order (see xcd_tile)
 };
+
+// Workgroup b is dispatched to XCD b % 8, and so is tile t (the persistent grid is a
+// multiple of 8).  xcd_tile gives each XCD one contiguous range of the logical
+// (split, row-tile, col-tile) order, so the column tiles that share an A row band
+// (and the tiles of one K slice) meet in the same 4 MB L2 instead of streaming the
+// band through all eight.  A bijection on [0, total) for any total.
+__device__ __forceinline__ int xcd_tile(int t, int total) {
+    const int x = t & 7, j = t >> 3, per = total >> 3, rem = total & 7;
+    return x * per + min(x, rem) + j;
+}
 
 __device__ __forceinline__ float epi_apply(float v, int m, int n, const GemmArgs &p) {
     if (p.epi == HSG_EPI_RELU_BWD) return p.aux[(size_t)m * p.ldaux + n] > 0.f ? v : 0.f;
@@ -156,6 +167,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     // first K slice of tile t into registers (single-buffer kernels prefetch the next
     // tile's first slice during the current tile's last K step)
     auto load_first = [&](int t) {
+        if (p.xcd) t = xcd_tile(t, total);
         const int tx_ = t % tiles_n, ty_ = (t / tiles_n) % tiles_m, tz_ = t / tiles_mn;
         const int k0 = tz_ * p.k_tiles_per_split * BK;
         ra.load(p.A, p.lda, ty_ * BM, p.M, k0, p.K);
@@ -164,7 +176,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
     if (NBUF == 1 && (int)blockIdx.x < total) load_first(blockIdx.x);
     // persistent over output tiles (grid may be smaller than the tile count)
     for (int t = blockIdx.x; t < total; t += gridDim.x) {
-    const int tx = t % tiles_n, ty = (t / tiles_n) % tiles_m, tz = t / tiles_mn;
+    const int lt = p.xcd ? xcd_tile(t, total) : t;
+    const int tx = lt % tiles_n, ty = (lt / tiles_n) % tiles_m, tz = lt / tiles_mn;
     const int m0 = ty * BM, n0 = tx * BN;
     const int kt0 = tz * p.k_tiles_per_split;
     const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
@@ -201,6 +214,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
         }
         const float *a_s = sA[NBUF == 2 ? cur : 0];
         const float *b_s = sB[NBUF == 2 ? cur : 0];
+        // double-buffered fragments (the scheduler folds them onto one register set,
+        // trading an LDS round trip per group for occupancy; pinning the order with
+        // sched_group_barrier measured slower at 111 VGPRs / 4 waves per SIMD)
         f32x4 af[2][TM], bf[2][TN];
         auto frag = [&](f32x4 (&fa)[TM], f32x4 (&fb)[TN], int s4) {
 #pragma unroll
@@ -426,7 +442,8 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     if (splits > 1 && !workspace) return HSG_EINVAL;
     if (splits > 1 && colsum_part) return HSG_EINVAL;     // column partials need the unsplit epilogue
     GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
-               (kt_total + splits - 1) / splits, workspace, colsum_part, splits};
+               (kt_total + splits - 1) / splits, workspace, colsum_part, splits, 1};
+    if (const char *x = getenv("HSG_GEMM_XCD")) p.xcd = atoi(x);        // dev A/B switch
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
     int best = plan_tile(M, N, K, splits);
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
