@@ -90,7 +90,11 @@ class Stack(torch.nn.Module):
 
     def forward(self, G, Xw, Xs):
         from hetersumgraph_amd.HiGraph import register_tfidf_table
-        register_tfidf_table(G, self._TFembed.weight)
+        from hetersumgraph_amd.stack import fused_stack_ok, gat_stack
+        T = self._TFembed.weight
+        register_tfidf_table(G, T)
+        if fused_stack_ok(G, self.word2sent, self.sent2word, T, Xw, Xs):   # as HSumGraph.gat_stack
+            return gat_stack(G, self.word2sent, self.sent2word, T, Xw, Xs, self.n_iter)
         w, s = Xw, self.word2sent(G, Xw, Xs)
         for _ in range(self.n_iter):
             w = self.sent2word(G, w, s)
@@ -250,7 +254,7 @@ def main():
     def step():
         hsg_rng.advance_all()          # fresh dropout masks every step (device-side: replays too)
         s = stack(G, Xw, Xs)
-        (s * R).sum().backward()
+        s.backward(R)                  # d/ds of sum(s * R): the upstream gradient of the stack output
 
     def allreduce():
         # the data-parallel exchange: bucketed mean all-reduce over RCCL

@@ -24,6 +24,8 @@ from .module.Encoder import sentEncoder
 from .module.GAT import WSWGAT
 from .module.GATLayer import CHECK_NAN, TFIDF_TAG
 from .module.PositionEmbedding import get_sinusoid_encoding_table
+from .stack import fused_stack_ok
+from .stack import gat_stack as fused_gat_stack
 
 
 def _cached(graph, key, fn):
@@ -108,7 +110,15 @@ class HSumGraph(nn.Module):
 
     # ---------------------------------------------------------------- forward
     def gat_stack(self, graph, word_feature, sent_feature):
-        """W2S, then n_iter x (S2W, W2S) (HiGraph.py:99-106) -> supernode state."""
+        """W2S, then n_iter x (S2W, W2S) (HiGraph.py:99-106) -> supernode state.
+
+        On a ROCm device with the TF-IDF table column registered by set_wnfeature
+        the stack runs as one autograd node (:mod:`hetersumgraph_amd.stack`); the
+        per-layer loop below is the same computation through WSWGAT.forward."""
+        T = self._TFembed.weight
+        if fused_stack_ok(graph, self.word2sent, self.sent2word, T, word_feature, sent_feature):
+            return fused_gat_stack(graph, self.word2sent, self.sent2word, T, word_feature, sent_feature,
+                                   self._n_iter)
         word_state = word_feature
         sent_state = self.word2sent(graph, word_feature, sent_feature)
         for _ in range(self._n_iter):

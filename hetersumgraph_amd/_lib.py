@@ -21,7 +21,7 @@ HSG_TAU_PER_EDGE = 1
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
            "hsg_gat_bwd_src_blocks", "hsg_attn_src_logits", "hsg_attn_params_fwd", "hsg_attn_params_bwd",
-           "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_colsum2",
+           "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_ffn_colsums",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
            "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build")
@@ -54,13 +54,13 @@ _SIGS = {
     "hsg_gat_bwd_src": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gat_bwd_src_blocks": [_RELP],
     "hsg_attn_params_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
-    "hsg_attn_params_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_attn_params_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "hsg_attn_params_bwd_workspace_floats": [_I, _I],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_row_tiles": [_I, _I, _I, _I],
-    "hsg_colsum2": [_I, _I, _P, _P, _I, _I, _P, _P, _P],
+    "hsg_ffn_colsums": [_I, _I, _P, _P, _I, _I, _P, _P, _P, _P, _I, _P],
     "hsg_gemm_workspace_floats": [_I, _I, _I, _I],
     "hsg_gemm_auto_splits": [_I, _I, _I],
     "hsg_ln_bwd_blocks": [_I],
@@ -68,9 +68,9 @@ _SIGS = {
     "hsg_dropmask_scale": [_F],
     "hsg_dropmask": [_I, _I, _I, _F, _P, ctypes.c_uint32, _P, _P],
     "hsg_hproj_fwd": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
-    "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
+    "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
-    "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _P],
+    "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _I, _P],
     "hsg_rel_build_workspace_bytes": [_I, _I],
     "hsg_rel_build": [_F, _F, _I, _I] + [_P] * 17 + [ctypes.c_size_t, _P],
     "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],

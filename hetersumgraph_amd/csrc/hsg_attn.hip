@@ -127,7 +127,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
                                                          const float *__restrict__ bf,
                                                          const float *__restrict__ T, float *__restrict__ dattn,
                                                          float *__restrict__ dwf, float *__restrict__ dbf,
-                                                         float *__restrict__ dT) {
+                                                         float *__restrict__ dT, int accumulate) {
     __shared__ float wlds[kWfLds];
     __shared__ float a3s[kDMax];
     __shared__ float dv[kFMax];
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
             const int t = i / F, f = i - (i / F) * F;
             float s = 0.f;
             for (int kk = 0; kk < H; ++kk) s = fmaf(dtau[t * H + kk], vall[kk * F + f], s);
-            dT[i] = s;
+            dT[i] = (accumulate & 2) ? dT[i] + s : s;
         }
         return;
     }
@@ -183,18 +183,24 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
         for (int f = 0; f < F; ++f) s = fmaf(dv[f], W[d * F + f], s);
         if (bf) {
             s = fmaf(dc, bf[k * D + d], s);
-            if (dbf) dbf[k * D + d] = a3s[d] * dc;
+            if (dbf) dbf[k * D + d] = (accumulate & 1) ? dbf[k * D + d] + a3s[d] * dc : a3s[d] * dc;
         }
         float g = 0.f;                             // d a1: stage rows in order
 #pragma unroll 16
         for (int r = 0; r < kStage; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
-        dattn[k * D3 + d] = g;
-        dattn[k * D3 + D + d] = 0.f;
-        dattn[k * D3 + 2 * D + d] = s;
+        if (accumulate & 1) {
+            dattn[k * D3 + d] += g;
+            dattn[k * D3 + 2 * D + d] += s;
+        } else {
+            dattn[k * D3 + d] = g;
+            dattn[k * D3 + D + d] = 0.f;
+            dattn[k * D3 + 2 * D + d] = s;
+        }
     }
     for (int i = tid; i < D * F; i += nt) {
         const int d = i / F, f = i - (i / F) * F;
-        dwf[(size_t)k * D * F + i] = a3s[d] * dv[f];
+        const float g = a3s[d] * dv[f];
+        dwf[(size_t)k * D * F + i] = (accumulate & 1) ? dwf[(size_t)k * D * F + i] + g : g;
     }
 }
 
@@ -221,7 +227,8 @@ size_t hsg_attn_params_bwd_workspace_floats(int H, int D) { return (size_t)kStag
 
 int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_part, int n_da1_part,
                         const float *da1_part, const float *attn, const float *wf, const float *bf, const float *T,
-                        float *dattn, float *dwf, float *dbf, float *dT, float *workspace, void *stream) {
+                        float *dattn, float *dwf, float *dbf, float *dT, float *workspace, int accumulate,
+                        void *stream) {
     if (!dims_ok(H, D, F) || n_dtau_part < 0 || n_da1_part < 0 || !dtau_part || !da1_part || !attn || !wf ||
         !T || !dattn || !dwf || !dT || !workspace)
         return HSG_EINVAL;
@@ -232,7 +239,7 @@ int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_
     int rc = status();
     if (rc) return rc;
     hipLaunchKernelGGL(k_attn_params_bwd, dim3(H + 1), dim3(256), 0, st, H, D, F, s0, s1, attn, wf, bf, T, dattn,
-                       dwf, dbf, dT);
+                       dwf, dbf, dT, accumulate);
     return status();
 }
 

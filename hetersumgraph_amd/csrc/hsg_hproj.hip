@@ -231,7 +231,7 @@ template <int CT, int HF>
 __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, const float *__restrict__ dZ,
                                                   int ldz, const float *__restrict__ W,
                                                   const uint32_t *__restrict__ bits, float scale,
-                                                  float *__restrict__ dX, int ldx) {
+                                                  float *__restrict__ dX, int ldx, int accumulate) {
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int nct = (in + 16 * CT - 1) / (16 * CT);
     const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -312,7 +312,10 @@ __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, c
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int gi = i0 + 4 * lk + r;
-            if (gi < n) dX[(long)gi * ldx + gc] = tot[t][r] * scale;
+            if (gi < n) {
+                const long o = (long)gi * ldx + gc;
+                dX[o] = accumulate ? dX[o] + tot[t][r] * scale : tot[t][r] * scale;
+            }
         }
     }
 }
@@ -466,12 +469,12 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
 }
 
 __global__ __launch_bounds__(256) void k_sum_parts(long total, int chunks, float scale, const float *__restrict__ part,
-                                                   float *__restrict__ out) {
+                                                   float *__restrict__ out, int accumulate) {
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         float s = 0.f;
 #pragma unroll 8
         for (int z = 0; z < chunks; ++z) s += part[(long)z * total + e];
-        out[e] = s * scale;
+        out[e] = accumulate ? out[e] + s * scale : s * scale;
     }
 }
 
@@ -535,7 +538,7 @@ int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const fl
 }
 
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W, const uint32_t *bits,
-                 float p, float *dX, int ldx, void *stream) {
+                 float p, float *dX, int ldx, int accumulate, void *stream) {
     if (n < 0 || in < 1 || H < 1 || D < 1 || ldz < H * D || !fits_buffers(n, in, H, D, ldz)) return HSG_EINVAL;
     if (n == 0) return 0;
     const float s = drop_scale(p);
@@ -545,11 +548,11 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const long wide = rtiles * ((in + 63) / 64);
     if (wide >= 2048) {
         hipLaunchKernelGGL((k_hproj_dx<4, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D, dZ,
-                           ldz, W, bits, s, dX, ldx);
+                           ldz, W, bits, s, dX, ldx, accumulate);
     } else {
         const long narrow = rtiles * ((in + 15) / 16);
         hipLaunchKernelGGL((k_hproj_dx<1, 4>), dim3((unsigned)((narrow + 3) / 4)), dim3(256), 0, st, n, in, H, D,
-                           dZ, ldz, W, bits, s, dX, ldx);
+                           dZ, ldz, W, bits, s, dX, ldx, accumulate);
     }
     return status();
 }
@@ -560,7 +563,7 @@ int hsg_hproj_dw_chunks(int n, int in, int H, int D) {
 }
 
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
-                 const uint32_t *bits, float p, float *part, float *dW, void *stream) {
+                 const uint32_t *bits, float p, float *part, float *dW, int accumulate, void *stream) {
     if (n < 0 || in < 1 || H < 1 || D < 1 || !part || !dW || ldx < in || ldz < H * D ||
         !fits_buffers(n, in, H, D, ldx > ldz ? ldx : ldz))
         return HSG_EINVAL;
@@ -576,7 +579,7 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     int blocks = (int)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(k_sum_parts, dim3(blocks), dim3(256), 0, st, total, n > 0 ? g.chunks : 0, drop_scale(p),
-                       part, dW);
+                       part, dW, accumulate);
     return status();
 }
 

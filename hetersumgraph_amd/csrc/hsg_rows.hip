@@ -163,18 +163,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
     }
 }
 
-// Column sums of up to two [rows][cols] partial slabs in one launch (block-row
-// partials of the FFN: GEMM colsum_part and hsg_ln_bwd's part).  Block =
-// (32 columns) x (8 row groups); group g sums rows g, g+8, ... in order, then
-// the 8 group sums are added in order -> deterministic.
-__global__ __launch_bounds__(256) void k_colsum2(int rows0, int cols0, const float *__restrict__ p0,
-                                                 float *__restrict__ o0, int rows1, int cols1,
-                                                 const float *__restrict__ p1, float *__restrict__ o1, int nb0) {
+// Column sums of the FFN backward's block-row partial slabs in one launch: the dH
+// GEMM's column partials hpart[rows_h][d_hid] -> db1, and hsg_ln_bwd's
+// part[rows_ln][3][d] -> dgamma, dbeta, db2.  Block = (32 columns) x (8 row
+// groups); group g sums rows g, g+8, ... in order, then the 8 group sums are added
+// in order -> deterministic.  accumulate: add into the outputs.
+__global__ __launch_bounds__(256) void k_ffn_colsums(int rows_h, int d_hid, const float *__restrict__ hpart,
+                                                     float *__restrict__ db1, int rows_ln, int d,
+                                                     const float *__restrict__ lnpart, float *__restrict__ dgamma,
+                                                     float *__restrict__ dbeta, float *__restrict__ db2, int nb0,
+                                                     int accumulate) {
     __shared__ float red[8][33];
     const bool second = (int)blockIdx.x >= nb0;
-    const int rows = second ? rows1 : rows0, cols = second ? cols1 : cols0;
-    const float *P = second ? p1 : p0;
-    float *O = second ? o1 : o0;
+    const int rows = second ? rows_ln : rows_h, cols = second ? 3 * d : d_hid;
+    const float *P = second ? lnpart : hpart;
     const int cb = (second ? (int)blockIdx.x - nb0 : (int)blockIdx.x) * 32;
     const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
     const int c = cb + cl;
@@ -193,7 +195,10 @@ __global__ __launch_bounds__(256) void k_colsum2(int rows0, int cols0, const flo
         float a = 0.f;
 #pragma unroll
         for (int q = 0; q < 8; ++q) a += red[q][cl];
-        O[c] = a;
+        float *o;
+        if (!second) o = db1 + c;
+        else o = c < d ? dgamma + c : (c < 2 * d ? dbeta + (c - d) : db2 + (c - 2 * d));
+        *o = accumulate ? *o + a : a;
     }
 }
 
@@ -253,14 +258,14 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
     return status();
 }
 
-int hsg_colsum2(int rows0, int cols0, const float *part0, float *out0, int rows1, int cols1, const float *part1,
-                float *out1, void *stream) {
-    if (rows0 < 0 || cols0 < 0 || rows1 < 0 || cols1 < 0) return HSG_EINVAL;
-    if ((cols0 && (!part0 || !out0)) || (cols1 && (!part1 || !out1))) return HSG_EINVAL;
-    const int nb0 = (cols0 + 31) / 32, nb1 = (cols1 + 31) / 32;
+int hsg_ffn_colsums(int rows_h, int d_hid, const float *hpart, float *db1, int rows_ln, int d, const float *lnpart,
+                    float *dgamma, float *dbeta, float *db2, int accumulate, void *stream) {
+    if (rows_h < 0 || d_hid < 0 || rows_ln < 0 || d < 0) return HSG_EINVAL;
+    if ((d_hid && (!hpart || !db1)) || (d && (!lnpart || !dgamma || !dbeta || !db2))) return HSG_EINVAL;
+    const int nb0 = (d_hid + 31) / 32, nb1 = (3 * d + 31) / 32;
     if (nb0 + nb1 == 0) return 0;
-    hipLaunchKernelGGL(k_colsum2, dim3(nb0 + nb1), dim3(256), 0, (hipStream_t)stream, rows0, cols0, part0, out0,
-                       rows1, cols1, part1, out1, nb0);
+    hipLaunchKernelGGL(k_ffn_colsums, dim3(nb0 + nb1), dim3(256), 0, (hipStream_t)stream, rows_h, d_hid, hpart, db1,
+                       rows_ln, d, lnpart, dgamma, dbeta, db2, nb0, accumulate);
     return status();
 }
 

@@ -11,7 +11,12 @@ Backward:              (dy, dx) = row kernel (LN + dropout backward, block parti
                        [GEMM, relu' epilogue]; dx += dH W1 [GEMM, accumulate
                        epilogue]; dW2 = dy^T H and dW1 = dH^T x [split-K GEMMs];
                        db1 from the dH GEMM's column-sum epilogue; one launch
-                       reduces both partial slabs.
+                       reduces both partial slabs (hsg_ffn_colsums).
+
+``ffn_fwd`` / ``ffn_bwd`` are the building blocks shared by the per-module
+autograd Function below and the fused stack (:mod:`hetersumgraph_amd.stack`),
+whose backward writes the parameter gradients straight into their destination
+(overwrite or accumulate) instead of returning them.
 """
 from __future__ import annotations
 
@@ -24,51 +29,74 @@ from .dense import gemm, row_tiles
 LN_EPS = 1e-5
 
 
+def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
+    """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  Returns (out, saved)."""
+    lib = load()
+    n, d = x.shape
+    H = gemm(x, w1, b_t=True, bias=b1, relu=True)          # [n, d_hid]
+    y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
+    out = torch.empty_like(x)
+    mean = x.new_empty(n)
+    rstd = x.new_empty(n)
+    seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
+    check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
+                         ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
+    return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
+
+
+def ffn_bwd(saved, dout, dst):
+    """Backward of :func:`ffn_fwd`.  ``dst`` = (dw1, acc_w1, dw2, acc_w2, db1, db2,
+    dgamma, dbeta, acc_b): gradient buffers shaped [d_hid, d], [d, d_hid], [d_hid],
+    [d], [d], [d] (None when not needed), each written or -- with its accumulate
+    flag -- added into.  Returns dx (a fresh tensor)."""
+    lib = load()
+    x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off = saved
+    dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
+    dout = dout.contiguous()
+    n, d = x.shape
+    st = stream_of(x)
+    nb = lib.hsg_ln_bwd_blocks(n)
+    d_hid = H.shape[1]
+    dy = torch.empty_like(x)
+    dx = torch.empty_like(x)
+    part = x.new_empty(nb, 3, d)
+    check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                         ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
+    rt = row_tiles(n, d_hid, d)
+    hpart = x.new_empty(rt, d_hid)
+    dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
+    gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
+    if dw2 is not None:
+        gemm(dy, H, a_t=True, out=dw2, add=dw2 if acc_w2 else None)  # [d, d_hid]
+    if dw1 is not None:
+        gemm(dH, x, a_t=True, out=dw1, add=dw1 if acc_w1 else None)  # [d_hid, d]
+    outs = [db1, dg, dbt, db2]
+    if any(o is not None for o in outs):
+        db1, dg, dbt, db2 = [o if o is not None else x.new_empty(n_)
+                             for o, n_ in zip(outs, (d_hid, d, d, d))]   # scratch for unneeded ones
+        check(lib.hsg_ffn_colsums(rt, d_hid, ptr(hpart), ptr(db1), nb, d, ptr(part), ptr(dg), ptr(dbt), ptr(db2),
+                                  int(bool(acc)), st), "hsg_ffn_colsums")
+    return dx
+
+
 class _FFN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, gamma, beta, p_drop, eps):
-        lib = load()
-        x = x.contiguous()
-        n, d = x.shape
-        w1 = w1.contiguous()
-        w2 = w2.contiguous()
-        H = gemm(x, w1, b_t=True, bias=b1, relu=True)          # [n, d_hid]
-        y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
-        out = torch.empty_like(x)
-        mean = x.new_empty(n)
-        rstd = x.new_empty(n)
-        seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
-        check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
-                             ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
+        out, saved = ffn_fwd(x.contiguous(), w1.contiguous(), b1, w2.contiguous(), b2, gamma, beta, p_drop, eps)
+        x, w1, w2, gamma, H, y, mean, rstd = saved[:8]
         ctx.save_for_backward(x, w1, w2, gamma, H, y, mean, rstd)
-        ctx.p_drop, ctx.seed_t, ctx.off = p_drop, seed_t, off
+        ctx.rest = saved[8:]
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        lib = load()
-        x, w1, w2, gamma, H, y, mean, rstd = ctx.saved_tensors
-        dout = dout.contiguous()
-        n, d = x.shape
-        nb = lib.hsg_ln_bwd_blocks(n)
-        d_hid = H.shape[1]
-        dy = torch.empty_like(x)
-        dx = torch.empty_like(x)
-        part = x.new_empty(nb, 3, d)
-        check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd),
-                             float(ctx.p_drop), ptr(ctx.seed_t), ctx.off, ptr(dy), ptr(dx), ptr(part),
-                             stream_of(x)), "hsg_ln_bwd")
-        rt = row_tiles(n, d_hid, d)
-        hpart = x.new_empty(rt, d_hid)
-        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
-        gemm(dH, w1, out=dx, add=dx)                           # dx += dH W1
-        dw2 = gemm(dy, H, a_t=True)                            # [d, d_hid]
-        dw1 = gemm(dH, x, a_t=True)                            # [d_hid, d]
-        db1 = x.new_empty(d_hid)
-        red = x.new_empty(3, d)                                # dgamma, dbeta, db2
-        check(lib.hsg_colsum2(rt, d_hid, ptr(hpart), ptr(db1), nb, 3 * d, ptr(part), ptr(red), stream_of(x)),
-              "hsg_colsum2")
-        dg, dbt, db2 = red
+        saved = tuple(ctx.saved_tensors) + ctx.rest
+        x, w1, w2 = saved[0], saved[1], saved[2]
+        d, d_hid = x.shape[1], w1.shape[0]
+        dw1, dw2 = torch.empty_like(w1), torch.empty_like(w2)
+        db1, db2 = x.new_empty(d_hid), x.new_empty(d)
+        dg, dbt = x.new_empty(d), x.new_empty(d)
+        dx = ffn_bwd(saved, dout, (dw1, False, dw2, False, db1, db2, dg, dbt, False))
         return dx, dw1, db1, dw2, db2, dg, dbt, None, None
 
 

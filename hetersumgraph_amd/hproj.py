@@ -6,6 +6,9 @@ training each head k projects its own dropout of the input,
 The H keep-masks are generated once per call as bits (seed in device memory,
 per-call offset) and shared by forward and backward; the H dropped copies of
 ``h`` are never materialised.
+
+``hproj_fwd`` / ``hproj_bwd`` are shared by the autograd Function below and the
+fused stack (:mod:`hetersumgraph_amd.stack`).
 """
 from __future__ import annotations
 
@@ -15,42 +18,53 @@ from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
 
 
+def hproj_fwd(X, W, H, D, p):
+    """Z [n, H*D] and the state its backward needs.  X, W contiguous fp32."""
+    lib = load()
+    n, d_in = X.shape
+    st = stream_of(X)
+    seed_t, off = hsg_rng.get(X.device).take()
+    bits = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=X.device)
+    check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
+    Z = X.new_empty(n, H * D)
+    check(lib.hsg_hproj_fwd(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D, st),
+          "hsg_hproj_fwd")
+    return Z, (X, W, bits, H, D, float(p))
+
+
+def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False):
+    """dX (into ``dX`` -- written or, with dX_acc, added) and dW (same, into ``dW``).
+    Either destination may be None (that gradient is skipped)."""
+    lib = load()
+    X, W, bits, H, D, p = saved
+    dZ = dZ.contiguous()
+    n, d_in = X.shape
+    st = stream_of(X)
+    if dX is not None:
+        check(lib.hsg_hproj_dx(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(bits), p, ptr(dX), d_in, int(dX_acc), st),
+              "hsg_hproj_dx")
+    if dW is not None:
+        part = X.new_empty(lib.hsg_hproj_dw_chunks(n, d_in, H, D) * H * D * d_in)
+        check(lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), p, ptr(part), ptr(dW),
+                               int(dW_acc), st), "hsg_hproj_dw")
+    return dX
+
+
 class _HeadProj(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, W, H, D, p):
-        lib = load()
-        X = X.contiguous()
-        W = W.contiguous()
-        n, d_in = X.shape
-        st = stream_of(X)
-        seed_t, off = hsg_rng.get(X.device).take()
-        bits = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=X.device)
-        check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
-        Z = X.new_empty(n, H * D)
-        check(lib.hsg_hproj_fwd(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D, st),
-              "hsg_hproj_fwd")
-        ctx.save_for_backward(X, W, bits)
+        Z, saved = hproj_fwd(X.contiguous(), W.contiguous(), H, D, p)
+        ctx.save_for_backward(saved[0], saved[1], saved[2])
         ctx.H, ctx.D, ctx.p = H, D, p
         return Z
 
     @staticmethod
     def backward(ctx, dZ):
-        lib = load()
         X, W, bits = ctx.saved_tensors
-        H, D, p = ctx.H, ctx.D, ctx.p
-        dZ = dZ.contiguous()
-        n, d_in = X.shape
-        st = stream_of(X)
-        dX = dW = None
-        if ctx.needs_input_grad[0]:
-            dX = torch.empty_like(X)
-            check(lib.hsg_hproj_dx(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(bits), float(p), ptr(dX), d_in, st),
-                  "hsg_hproj_dx")
-        if ctx.needs_input_grad[1]:
-            dW = torch.empty_like(W)
-            part = X.new_empty(lib.hsg_hproj_dw_chunks(n, d_in, H, D) * H * D * d_in)
-            check(lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), float(p), ptr(part),
-                                   ptr(dW), st), "hsg_hproj_dw")
+        saved = (X, W, bits, ctx.H, ctx.D, float(ctx.p))
+        dX = torch.empty_like(X) if ctx.needs_input_grad[0] else None
+        dW = torch.empty_like(W) if ctx.needs_input_grad[1] else None
+        hproj_bwd(saved, dZ, dX=dX, dW=dW)
         return dX, dW, None, None, None
 
 

@@ -94,6 +94,67 @@ class _GatAggregate(torch.autograd.Function):
         return dZ, da1, dtau, (dout if ctx.has_origin else None), None, None, None, None, None
 
 
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope):
+    """Forward of one multi-head application with the TF-IDF-table edge term:
+    3 launches (attention parameters -> tau table, sigma, edge pass).  Returns
+    (out, saved)."""
+    lib = load()
+    n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
+    if Z.shape != (n_src, HD):
+        raise ValueError(f"Z has shape {tuple(Z.shape)}, relation expects ({n_src}, {HD})")
+    if origin is not None and origin.shape != (n_dst, HD):
+        raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
+    F = T.shape[1]
+    st = stream_of(Z)
+    a1 = Z.new_empty(H, D)
+    tau = Z.new_empty(N_BOX + 1, H)
+    check(lib.hsg_attn_params_fwd(H, D, F, ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(a1), ptr(tau), st),
+          "hsg_attn_params_fwd")
+    sigma = Z.new_empty(n_src, H)
+    check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
+    relp = ctypes.byref(rel.cstruct())
+    h = Z.new_empty(n_dst, HD)
+    out = Z.new_empty(n_dst, HD) if origin is not None else None
+    m = Z.new_empty(n_dst, H)
+    l = Z.new_empty(n_dst, H)
+    check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                          ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+    saved = (Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, origin is not None)
+    return (out if origin is not None else h), saved
+
+
+def gat_table_bwd(saved, dout, dZ=True, dst=None):
+    """Backward of :func:`gat_table_fwd`: 3 launches (dst pass, src pass with the
+    d a1 partials, parameter backward).  Returns dZ (None with dZ=False).  ``dst`` =
+    (dattn, dwf, dbf, dT, acc_head, acc_T): gradient buffers written or added into
+    (dbf None on W2S).  The origin gradient is ``dout`` itself."""
+    lib = load()
+    Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin = saved
+    dout = dout.contiguous()
+    st = stream_of(Z)
+    relp = ctypes.byref(rel.cstruct())
+    G = torch.empty_like(h)
+    dpre = Z.new_empty(rel.n_typed, H)
+    nbd = lib.hsg_gat_bwd_blocks(relp)
+    dtp = Z.new_empty(nbd, N_BOX + 1, H)
+    check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
+                              ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                              ptr(dtp), st), "hsg_gat_bwd_dst")
+    dZt = torch.empty_like(Z)
+    nbs = lib.hsg_gat_bwd_src_blocks(relp)
+    da1p = Z.new_empty(nbs, H * D)
+    check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                              ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
+          "hsg_gat_bwd_src")
+    if dst is not None:
+        dattn, dwf, dbf, dT, acc_head, acc_T = dst
+        ws = Z.new_empty(lib.hsg_attn_params_bwd_workspace_floats(H, D))
+        check(lib.hsg_attn_params_bwd(H, D, T.shape[1], nbd, ptr(dtp), nbs, ptr(da1p), ptr(attn), ptr(wf),
+                                      ptr(bf), ptr(T), ptr(dattn), ptr(dwf), ptr(dbf), ptr(dT), ptr(ws),
+                                      int(bool(acc_head)) | (2 if acc_T else 0), st), "hsg_attn_params_bwd")
+    return dZt if dZ else None
+
+
 class _GatHeadsTable(torch.autograd.Function):
     """One multi-head application whose edge-type term comes from the TF-IDF table.
 
@@ -105,67 +166,25 @@ class _GatHeadsTable(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Z, attn, T, wf, bf, origin, rel, H, D, slope):
-        lib = load()
         Z = Z.contiguous()
         origin = None if origin is None else origin.contiguous()
-        n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
-        if Z.shape != (n_src, HD):
-            raise ValueError(f"Z has shape {tuple(Z.shape)}, relation expects ({n_src}, {HD})")
-        if origin is not None and origin.shape != (n_dst, HD):
-            raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
-        F = T.shape[1]
-        st = stream_of(Z)
-        a1 = Z.new_empty(H, D)
-        tau = Z.new_empty(N_BOX + 1, H)
-        check(lib.hsg_attn_params_fwd(H, D, F, ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(a1), ptr(tau), st),
-              "hsg_attn_params_fwd")
-        sigma = Z.new_empty(n_src, H)
-        check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
-        relp = ctypes.byref(rel.cstruct())
-        h = Z.new_empty(n_dst, HD)
-        out = Z.new_empty(n_dst, HD) if origin is not None else None
-        m = Z.new_empty(n_dst, H)
-        l = Z.new_empty(n_dst, H)
-        check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
-        ctx.save_for_backward(Z, attn, T, wf, bf, a1, sigma, tau, h, m, l)
-        ctx.rel, ctx.H, ctx.D, ctx.slope = rel, H, D, slope
-        ctx.has_origin = origin is not None
-        return out if origin is not None else h
+        out, saved = gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope)
+        ctx.save_for_backward(*saved[:11])
+        ctx.rest = saved[11:]
+        return out
 
     @staticmethod
     def backward(ctx, dout):
-        lib = load()
-        Z, attn, T, wf, bf, a1, sigma, tau, h, m, l = ctx.saved_tensors
-        rel, H, D, slope = ctx.rel, ctx.H, ctx.D, ctx.slope
-        dout = dout.contiguous()
-        st = stream_of(Z)
-        relp = ctypes.byref(rel.cstruct())
-        G = torch.empty_like(h)
-        dpre = Z.new_empty(rel.n_typed, H)
-        nbd = lib.hsg_gat_bwd_blocks(relp)
-        dtp = Z.new_empty(nbd, N_BOX + 1, H)
-        check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(ctx.has_origin), slope, ptr(Z), ptr(sigma),
-                                  ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                                  ptr(dtp), st), "hsg_gat_bwd_dst")
-        dZ = torch.empty_like(Z)
-        nbs = lib.hsg_gat_bwd_src_blocks(relp)
-        da1p = Z.new_empty(nbs, H * D)
-        check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
-                                  ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZ), None, ptr(da1p), st),
-              "hsg_gat_bwd_src")
-        dattn = torch.empty_like(attn)
-        dwf = torch.empty_like(wf)
+        saved = tuple(ctx.saved_tensors) + ctx.rest
+        attn, T, wf, bf = saved[1:5]
+        has_origin = saved[-1]
+        dattn, dwf, dT = torch.empty_like(attn), torch.empty_like(wf), torch.empty_like(T)
         dbf = torch.empty_like(bf) if bf is not None else None
-        dT = torch.empty_like(T)
-        ws = Z.new_empty(lib.hsg_attn_params_bwd_workspace_floats(H, D))
-        check(lib.hsg_attn_params_bwd(H, D, T.shape[1], nbd, ptr(dtp), nbs, ptr(da1p), ptr(attn), ptr(wf),
-                                      ptr(bf), ptr(T), ptr(dattn), ptr(dwf), ptr(dbf), ptr(dT), ptr(ws), st),
-              "hsg_attn_params_bwd")
         need = ctx.needs_input_grad
-        return (dZ if need[0] else None, dattn if need[1] else None, dT if need[2] else None,
+        dZ = gat_table_bwd(saved, dout, dZ=need[0], dst=(dattn, dwf, dbf, dT, False, False))
+        return (dZ, dattn if need[1] else None, dT if need[2] else None,
                 dwf if need[3] else None, dbf if need[4] else None,
-                (dout if ctx.has_origin else None), None, None, None, None)
+                (dout if has_origin else None), None, None, None, None)
 
 
 def gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, slope=LEAKY_SLOPE):

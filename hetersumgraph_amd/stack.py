@@ -1,0 +1,213 @@
+"""The WSWGAT stack as one autograd node (HiGraph.py:99-106).
+
+``HSumGraph.forward`` runs W2S, then ``n_iter`` x (S2W, W2S), over the same two
+modules: word2sent is applied n_iter+1 times, sent2word n_iter times, and every
+application reads the shared ``_TFembed`` table.  Run layer by layer through
+autograd, each extra application of a parameter costs a gradient-accumulation
+kernel (``p.grad += g``), and each state tensor used both as a residual origin and
+as the next layer's neighbour costs another (~30 small launches per cfg2 step).
+
+Here the whole stack is one ``torch.autograd.Function``: the forward runs the
+same C-ABI kernels in the same order (so dropout masks, drawn in call order, are
+the per-layer path's), and the backward walks the applications in reverse and
+lets the kernels do the sums in their epilogues:
+
+* parameter gradients go straight into ``p.grad`` -- written by the first
+  contribution when ``p.grad`` is None, added by every later one (GEMM ADD
+  epilogue, and the ``accumulate`` flag of hsg_hproj_dw / hsg_attn_params_bwd /
+  hsg_ffn_colsums), the same semantics as autograd's AccumulateGrad;
+* a state's gradient starts as the FFN backward's residual-branch ``dx`` of the
+  layer it was the origin of, and the head-projection backward of the layer it
+  was the neighbour of adds into it (hsg_hproj_dx accumulate).
+
+Parameters are inputs of the node (so autograd tracks them) but their returned
+gradients are None: they were already stored.  Gradient hooks registered on the
+parameters therefore do not fire on this path; ``HSumGraph`` falls back to the
+per-layer path (module/GAT.py) for anything it does not cover (CPU tensors, a
+foreign ``tfidfembed`` column, HSG_CHECK_NAN=1).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .dense import gemm
+from .ffn import ffn_bwd, ffn_fwd
+from .hproj import hproj_bwd, hproj_fwd
+from .ops import LEAKY_SLOPE, gat_table_bwd, gat_table_fwd
+
+
+def _grad_dst(p):
+    """(buffer, accumulate) for p's gradient: p.grad (accumulate) or a new tensor
+    installed as p.grad (written).  (None, False) if p needs no gradient."""
+    if p is None or not p.requires_grad:
+        return None, False
+    if p.grad is None:
+        p.grad = torch.empty_like(p)
+        return p.grad, False
+    return p.grad, True
+
+
+def _grad_group(ps):
+    """Buffers for parameters whose gradients one kernel writes together under one
+    accumulate flag: all fresh -> written; otherwise missing ones start at zero."""
+    live = [p for p in ps if p is not None and p.requires_grad]
+    if not live:
+        return [None] * len(ps), False
+    if all(p.grad is None for p in live):
+        for p in live:
+            p.grad = torch.empty_like(p)
+        acc = False
+    else:
+        for p in live:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        acc = True
+    return [p.grad if (p is not None and p.requires_grad) else None for p in ps], acc
+
+
+class _Layer:
+    """The tensors of one WSWGAT module (module/GAT.py:31-43) as the kernels take them."""
+
+    def __init__(self, m):
+        L, f = m.layer, m.ffn
+        self.kind = m.layerType
+        self.H, self.D = L.num_heads, L.head_dim
+        self.W, self.attn, self.wf, self.bf = L.fused_params()
+        self.w1, self.b1, self.w2, self.b2 = f.w_1.weight, f.w_1.bias, f.w_2.weight, f.w_2.bias
+        self.gamma, self.beta, self.eps = f.layer_norm.weight, f.layer_norm.bias, f.layer_norm.eps
+        self.p_attn = L.dropout.p if (L.dropout.training and L.dropout.p > 0) else 0.0
+        self.p_ffn = f.dropout.p if (f.dropout.training and f.dropout.p > 0) else 0.0
+
+    def params(self):
+        return [p for p in (self.W, self.attn, self.wf, self.bf, self.w1, self.b1, self.w2, self.b2,
+                            self.gamma, self.beta) if p is not None]
+
+
+def _apply_fwd(lay, rel, T, neighbor, origin):
+    """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59."""
+    H, D = lay.H, lay.D
+    if lay.p_attn > 0:
+        Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn)
+    else:
+        Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
+    x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE)
+    d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+    out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
+                          lay.p_ffn, lay.eps)
+    return out, (hsaved, neighbor, gsaved, fsaved)
+
+
+def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc):
+    """Backward of one application.  Parameter gradients go to p.grad; the
+    neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
+    not None.  Returns the origin's gradient (the FFN's residual-branch dx)."""
+    hsaved, neighbor, gsaved, fsaved = saved
+    d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+    dw1, a_w1 = _grad_dst(lay.w1)
+    dw2, a_w2 = _grad_dst(lay.w2)
+    (db1, db2, dg, dbt), a_b = _grad_group([lay.b1, lay.b2, lay.gamma, lay.beta])
+    dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
+                                dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b))
+    (dattn, dwf, dbf), a_h = _grad_group([lay.attn, lay.wf, lay.bf])
+    dT, a_T = _grad_dst(T)
+    need_dz = nb_grad is not None or lay.W.requires_grad
+    any_param = any(t is not None for t in (dattn, dwf, dbf, dT))
+    if any_param:                       # the kernel writes all four: scratch for unneeded ones
+        dattn, dwf, dT = [t if t is not None else torch.empty_like(p)
+                          for t, p in ((dattn, lay.attn), (dwf, lay.wf), (dT, T))]
+        if lay.bf is not None and dbf is None:
+            dbf = torch.empty_like(lay.bf)
+    dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=(dattn, dwf, dbf, dT, a_h, a_T) if any_param else None)
+    if need_dz:
+        dW, a_W = _grad_dst(lay.W)
+        if hsaved is not None:
+            hproj_bwd(hsaved, dZ, dX=nb_grad, dX_acc=nb_acc, dW=dW, dW_acc=a_W)
+        else:                                   # eval-mode projection Z = neighbor W^T
+            if nb_grad is not None:
+                gemm(dZ, lay.W, out=nb_grad, add=nb_grad if nb_acc else None)
+            if dW is not None:
+                gemm(dZ, neighbor, a_t=True, out=dW, add=dW if a_W else None)
+    return dx
+
+
+class _GatStack(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, cfg, w0, s0, *params):
+        G, w2s, s2w, T, n_iter = cfg
+        rw, rs = G.relation("W2S"), G.relation("S2W")
+        states = {("w", 0): w0.contiguous(), ("s", 0): s0.contiguous()}
+        apps = []                               # (layer, saved, neighbour key, origin key)
+
+        def run(lay, rel, nb, org, outk):
+            out, saved = _apply_fwd(lay, rel, T, states[nb], states[org])
+            states[outk] = out
+            apps.append((lay, saved, nb, org))
+
+        run(w2s, rw, ("w", 0), ("s", 0), ("s", 1))
+        for i in range(n_iter):
+            run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))
+            run(w2s, rw, ("w", i + 1), ("s", i + 1), ("s", i + 2))
+        ctx.cfg, ctx.apps = cfg, apps
+        ctx.need = (w0.requires_grad, s0.requires_grad)
+        ctx.shapes = {k: v.shape for k, v in states.items()}
+        return states[("s", n_iter + 1)]
+
+    @staticmethod
+    def backward(ctx, ds):
+        if ctx.apps is None:
+            raise RuntimeError("the fused WSWGAT stack's saved state was freed (backward called twice?)")
+        n_iter = ctx.cfg[4]
+        T = ctx.cfg[3]
+        grads = {("s", n_iter + 1): ds.contiguous()}
+        need_w0, need_s0 = ctx.need
+        skip = {("w", 0)} if not need_w0 else set()
+        if not need_s0:
+            skip.add(("s", 0))
+        for lay, saved, nb, org in reversed(ctx.apps):
+            dout = grads.pop((org[0], org[1] + 1))
+            nb_grad, nb_acc = None, False
+            if nb not in skip:
+                if nb in grads:
+                    nb_grad, nb_acc = grads[nb], True
+                else:
+                    nb_grad = saved[1].new_empty(ctx.shapes[nb])
+                    grads[nb] = nb_grad
+            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc)
+            if org in skip:
+                continue
+            if org in grads:
+                grads[org].add_(dx)
+            else:
+                grads[org] = dx
+        ctx.apps = None
+        dw0 = grads.get(("w", 0)) if need_w0 else None
+        ds0 = grads.get(("s", 0)) if need_s0 else None
+        n_params = len(ctx.needs_input_grad) - 3
+        return (None, dw0, ds0) + (None,) * n_params
+
+
+def fused_stack_ok(G, word2sent, sent2word, T, w, s):
+    """Whether :func:`gat_stack` covers this call (else use the per-layer path)."""
+    from .module.GATLayer import CHECK_NAN, table_weight
+    if os.environ.get("HSG_FUSED_STACK", "1") == "0":   # per-layer path (A/B tests)
+        return False
+    if CHECK_NAN or not (w.is_cuda and s.is_cuda) or w.dtype != torch.float32 or s.dtype != torch.float32:
+        return False
+    if word2sent.layerType != "W2S" or sent2word.layerType != "S2W":
+        return False
+    try:
+        tw = table_weight(G)
+    except KeyError:
+        return False
+    return tw is T and T.shape[1] == word2sent.layer.feat_weight.shape[2] == sent2word.layer.feat_weight.shape[2]
+
+
+def gat_stack(G, word2sent, sent2word, T, w, s, n_iter):
+    """Sentence (supernode) state after W2S + n_iter x (S2W, W2S) -- the loop of
+    HiGraph.py:99-106 -- as one autograd node (see the module docstring).
+    ``T`` is the ``_TFembed`` weight registered as the graph's tfidfembed table."""
+    w2s, s2w = _Layer(word2sent), _Layer(sent2word)
+    params = w2s.params() + s2w.params() + [T]
+    return _GatStack.apply((G, w2s, s2w, T, int(n_iter)), w, s, *params)

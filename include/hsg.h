@@ -108,13 +108,16 @@ int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, fl
  *      (hsg_gat_bwd_src, n_da1_part rows of H*D) in a fixed order (two launches,
  *      hsg_attn_params_bwd_workspace_floats(H, D) floats of workspace) and writes
  *      dattn [H][3D] (= [da1 | 0 | da3]), dwf [H][D][F], dbf [H][D] (if bf and dbf),
- *      dT [10][F].  H <= 16, H*D <= 512, F <= 256. */
+ *      dT [10][F] -- or adds into those buffers (a layer applied several times
+ *      per step: the gradient sums over its applications): accumulate bit 0 for
+ *      dattn / dwf / dbf, bit 1 for dT (the table is shared by both layer kinds).
+ *      H <= 16, H*D <= 512, F <= 256. */
 int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf, const float *bf,
                         const float *T, float *a1, float *tau, void *stream);
 int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_part, int n_da1_part,
                         const float *da1_part, const float *attn, const float *wf, const float *bf,
                         const float *T, float *dattn, float *dwf, float *dbf, float *dT, float *workspace,
-                        void *stream);
+                        int accumulate, void *stream);
 size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 
 /* ---- dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32) ---------------------------
@@ -154,10 +157,13 @@ int hsg_gemm_row_tiles(int M, int N, int K, int splits);
  * per-call constant; forward and backward with equal (seed, offset) agree.
  * d <= 512; p_drop in [0, 1). */
 int hsg_ln_bwd_blocks(int n);
-/* out0[c] = sum_r part0[r][c] (and the same for slab 1) in a fixed order, one launch:
- * the reduction of the FFN's block-row partials (GEMM colsum_part, hsg_ln_bwd part). */
-int hsg_colsum2(int rows0, int cols0, const float *part0, float *out0, int rows1, int cols1,
-                const float *part1, float *out1, void *stream);
+/* The FFN backward's bias / LayerNorm parameter gradients, one launch, fixed order:
+ *   db1[c] = sum_r hpart[r][c]                        (hsg_gemm_f32 colsum_part of dH)
+ *   dgamma[c], dbeta[c], db2[c] = sum_r lnpart[r][0..2][c]      (hsg_ln_bwd part)
+ * accumulate != 0: add into the outputs (a layer applied several times per step). */
+int hsg_ffn_colsums(int rows_h, int d_hid, const float *hpart, float *db1, int rows_ln, int d,
+                    const float *lnpart, float *dgamma, float *dbeta, float *db2, int accumulate,
+                    void *stream);
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
                float eps, float p_drop, const int64_t *seed, uint32_t offset,
                float *out, float *mean, float *rstd, void *stream);
@@ -179,7 +185,8 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
  *   hsg_hproj_dw:  dW[kD+d, c] = s * sum_i dZ[i, kD+d] bit X[i,c]
  *                  (part: hsg_hproj_dw_chunks(n,in,H,D) * H*D*in floats of workspace)
  * W is the fused fc weight [H*D][in] (row-major); s = 1/(1-p_eff) =
- * hsg_dropmask_scale(p).  Any H, D >= 1. */
+ * hsg_dropmask_scale(p).  Any H, D >= 1.  dx / dw with accumulate != 0 add into
+ * dX / dW instead of overwriting them. */
 int hsg_dropmask_words(int n, int in, int H);
 float hsg_dropmask_scale(float p);
 int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t offset, uint32_t *bits,
@@ -187,10 +194,10 @@ int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t of
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                   const uint32_t *bits, float p, float *Z, int ldz, void *stream);
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
-                 const uint32_t *bits, float p, float *dX, int ldx, void *stream);
+                 const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
-                 const uint32_t *bits, float p, float *part, float *dW, void *stream);
+                 const uint32_t *bits, float p, float *part, float *dW, int accumulate, void *stream);
 
 /* Device construction of one typed relation from the batched graph's COO edges.
  * Replaces DGL's per-call filter_nodes/filter_edges (GATLayer.py:105-107, 143-145),

@@ -17,7 +17,8 @@ def unpack(bits, n):
 
 @pytest.mark.parametrize("n,d_in,H,D", [(19200 // 4, 300, 8, 8), (1120, 64, 6, 50), (333, 70, 3, 16),
                                          (65, 33, 1, 64), (200, 40, 3, 5), (130, 50, 2, 75),
-                                         (97, 300, 16, 25)])
+                                         (97, 300, 16, 25), (1000, 64, 16, 4), (257, 128, 3, 16),
+                                         (70, 300, 8, 8)])
 def test_head_projection_matches_masked_reference(n, d_in, H, D):
     from hetersumgraph_amd import _lib, rng
     from hetersumgraph_amd.hproj import _HeadProj
