@@ -17,6 +17,10 @@ OUT = os.path.join(HERE, "libhsg.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
 HEADERS = [os.path.join(ROOT, "include", "hsg.h"), os.path.join(HERE, "csrc", "hsg_rng.h")]
+# host-only graph builder (no HIP runtime: usable in DataLoader workers)
+HOST_SOURCES = [os.path.join(HERE, "csrc", "hsg_graphbuild.cpp")]
+HOST_HEADERS = [os.path.join(ROOT, "include", "hsg_graph.h")]
+HOST_OUT = os.path.join(HERE, "libhsg_host.so")
 
 
 def hipcc():
@@ -56,7 +60,23 @@ def _compile(src, force, verbose):
     return obj
 
 
+def build_host(force=False, verbose=True):
+    """libhsg_host.so with g++ (the native graph builder, include/hsg_graph.h)."""
+    if not force and os.path.exists(HOST_OUT):
+        t = os.path.getmtime(HOST_OUT)
+        if all(os.path.getmtime(s) <= t for s in HOST_SOURCES + HOST_HEADERS):
+            return HOST_OUT
+    cmd = [os.environ.get("CXX", "g++"), "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-pthread",
+           "-I", os.path.join(ROOT, "include"), "-o", HOST_OUT + ".tmp"] + HOST_SOURCES
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(HOST_OUT + ".tmp", HOST_OUT)
+    return HOST_OUT
+
+
 def build(force=False, verbose=True):
+    build_host(force=force, verbose=verbose)
     if not force and not needs_build():
         return OUT
     os.makedirs(OBJDIR, exist_ok=True)

@@ -129,6 +129,9 @@ class DGLGraph:
         for k, val in (data or {}).items():
             self.edata.write(k, torch.arange(old, old + m), torch.as_tensor(val))
 
+    def add_edge(self, u, v, data=None):
+        self.add_edges(u, v, data)
+
     @property
     def nodes(self):
         return _View(self.ndata, lambda: self.n)

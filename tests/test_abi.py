@@ -44,3 +44,16 @@ def test_code_object_is_gfx950():
     from hetersumgraph_amd import _lib
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_host_library_exports_graph_builder():
+    """libhsg_host.so (g++, no HIP runtime) exports every symbol include/hsg_graph.h declares."""
+    from hetersumgraph_amd import build, datapipe
+    build.build_host(verbose=False)
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "hsg_graph.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b(hsg_[a-z0-9_]+)\s*\(", src)))
+    assert names == ["hsg_graph_count", "hsg_graph_fill"]
+    lib = ctypes.CDLL(datapipe.HOST_LIB)
+    for name in names:
+        assert hasattr(lib, name), name
+    assert ctypes.sizeof(datapipe.HsgDocs) == 8 + 12 * 8
