@@ -1,20 +1,21 @@
 """Sentence CNN encoder (reference: module/Encoder.py:18-76).
 
-Not part of the WSWGAT hot path but in the logits
-path, so it is provided with the reference's parameter layout
-(``ngram_enc.{embed,position_embedding,convs.0-5}``).  Differences in *how*:
-positions are built with one tensor op on the input's device instead of a Python
-loop over sentences (Encoder.py:60-66), and the six convolutions run through
-MIOpen/PyTorch.
+Not part of the WSWGAT hot path but in the logits path and the
+next row of SURVEY §8f (rank 3).  Same parameter layout as the reference
+(``ngram_enc.{embed,position_embedding,convs.0-5}``), so state_dicts load unchanged.
+Differences in *how*: no Python loop over sentences for the positions
+(Encoder.py:60-66), and the six convolutions + ReLU + max-pool run as one MFMA GEMM
+over the sentences' real rows plus the HIP gather / pool kernels
+(:mod:`hetersumgraph_amd.cnn`, hsg_cnn.hip).  There is no CPU path.
 """
 from __future__ import annotations
 
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 import torch.nn.init as init
 
+from ..cnn import sent_cnn
 from .PositionEmbedding import get_sinusoid_encoding_table
 
 WORD_PAD = "[PAD]"
@@ -35,16 +36,7 @@ class sentEncoder(nn.Module):
             init.xavier_normal_(conv.weight.data, gain=np.sqrt(6.0))
 
     def forward(self, input):
-        # input: [n_sent, L] token ids, PAD = 0
-        L = input.shape[1]
-        sent_len = (input != 0).sum(dim=1, keepdim=True)
-        ar = torch.arange(1, L + 1, device=input.device).unsqueeze(0)
-        lim = torch.clamp(sent_len, max=self.sent_max_len)
-        pos = torch.where(ar <= lim, ar, torch.zeros_like(ar))
-        x = self.embed(input) + self.position_embedding(pos)
-        x = x.unsqueeze(1)                                        # [n, 1, L, D]
-        feats = []
-        for conv in self.convs:
-            y = F.relu(conv(x)).squeeze(3)                        # [n, 50, L-kh+1]
-            feats.append(torch.amax(y, dim=2))                    # max-pool over time
-        return torch.cat(feats, 1)                                # [n, 300]
+        # input: [n_sent, L] token ids, PAD = 0 (trailing) -> [n_sent, 300]
+        return sent_cnn(input, self.embed.weight, self.position_embedding.weight,
+                        [c.weight for c in self.convs], [c.bias for c in self.convs],
+                        padding_idx=getattr(self.embed, "padding_idx", None))

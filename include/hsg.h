@@ -222,6 +222,28 @@ int hsg_rel_build(float src_unit, float dst_unit, int n_nodes, int n_edges, cons
                   int64_t *src_nodes, int64_t *dst_nodes, void *workspace, size_t workspace_bytes,
                   void *stream);
 
+/* ---- sentence CNN encoder (module/Encoder.py:56-76) --------------------------------
+ * Six Conv2d(1, 50, (h, D)), h = 2..7, + ReLU + max-pool over time, restated as one
+ * GEMM Y = X Wall^T (hsg_gemm_f32; Wall [27*50][D], row (tap(h,i))*50 + c =
+ * W_h[c][0][i][:], taps ordered h = 2..7, i = 0..h-1) plus a shifted sum.  X holds
+ * only the rows a window can see: for sentence s, rows rowoff[s] .. rowoff[s]+len_s-1
+ * are embed[ids[s][t]] + pos[t+1] and row rowoff[s]+len_s is the pad row embed[0] +
+ * pos[0] (rowoff [n+1], rowoff[s+1]-rowoff[s] = len_s+1; padding must be trailing).
+ *   hsg_cnn_gather:   builds X [rows][D].
+ *   hsg_cnn_pool:     feat[s][(h-2)*50+c] = relu(max_t (b_h[c] + sum_i Y[row(s,t+i)][tap(h,i)*50+c]))
+ *                     and arg = the first t of the max (CPU max_pool1d order); bias = 6
+ *                     device pointers (host array).
+ *   hsg_cnn_pool_bwd: adds dfeat (ReLU-masked) into the h rows of each max window of a
+ *                     zero-filled dY [rows][lddy]; then dWall = dY^T X (hsg_gemm_f32).
+ * hsg_cnn_taps() = 27*50 (columns of Y).  ldy, lddy >= 1350. */
+int hsg_cnn_taps(void);
+int hsg_cnn_gather(int n, int L, int D, const int64_t *ids, const float *embed, const float *pos,
+                   const int32_t *rowoff, long rows, float *X, void *stream);
+int hsg_cnn_pool(int n, int L, const int32_t *rowoff, const float *Y, int ldy, const float *const *bias,
+                 float *feat, int32_t *arg, void *stream);
+int hsg_cnn_pool_bwd(int n, const int32_t *rowoff, const float *feat, const int32_t *arg, const float *dfeat,
+                     float *dY, int lddy, void *stream);
+
 /* Library build identification (ABI version, gfx target). */
 const char *hsg_version(void);
 

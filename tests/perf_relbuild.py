@@ -1,12 +1,13 @@
-"""Dev tool: time hsg_rel_build (device) for the cfg2 batch against the numpy
+"""Timing script (GPU; tests/ may use the oracle as a baseline; not collected by pytest): time hsg_rel_build (device) for the cfg2 batch against the numpy
 restatement oracle.fused.typed_relation + CSR/CSC sorts (host)."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import numpy as np
 import torch
 from hetersumgraph_amd import synth
 from hetersumgraph_amd.relation import build_relation
-from tests.test_gpu_relbuild import batch, expected
+from test_gpu_relbuild import batch, expected
 
 dev = torch.device("cuda", 0)
 for cfg in ("cfg2", "cfg5"):
