@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--n-iter", type=int, default=2)
+    ap.add_argument("--dtype", choices=("f32", "bf16"), default="f32",
+                    help="GEMM operand precision: f32 (parity contract) or bf16 (config 5)")
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -61,6 +63,13 @@ def cpu_model():
     except OSError:
         pass
     return platform.processor()
+
+
+def workload_shape(config):
+    from hetersumgraph_amd import synth
+    kind, per_gpu, p = synth.CONFIGS[config]
+    shape = ", ".join(f"{k}={v}" for k, v in p.items())
+    return f"{per_gpu} {kind.upper()} docs/GPU x ({shape})"
 
 
 def make_shard(config, rank, world, seed):
@@ -236,6 +245,8 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     from hetersumgraph_amd import _lib
     _lib.load()
+    from hetersumgraph_amd.dense import set_gemm_dtype
+    set_gemm_dtype(args.dtype)
 
     docs, G, E_global = make_shard(args.config, rank, world, args.seed)
     E_total = G.number_of_edges()
@@ -345,10 +356,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": args.dtype,
         "data": "synthetic (seeded CNN/DM-shaped graphs, random-init weights of the reference architecture)",
         "config": {"workload": f"{args.config}: HSG WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) fwd+bwd, "
-                               "train mode, 32 docs/GPU x (N=35, W=600, k=36)",
+                               f"train mode, {workload_shape(args.config)}",
+                   "gemm_operands": args.dtype,
+                   "edge_kernels_ln_head_projection": "f32",
                    "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
                    "typed_edges_per_direction": rel_w.n_typed,
                    "dropout": args.dropout, "parallelism": f"dp{world}",

@@ -21,6 +21,8 @@
 //     consecutive columns -> conflict-free).
 // K of one MFMA k-step s (0..15) is s for lanes 0-31 and 16+s for lanes 32-63,
 // identically for A and B, so the sum over a 32-deep tile is exact.
+// BF = true (hsg_gemm_bf16): the same tiles, operands rounded to bf16 (RNE) when the
+// fragments are read from LDS, v_mfma_f32_32x32x16_bf16 with fp32 accumulation.
 // Split-K (grid.z > 1) writes fp32 partial slabs, reduced (with the epilogue) by
 // k_splitk_reduce in split order -> deterministic.
 #include <hip/hip_runtime.h>
@@ -35,6 +37,7 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kBK = 32;
 constexpr int kPad = 4;
@@ -143,7 +146,7 @@ struct Stage {
 __device__ unsigned long long g_census[16384 * 4];
 #endif
 
-template <int BM, int BN, bool AK, bool BKC, int NBUF, int BK>
+template <int BM, int BN, bool AK, bool BKC, int NBUF, int BK, bool BF = false>
 __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
 #ifdef HSG_GEMM_CENSUS
     const unsigned long long c_t0 = __builtin_readcyclecounter();
@@ -240,6 +243,47 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
                 }
             }
         };
+        if constexpr (BF) {
+            // bf16 operands (RNE from the fp32 LDS image), fp32 accumulate:
+            // v_mfma_f32_32x32x16_bf16, lane (li, h) element j <-> k = h*BK/2 + 8s + j
+#pragma unroll
+            for (int s8 = 0; s8 < BK / 16; ++s8) {
+                bf16x8 xa[TM], xb[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int row = wm * WM + i * 32 + li;
+                    if constexpr (AK) {
+                        const float *q = a_s + row * SA::LD + h * (BK / 2) + 8 * s8;
+                        const f32x4 lo = *reinterpret_cast<const f32x4 *>(q);
+                        const f32x4 hi = *reinterpret_cast<const f32x4 *>(q + 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) { xa[i][e] = (__bf16)lo[e]; xa[i][4 + e] = (__bf16)hi[e]; }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) xa[i][e] = (__bf16)a_s[(h * (BK / 2) + 8 * s8 + e) * SA::LD + row];
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int col = wn * WN + j * 32 + li;
+                    if constexpr (BKC) {
+                        const float *q = b_s + col * SB::LD + h * (BK / 2) + 8 * s8;
+                        const f32x4 lo = *reinterpret_cast<const f32x4 *>(q);
+                        const f32x4 hi = *reinterpret_cast<const f32x4 *>(q + 4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) { xb[j][e] = (__bf16)lo[e]; xb[j][4 + e] = (__bf16)hi[e]; }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) xb[j][e] = (__bf16)b_s[(h * (BK / 2) + 8 * s8 + e) * SB::LD + col];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[i], xb[j], acc[i][j], 0, 0, 0);
+            }
+        } else {
         frag(af[0], bf[0], 0);
 #pragma unroll
         for (int g = 0; g < BK / 8; ++g) {
@@ -252,6 +296,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[g & 1][i][q], bf[g & 1][j][q],
                                                                           acc[i][j], 0, 0, 0);
+        }
         }
         if constexpr (NBUF == 2) {
             if (more) {
@@ -355,7 +400,7 @@ long resident_blocks(bool a, int b, F kernel_of) {
     return (long)cus * per;
 }
 
-template <int BM, int BN, int NBUF = 2, int BK = kBK>
+template <int BM, int BN, int NBUF = 2, int BK = kBK, bool BF = false>
 int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     const int kt_total = (p.K + BK - 1) / BK;
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
@@ -367,19 +412,19 @@ int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     long g = tiles;
     if (NBUF == 1) {
         const long cap = resident_blocks(ak, bk ? 1 : 0, [&](int a, int b) -> const void * {
-            if (a && b) return (const void *)k_gemm<BM, BN, true, true, NBUF, BK>;
-            if (a) return (const void *)k_gemm<BM, BN, true, false, NBUF, BK>;
-            if (b) return (const void *)k_gemm<BM, BN, false, true, NBUF, BK>;
-            return (const void *)k_gemm<BM, BN, false, false, NBUF, BK>;
+            if (a && b) return (const void *)k_gemm<BM, BN, true, true, NBUF, BK, BF>;
+            if (a) return (const void *)k_gemm<BM, BN, true, false, NBUF, BK, BF>;
+            if (b) return (const void *)k_gemm<BM, BN, false, true, NBUF, BK, BF>;
+            return (const void *)k_gemm<BM, BN, false, false, NBUF, BK, BF>;
         });
         if (cap > 0 && cap < g) g = cap;
     }
     if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
-    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK>), grid, dim3(256), 0, st, p);
-    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF, BK>), grid, dim3(256), 0, st, p);
-    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF, BK>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false, NBUF, BK>), grid, dim3(256), 0, st, p);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, false, true, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm<BM, BN, false, false, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -425,9 +470,13 @@ int hsg_gemm_row_tiles(int M, int N, int K, int splits) {
     return (M + bm - 1) / bm;
 }
 
-int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
-                 int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
-                 int relu, int splits, float *workspace, float *colsum_part, void *stream) {
+}  // extern "C"
+
+namespace {
+
+int gemm_impl(bool bf16, int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+              int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
+              int relu, int splits, float *workspace, float *colsum_part, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
@@ -449,7 +498,12 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
         if (!colsum_part) best = atoi(f);
     int rc;
-    if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
+    if (bf16) {
+        // bf16 operands: the two single-buffer plans (the K loop is load-bound, so the
+        // deeper tiles of the f32 plan table do not pay)
+        if (best == 4) rc = launch_tiles<128, 64, 1, kBK, true>(p, ak, bk, splits, st);
+        else rc = launch_tiles<64, 64, 1, kBK, true>(p, ak, bk, splits, st);
+    } else if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
     else if (best == 1) rc = launch_tiles<128, 64>(p, ak, bk, splits, st);
     else if (best == 2) rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
     else if (best == 3) rc = launch_tiles<128, 128, 1>(p, ak, bk, splits, st);
@@ -466,6 +520,24 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
     hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, st, p, splits);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                 int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
+                 int relu, int splits, float *workspace, float *colsum_part, void *stream) {
+    return gemm_impl(false, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
+                     splits, workspace, colsum_part, stream);
+}
+
+int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                  int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
+                  int relu, int splits, float *workspace, float *colsum_part, void *stream) {
+    return gemm_impl(true, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
+                     splits, workspace, colsum_part, stream);
 }
 
 #ifdef HSG_GEMM_CENSUS

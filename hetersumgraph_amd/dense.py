@@ -4,13 +4,47 @@
 ``op(X) = X.T if x_t else X``, plus the fused epilogues the FFN and the head
 projection need (bias, ReLU, ReLU-backward mask, accumulate).  Everything is
 enqueued on the current stream; no host synchronisation.
+
+Operand precision: fp32 (hsg_gemm_f32, the default and the parity contract) or,
+for the bf16 configuration (config 5), fp32 storage with bf16-rounded
+MFMA operands and fp32 accumulation (hsg_gemm_bf16) -- chosen process-wide with
+:func:`set_gemm_dtype` / :func:`gemm_dtype` or ``HSG_GEMM_DTYPE=bf16``.
 """
 from __future__ import annotations
+
+import contextlib
+import os
 
 import torch
 
 from . import _lib
 from ._lib import HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr, stream_of
+
+
+_GEMM_DTYPE = os.environ.get("HSG_GEMM_DTYPE", "f32")
+
+
+def set_gemm_dtype(dtype):
+    """'f32' (exact fp32 MFMA) or 'bf16' (bf16 operands, fp32 accumulate) for every
+    GEMM issued through :func:`gemm` (FFN, sentence CNN)."""
+    global _GEMM_DTYPE
+    if dtype not in ("f32", "bf16"):
+        raise ValueError(f"gemm dtype must be 'f32' or 'bf16', not {dtype!r}")
+    _GEMM_DTYPE = dtype
+
+
+def get_gemm_dtype():
+    return _GEMM_DTYPE
+
+
+@contextlib.contextmanager
+def gemm_dtype(dtype):
+    prev = _GEMM_DTYPE
+    set_gemm_dtype(dtype)
+    try:
+        yield
+    finally:
+        set_gemm_dtype(prev)
 
 
 def _ld(t):
@@ -20,14 +54,16 @@ def _ld(t):
 
 
 def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=None, add=None,
-         splits=0, workspace=None, colsum_part=None):
+         splits=0, workspace=None, colsum_part=None, dtype=None):
     """C = op(A) @ op(B) [+ bias] [relu] | * (relu_mask > 0) | + add.
 
     A [M,K] (or [K,M] with a_t), B [K,N] (or [N,K] with b_t), fp32 on the GPU.
     ``add`` may be ``out`` itself (accumulate).  ``colsum_part``: a tensor of
     ``row_tiles(M, N, K) * N`` floats that receives per-tile-row column sums of C
-    (unsplit GEMMs)."""
+    (unsplit GEMMs).  ``dtype``: 'f32' / 'bf16' operands (default: the process-wide
+    setting)."""
     lib = load()
+    fn = lib.hsg_gemm_bf16 if (dtype or _GEMM_DTYPE) == "bf16" else lib.hsg_gemm_f32
     if not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
         raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
     M, K = (A.shape[1], A.shape[0]) if a_t else (A.shape[0], A.shape[1])
@@ -47,9 +83,9 @@ def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=
     if splits > 1:
         n = lib.hsg_gemm_workspace_floats(M, N, K, splits)
         ws = workspace if workspace is not None and workspace.numel() >= n else A.new_empty(n)
-    check(lib.hsg_gemm_f32(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), ptr(out),
+    check(fn(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), ptr(out),
                            _ld(out), ptr(bias), ptr(aux), _ld(aux) if aux is not None else 0, epi,
-                           int(relu), int(splits), ptr(ws), ptr(colsum_part), stream_of(A)), "hsg_gemm_f32")
+                           int(relu), int(splits), ptr(ws), ptr(colsum_part), stream_of(A)), fn.__name__)
     return out
 
 

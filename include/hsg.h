@@ -145,6 +145,15 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
  * C, [hsg_gemm_row_tiles(M,N,K,splits)][N] -- e.g. the bias gradient of the FFN's
  * first layer taken from the dH epilogue instead of a second pass over dH. */
 int hsg_gemm_row_tiles(int M, int N, int K, int splits);
+/* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
+ * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
+ * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
+ * bf16).  Products of bf16 values are exact in fp32, so the result equals
+ * an fp32 GEMM of the rounded operands up to fp32 summation order. */
+int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig,
+                  const float *B, int ldb, int b_kcontig, float *C, int ldc,
+                  const float *bias, const float *aux, int ldaux, int epi, int relu,
+                  int splits, float *workspace, float *colsum_part, void *stream);
 
 /* ---- PositionwiseFeedForward row epilogue (GATLayer.py:40-42) -------------------
  * Forward:  s = dropout(y; p, seed, offset) + x;  out = (s-mean)*rstd*gamma + beta

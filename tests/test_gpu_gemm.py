@@ -93,3 +93,41 @@ def test_speed_smoke():
     torch.cuda.synchronize()
     ms2 = e0.elapsed_time(e1) / 20
     print(f"torch linear same shape: {ms2 * 1e3:.1f} us, {2 * 19200 * 300 * 512 / (ms2 * 1e-3) / 1e12:.1f} TFLOP/s")
+
+
+# ---- hsg_gemm_bf16: bf16-rounded operands, fp32 accumulation (config 5) ----------
+def bf16_ref(A, B, a_t, b_t):
+    """fp64 GEMM of the operands rounded to bf16 (RNE, as v_cvt_pk_bf16_f32): every
+    bf16 x bf16 product is exact in fp32, so only the fp32 summation differs."""
+    return ref(A.bfloat16().float(), B.bfloat16().float(), a_t, b_t)
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("a_t,b_t", [(False, False), (False, True), (True, False), (True, True)])
+def test_bf16_layouts(M, N, K, a_t, b_t):
+    from hetersumgraph_amd.dense import gemm
+    torch.manual_seed(M + N + K + 1)
+    A = mk(K, M) if a_t else mk(M, K)
+    B = mk(N, K) if b_t else mk(K, N)
+    C = gemm(A, B, a_t, b_t, dtype="bf16")
+    err = (C.double() - bf16_ref(A, B, a_t, b_t)).abs().max().item()
+    assert err <= 1e-5 * max(1.0, K ** 0.5) * 4, err
+    # and it is a real reduced-precision result: far from the fp32 GEMM at large K
+    if K >= 300:
+        assert (C.double() - ref(A, B, a_t, b_t)).abs().max().item() > 1e-4
+
+
+def test_bf16_epilogue_and_split_k():
+    from hetersumgraph_amd.dense import gemm, gemm_dtype
+    torch.manual_seed(5)
+    X = torch.randn(777, 300, device="cuda")
+    W = torch.randn(512, 300, device="cuda")
+    b = torch.randn(512, device="cuda")
+    with gemm_dtype("bf16"):
+        H = gemm(X, W, b_t=True, bias=b, relu=True)
+        A = torch.randn(4000, 300, device="cuda")
+        B = torch.randn(4000, 512, device="cuda")
+        C = gemm(A, B, a_t=True, splits=7)
+    Hr = torch.relu(bf16_ref(X, W, False, True) + b.double())
+    assert (H.double() - Hr).abs().max().item() < 1e-4
+    assert (C.double() - bf16_ref(A, B, True, False)).abs().max().item() < 2e-3

@@ -101,3 +101,22 @@ def test_train_step_runs_and_learns():
         G.ndata.pop("loss")          # train.py gets a fresh graph every step
         losses.append(loss.item())
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("name,cls,seed", [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5)])
+def test_model_logits_bf16_gemm_error_budget(name, cls, seed):
+    """Config-5 precision mode (bf16 GEMM operands, fp32 accumulate and storage): the
+    logits stay within the SURVEY §8c bf16 budget (2e-2) of the reference fp64 run.
+    This is a reduced-precision mode, not the 1e-4 fp32 contract."""
+    from hetersumgraph_amd.dense import gemm_dtype
+    z = load_fixture(name)
+    G = build_graph(z, z["sent_words"], z["sent_label"])
+    G.to(torch.device("cuda"))
+    model = build_model(cls, seed)
+    model.lstm.train()
+    model.lstm.dropout = 0.0
+    with gemm_dtype("bf16"):
+        logits = model(G)
+    err = np.abs(logits.detach().cpu().double().numpy() - z["logits64"]).max()
+    print(f"{name}: bf16-GEMM logit max |diff| vs reference fp64 = {err:.3e}")
+    assert err <= 2e-2, err
