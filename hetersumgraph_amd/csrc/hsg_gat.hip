@@ -31,6 +31,8 @@
 
 namespace {
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ void wave_lds_sync() {
     // Order this wave's LDS writes before its own subsequent reads by other lanes.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -353,6 +355,150 @@ __global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, in
         if (kact && l == 0) {
             mout[v * H + k] = any ? mx : 0.f;
             lout[v * H + k] = any ? sm : 1.f;
+        }
+    }
+}
+
+// Row-tile forward for short segments (S2W at config 2: ~2 in-edges per word,
+// H*D = 300).  A block owns RT consecutive destinations, i.e. one contiguous
+// RT*H*D-float band of origin / h / out, and streams it as float4 slots
+// (slot q -> row q / (HD/4), columns 4(q % (HD/4)) .. +3; a slot may straddle two
+// heads, so each component carries its own head index).
+//   phase A: thread p < RT*H owns (row r, head k) = (p / H, p % H): online
+//            (max, sum) over the row's CSR segment in edge order, scores parked in
+//            LDS; after the phantom fold, the same thread turns them into alphas.
+//   phase B: every slot sums alpha * Z[src] (float4 gathers) over its row's edges
+//            in CSR order, then writes h and elu(h) + origin with float4 stores.
+// Block edge ranges longer than kRowsEcap edges are processed in kRowsEcap chunks
+// (scores recomputed for the chunks after the first).  The origin band is loaded
+// before phase A so the HBM stream overlaps the index -> score chain.
+constexpr int kRowsThreads = 256;
+constexpr int kRowsEcap = 512;            // edges staged per chunk
+constexpr int kRowsAlpha = 4096;          // floats of staged alphas (kRowsEcap x H <= this)
+constexpr int kRowsMaxPairs = 512;        // RT * H bound
+
+template <int NQ, int TAU_MODE>
+__global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H, int D, int RT, float slope,
+                                                               const float *__restrict__ Z,
+                                                               const float *__restrict__ sigma,
+                                                               const float *__restrict__ tau,
+                                                               const float *__restrict__ origin,
+                                                               float *__restrict__ hout, float *__restrict__ out,
+                                                               float *__restrict__ mout, float *__restrict__ lout) {
+    __shared__ int s_ptr[kRowsMaxPairs + 1];
+    __shared__ int s_src[kRowsEcap];
+    __shared__ float s_alpha[kRowsAlpha];
+    __shared__ float s_m[kRowsMaxPairs], s_inv[kRowsMaxPairs];
+    const int HD = H * D, HD4 = HD >> 2;
+    const int ecap = min(kRowsEcap, kRowsAlpha / H);
+    const int t = threadIdx.x;
+    const int v0 = blockIdx.x * RT;
+    const int rows = min(RT, R.n_dst - v0);
+    const int nslot = rows * HD4;
+    // slot geometry and the residual band, issued first
+    // skh: head k0 of the slot's first column and the component b from which the
+    // columns belong to head k0 + 1 (b = 4: none), packed as k0 * 8 + b
+    int srow[NQ], scol[NQ], skh[NQ];
+    f32x4_t org[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const int q = t + kRowsThreads * i;
+        const int qc = q < nslot ? q : nslot - 1;          // clamped (never stored)
+        srow[i] = qc / HD4;
+        scol[i] = (qc - srow[i] * HD4) * 4;
+        const int k0 = scol[i] / D;
+        skh[i] = k0 * 8 + min(4, (k0 + 1) * D - scol[i]);
+        org[i] = origin ? *reinterpret_cast<const f32x4_t *>(origin + (size_t)(v0 + srow[i]) * HD + scol[i])
+                        : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int r = t; r <= rows; r += kRowsThreads) s_ptr[r] = R.indptr[v0 + r];
+    __syncthreads();
+    const int E0 = s_ptr[0], E1 = s_ptr[rows];
+    // phase A: per (row, head) softmax state
+    for (int p = t; p < rows * H; p += kRowsThreads) {
+        const int r = p / H, k = p - (p / H) * H;
+        const int beg = s_ptr[r], end = s_ptr[r + 1];
+        float mx = -INFINITY, sm = 0.f;
+        for (int e = beg; e < end; ++e) {
+            const int u = R.src[e];
+            const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+            if (e - E0 < ecap) {
+                s_alpha[(e - E0) * H + k] = s;
+                if (k == 0) s_src[e - E0] = u;
+            }
+            if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
+            else sm += __expf(s - mx);
+        }
+        const int c = R.phantom[v0 + r];
+        if (c > 0) lse_merge(mx, sm, 0.f, (float)c);
+        const bool any = end > beg;
+        const float inv = any ? 1.f / sm : 0.f;
+        mout[(v0 + r) * H + k] = any ? mx : 0.f;
+        lout[(v0 + r) * H + k] = any ? sm : 1.f;
+        s_m[p] = mx;
+        s_inv[p] = inv;
+        for (int e = beg; e < end && e - E0 < ecap; ++e) s_alpha[(e - E0) * H + k] = __expf(s_alpha[(e - E0) * H + k] - mx) * inv;
+    }
+    __syncthreads();
+    f32x4_t acc[NQ];
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int c0 = E0; c0 < E1; c0 += ecap) {
+        const int c1 = min(E1, c0 + ecap);
+        if (c0 > E0) {                                   // later chunks: recompute alphas
+            __syncthreads();                             // the previous chunk is consumed
+            for (int p = t; p < rows * H; p += kRowsThreads) {
+                const int r = p / H, k = p - (p / H) * H;
+                const int beg = max(s_ptr[r], c0), end = min(s_ptr[r + 1], c1);
+                for (int e = beg; e < end; ++e) {
+                    const int u = R.src[e];
+                    const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                    s_alpha[(e - c0) * H + k] = __expf(s - s_m[p]) * s_inv[p];
+                    if (k == 0) s_src[e - c0] = u;
+                }
+            }
+            __syncthreads();
+        }
+        // edge jj of every slot's row in one step, so a thread's NQ gathers are in
+        // flight together; per slot the sum still runs in CSR edge order
+        int sb[NQ], sn[NQ], nmax = 0;
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            sb[i] = max(s_ptr[srow[i]], c0);
+            sn[i] = max(0, min(s_ptr[srow[i] + 1], c1) - sb[i]);
+            nmax = max(nmax, sn[i]);
+        }
+        for (int jj = 0; jj < nmax; ++jj) {
+            f32x4_t z[NQ];
+            int j[NQ];
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                j[i] = (jj < sn[i] ? sb[i] + jj : c0) - c0;      // clamped to a staged edge
+                z[i] = *reinterpret_cast<const f32x4_t *>(Z + (size_t)s_src[j[i]] * HD + scol[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                if (jj < sn[i]) {
+                    const int k0 = skh[i] >> 3, b = skh[i] & 7;
+                    const float w0 = s_alpha[j[i] * H + k0], w1 = s_alpha[j[i] * H + min(k0 + 1, H - 1)];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) acc[i][q] = fmaf(q < b ? w0 : w1, z[i][q], acc[i][q]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        const int q = t + kRowsThreads * i;
+        if (q < nslot) {
+            const size_t o = (size_t)(v0 + srow[i]) * HD + scol[i];
+            *reinterpret_cast<f32x4_t *>(hout + o) = acc[i];
+            if (origin) {
+                f32x4_t y;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) y[j] = (acc[i][j] > 0.f ? acc[i][j] : expm1f(acc[i][j])) + org[i][j];
+                *reinterpret_cast<f32x4_t *>(out + o) = y;
+            }
         }
     }
 }
@@ -801,6 +947,55 @@ int fwd_lanes_per_node(const hsg_rel *r, int H, int D) {
     return lpn;
 }
 
+// Row-tile forward plan: float4 slots per thread (NQ) and rows per block (RT) with
+// the least idle slots; 0 when the shape or alignment does not allow it.
+struct RowsPlan { int nq, rt; };
+RowsPlan rows_plan(int H, int D, bool aligned) {
+    RowsPlan best{0, 0};
+    // opt-in (HSG_GAT_ROWS = -1: auto NQ, n > 0: NQ = n).  On the cfg2 S2W pass it
+    // measured 25.3 us at NQ = 3 and 28.5 us at the auto NQ = 5 against 23.4 us for
+    // one destination per wave (tools/gat_fwd_lpn.py): the per-(row, head) index ->
+    // score chain of phase A costs more latency than the float4 band saves.
+    int force = 0;
+    if (const char *e = getenv("HSG_GAT_ROWS")) force = atoi(e);
+    if (force == 0) return best;
+    const int HD = H * D;
+    // a 4-column slot must not span more than two heads: D >= 2 (D = 2 slots are head-aligned)
+    if (HD % 4 || D < 2 || !aligned) return best;
+    const int hd4 = HD / 4;
+    static const int nqs[] = {1, 2, 3, 4, 5, 6, 8};
+    double best_u = 0.0;
+    for (int nq : nqs) {
+        if (force > 0 && nq != force) continue;
+        int rt = kRowsThreads * nq / hd4;
+        if (rt > kRowsMaxPairs / H) rt = kRowsMaxPairs / H;
+        if (rt < 1) continue;
+        const double u = (double)rt * hd4 / (kRowsThreads * nq);
+        if (u > best_u + 1e-9) { best_u = u; best = RowsPlan{nq, rt}; }
+    }
+    return best;
+}
+
+template <int TAU>
+int fwd_rows_dispatch(RowsPlan pl, hipStream_t st, RelPtrs R, int H, int D, float slope, const float *Z,
+                      const float *sg, const float *tau, const float *org, float *h, float *out, float *m,
+                      float *l) {
+    const dim3 grid((unsigned)((R.n_dst + pl.rt - 1) / pl.rt));
+#define HSG_FR(NQ_)                                                                                     \
+    case NQ_:                                                                                           \
+        hipLaunchKernelGGL((k_gat_fwd_rows<NQ_, TAU>), grid, dim3(kRowsThreads), 0, st, R, H, D, pl.rt, \
+                           slope, Z, sg, tau, org, h, out, m, l);                                        \
+        break;
+    switch (pl.nq) {
+        HSG_FR(1) HSG_FR(2) HSG_FR(3) HSG_FR(4) HSG_FR(5) HSG_FR(6) HSG_FR(8)
+        default: return HSG_EINVAL;
+    }
+#undef HSG_FR
+    return launch_status();
+}
+
+bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
 template <int TAU, int WPN>
 int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int lph, int om, float slope,
                         const float *Z, const float *sg, const float *tau, const float *h, const float *m,
@@ -888,6 +1083,15 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     }
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
+    if (wpn == 1) {                      // short segments: row-tile float4 kernel
+        const bool al = aligned16p(Z) && aligned16p(h) && (!origin || (aligned16p(origin) && aligned16p(out)));
+        const RowsPlan pl = rows_plan(H, D, al);
+        if (pl.nq > 0) {
+            if (tau_mode == HSG_TAU_TABLE)
+                return fwd_rows_dispatch<HSG_TAU_TABLE>(pl, st, R, H, D, slope, Z, sigma, tau, origin, h, out, m, l);
+            return fwd_rows_dispatch<HSG_TAU_PER_EDGE>(pl, st, R, H, D, slope, Z, sigma, tau, origin, h, out, m, l);
+        }
+    }
     const dim3 grid(grid_nodes(rel->n_dst, wpn, kFwdGridCap));
     const int lph = lanes_per_head(H);
 #define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)

@@ -512,6 +512,8 @@ int gemm_impl(bool bf16, int M, int N, int K, const float *A, int lda, int a_kco
     else if (best == 6) rc = launch_tiles<64, 64, 1, 64>(p, ak, bk, splits, st);
     else if (best == 7) rc = launch_tiles<128, 64, 1, 64>(p, ak, bk, splits, st);
     else if (best == 8) rc = launch_tiles<64, 64, 2, 64>(p, ak, bk, splits, st);
+    else if (best == 10) rc = launch_tiles<64, 128, 1>(p, ak, bk, splits, st);
+    else if (best == 11) rc = launch_tiles<64, 128, 2>(p, ak, bk, splits, st);
     else rc = launch_tiles<128, 128, 1, 64>(p, ak, bk, splits, st);
     if (rc || splits == 1) return rc;
     const size_t total = (size_t)M * N;

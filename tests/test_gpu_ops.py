@@ -157,3 +157,53 @@ def test_gat_heads_table_matches_restatement(H, D, F, max_deg, bias):
             continue
         scale = want.grad.abs().max().item() + 1e-6
         assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
+
+
+@pytest.mark.parametrize("nq", ["0", "-1", "1", "2", "3", "5", "8"])
+@pytest.mark.parametrize("H,D,dense_band,per_edge", [(6, 50, False, False), (6, 50, True, False), (4, 3, True, False),
+                                                     (1, 300, False, True), (16, 8, True, False), (2, 2, False, False)])
+def test_forward_row_tile_variants(monkeypatch, nq, H, D, dense_band, per_edge):
+    """The row-tile forward (k_gat_fwd_rows, float4 slots, HSG_GAT_ROWS = slots per
+    thread; 0 = one destination per wave) against the fp64 restatement.  dense_band
+    puts 24 consecutive destinations of 100 in-edges each among short segments, so a
+    block's edge range exceeds the 512-edge LDS chunk and later chunks recompute
+    their alphas; D = 3 and D = 2 put two heads into one float4 slot."""
+    from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
+    from hetersumgraph_amd.relation import Relation
+    from oracle.fused import gat_aggregate_ref
+    monkeypatch.setenv("HSG_GAT_ROWS", nq)
+    rng = np.random.default_rng(H * 17 + D + dense_band)
+    n_src, n_dst = 120, 700
+    deg = rng.integers(0, 4, size=n_dst)
+    if dense_band:
+        deg[300:324] = 100
+    e_dst = np.repeat(np.arange(n_dst), deg)
+    e_src = rng.integers(0, n_src, size=len(e_dst))
+    tf = rng.integers(0, 11, size=len(e_dst)).astype(np.uint8)
+    phantom = rng.integers(0, 3, size=n_dst)
+    indptr = np.concatenate([[0], np.cumsum(deg)])
+    corder = np.argsort(e_src, kind="stable")
+    cindptr = np.concatenate([[0], np.cumsum(np.bincount(e_src, minlength=n_src))])
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)
+    rel = Relation("S2W", n_src, n_dst, np.arange(n_src), np.arange(n_dst), i32(indptr), i32(e_src), tf,
+                   np.arange(len(e_src)), i32(phantom), i32(cindptr), i32(e_dst[corder]), i32(corder),
+                   len(e_src) + phantom.sum()).to("cuda")
+    f64 = dict(dtype=torch.float64)
+    Z = torch.randn(n_src, H * D, **f64)
+    a1 = torch.randn(H, D, **f64) * 0.3
+    tau = torch.randn(len(e_src) if per_edge else 11, H, **f64)
+    org = torch.randn(n_dst, H * D, **f64)
+    R = torch.randn(n_dst, H * D, **f64)
+    leaves = [t.clone().requires_grad_() for t in (Z, a1, tau, org)]
+    rows = np.arange(len(e_src)) if per_edge else tf
+    ref = gat_aggregate_ref(e_src, e_dst, rows, phantom, n_dst, *leaves)
+    (ref * R).sum().backward()
+    dl = [t.float().cuda().requires_grad_() for t in (Z, a1, tau, org)]
+    out = gat_aggregate(*dl[:3], dl[3], rel, H, D, tau_mode=HSG_TAU_PER_EDGE if per_edge else HSG_TAU_TABLE)
+    (out * R.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    err = lambda a, b: (a.detach().cpu().double() - b.detach()).abs().max().item()
+    assert err(out, ref) < 2e-5
+    for name, got, want in zip(("Z", "a1", "tau", "origin"), dl, leaves):
+        scale = want.grad.abs().max().item() + 1e-6
+        assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)

@@ -1,5 +1,7 @@
-"""Dev tool: S2W hsg_gat_fwd (the bench roofline kernel) per forward work split
-HSG_GAT_LPN (64 = one destination per wave, 32 / 16 = 2 / 4 per wave) on cfg2."""
+"""Dev tool: S2W hsg_gat_fwd (the bench roofline kernel) per forward variant on cfg2.
+Arguments are VAR=VALUE env settings, one variant each, e.g.
+  HSG_GAT_ROWS=0 (one destination per wave)  HSG_GAT_ROWS=0,HSG_GAT_LPN=32 (grouped)
+  HSG_GAT_ROWS=5 (row-tile kernel, 5 float4 slots per thread)"""
 import os
 import sys
 
@@ -20,8 +22,13 @@ gen = torch.Generator(device=dev).manual_seed(0)
 rel_s = G.relation("S2W")
 Xw = 0.4 * torch.randn(rel_s.n_dst, 300, device=dev, generator=gen)
 Xs = torch.randn(rel_s.n_src, 64, device=dev, generator=gen)
-for lpn in sys.argv[1:] or ["64", "32", "16"]:
-    os.environ["HSG_GAT_LPN"] = lpn
+for variant in sys.argv[1:] or ["HSG_GAT_ROWS=0", "HSG_GAT_ROWS=-1"]:
+    saved = dict(os.environ)
+    for kv in variant.split(","):
+        k, v = kv.split("=")
+        os.environ[k] = v
     ms, med, nbytes = bench.time_fwd_kernel(G, stack, Xw, Xs, 100)
-    print(f"LPN={lpn:3s} mean {ms * 1e3:6.1f} us  median {med * 1e3:6.1f} us  "
+    print(f"{variant:28s} mean {ms * 1e3:6.1f} us  median {med * 1e3:6.1f} us  "
           f"{nbytes / (ms * 1e-3) / 1e9:7.1f} GB/s", flush=True)
+    os.environ.clear()
+    os.environ.update(saved)
