@@ -51,8 +51,62 @@ def parse():
     ap.add_argument("--cpu-docs", type=int, default=4, help="docs in the bounded CPU-baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the secondary end-to-end train-step line")
+    ap.add_argument("--e2e-steps", type=int, default=10)
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
+
+
+class _HPS:
+    """train.py's argparse defaults (train.py:279-309), n_iter from the bench."""
+
+    def __init__(self, n_iter):
+        self.__dict__.update(dict(
+            vocab_size=50000, n_iter=n_iter, word_emb_dim=300, embed_train=False, feat_embed_size=50,
+            lstm_hidden_state=128, lstm_layers=2, bidirectional=True, n_feature_size=128, hidden_size=64,
+            ffn_inner_hidden_size=512, n_head=8, recurrent_dropout_prob=0.1, atten_dropout_prob=0.1,
+            ffn_dropout_prob=0.1, sent_max_len=100, doc_max_timesteps=50, lr=0.0005, cuda=True))
+
+
+def time_train_step(G, config, n_iter, steps, warmup, dev):
+    """Secondary figure: one whole training iteration of train.py:104-133
+    on this rank's batch -- HSumGraph (HSumDocGraph for cfg4) forward with the CNN +
+    LSTM sentence encoder, per-sentence cross entropy summed per graph and averaged,
+    the finiteness check (a host sync, as the reference does), zero_grad, backward,
+    Adam.  Eager launches, random-init weights, frozen embedding (embed_train=False)."""
+    from hetersumgraph_amd import HiGraph
+    from hetersumgraph_amd import graph as hg
+    hps = _HPS(n_iter)
+    torch.manual_seed(1)
+    embed = torch.nn.Embedding(hps.vocab_size, hps.word_emb_dim, padding_idx=0)
+    embed.weight.requires_grad = hps.embed_train
+    cls = HiGraph.HSumDocGraph if config == "cfg4" else HiGraph.HSumGraph
+    model = cls(hps, embed).to(dev).train()
+    opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=hps.lr)
+    criterion = torch.nn.CrossEntropyLoss(reduction="none")
+
+    def step():
+        outputs = model.forward(G)                                          # [n_snodes, 2]
+        snode_id = G.filter_nodes(lambda nodes: nodes.data["dtype"] == 1)
+        label = G.ndata["label"][snode_id].sum(-1)
+        G.nodes[snode_id].data["loss"] = criterion(outputs, label).unsqueeze(-1)
+        loss = hg.sum_nodes(G, "loss").mean()
+        if not bool(torch.isfinite(loss).item()):          # host sync, as train.py:120
+            raise RuntimeError("train loss is not finite")
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        G.ndata.pop("loss")          # train.py sees a fresh graph per batch; this one is reused
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return dt
 
 
 def cpu_model():
@@ -378,6 +432,15 @@ def main():
                            "frac": d_tf / FP32_MFMA_PEAK_TFLOPS, "flops_per_launch": d_flops,
                            "avg_launch_us": d_ms * 1e3},
     }
+    if world == 1 and not args.no_e2e:
+        try:
+            dt = time_train_step(G, args.config, args.n_iter, args.e2e_steps, 3, dev)
+            out["e2e_train_step"] = {
+                "value": E_total / dt, "unit": "graph-edges/s", "ms_per_step": dt * 1e3, "steps": args.e2e_steps,
+                "what": "whole train.py iteration (HiGraph forward incl. CNN+LSTM sentence encoder, "
+                        "cross-entropy, backward, Adam; eager, 1 GPU)"}
+        except Exception as exc:  # pragma: no cover - reported in the JSON
+            out["e2e_train_step"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(docs, args, stack)

@@ -135,9 +135,11 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
     const int tid = threadIdx.x, nt = blockDim.x;
     const int NTH = kNT * H;
     // d tau [11][H], summed over the stage rows in order
+    // (full unrolls here and below: all kStage slab loads of a thread are in flight
+    // before the in-order adds -- this kernel is one latency chain per block)
     for (int i = tid; i < NTH; i += nt) {
         float s = 0.f;
-#pragma unroll 16
+#pragma unroll
         for (int r = 0; r < kStage; ++r) s += dtau_st[r * NTH + i];
         dtau[i] = s;
     }
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
             const int kk = i / F, f = i - (i / F) * F;
             const float *wk = wf + (size_t)kk * D * F;
             float s = 0.f;
-#pragma unroll 8
+#pragma unroll 32
             for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
             vall[i] = s;
         }
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
             if (dbf) dbf[k * D + d] = (accumulate & 1) ? dbf[k * D + d] + a3s[d] * dc : a3s[d] * dc;
         }
         float g = 0.f;                             // d a1: stage rows in order
-#pragma unroll 16
+#pragma unroll
         for (int r = 0; r < kStage; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
         if (accumulate & 1) {
             dattn[k * D3 + d] += g;
