@@ -12,7 +12,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip", "hsg_cnn.hip")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip", "hsg_cnn.hip", "hsg_ffn.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")

@@ -1,0 +1,200 @@
+// hsg_ffn.hip -- the whole PositionwiseFeedForward forward in one launch, for the
+// narrow FFN of the word->sentence layer (d = 64, d_hid = 512 at every config).
+//
+// Reference (module/GATLayer.py:35-44):
+//     out = LayerNorm(Dropout(W2 relu(W1 x + b1) + b2) + x),  eps 1e-5
+// On the W2S side the FFN runs over the sentence (and doc) nodes only -- 1,120 rows
+// at config 2 -- so the split path (two hsg_gemm_f32 launches + hsg_ln_fwd) is
+// three latency-bound launches with ~0.15 GFLOP between them.  Here one block of
+// 8 waves owns 16 rows end to end, and every global operand of both GEMMs (the
+// wave's W1 columns, its W2 K slice, the x tile) is requested at kernel start, so
+// the block pays one memory latency rather than one per K chunk:
+//   phase 1  H[16][d_hid] = relu(x W1^T + b1)    wave w: columns [w*d_hid/8, ...)
+//            v_mfma_f32_16x16x4_f32, x from LDS; H is written to global (the
+//            backward needs it) and kept in LDS
+//   phase 2  y[16][d] = H W2^T + b2              wave w: K slice [w*d_hid/8, ...)
+//            for all d/16 column tiles; the eight K-slice partials are added in
+//            wave order through LDS (deterministic)
+//   phase 3  out = LN(dropout(y) + x) per row    one wave per row, the same hash
+//            dropout (hsg_rng.h, index r*d + c) and the same reductions as
+//            hsg_ln_fwd, so hsg_ln_bwd consumes (y, mean, rstd) unchanged
+// MFMA operand layout (16x16x4): lane (li = l&15, lk = l>>4) feeds k = k0 + 4lk + e
+// to the e-th of 4 consecutive MFMAs, so every operand read is one 16-byte quad.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hsg.h"
+#include "hsg_rng.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kRB = 16;          // rows per block
+
+__device__ __forceinline__ float wsum(float v) {
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+template <int D, int HID>
+__global__ __launch_bounds__(512) void k_ffn_small_fwd(int n, const float *__restrict__ x,
+                                                       const float *__restrict__ w1, const float *__restrict__ b1,
+                                                       const float *__restrict__ w2, const float *__restrict__ b2,
+                                                       const float *__restrict__ gamma,
+                                                       const float *__restrict__ beta, float eps, float p_drop,
+                                                       const int64_t *__restrict__ seedp, uint32_t offset,
+                                                       float *__restrict__ Hout, float *__restrict__ yout,
+                                                       float *__restrict__ out, float *__restrict__ mean,
+                                                       float *__restrict__ rstd) {
+    constexpr int NW = 8;                    // waves per block
+    constexpr int LX = D + 4, LH = HID + 4;
+    constexpr int C1 = HID / NW;             // phase-1 columns per wave
+    constexpr int CT1 = C1 / 16;             // ... as 16-wide MFMA tiles
+    constexpr int KC1 = D / 16;              // phase-1 16-deep K chunks
+    constexpr int KS2 = HID / NW;            // phase-2 K slice per wave
+    constexpr int KC2 = KS2 / 16;
+    constexpr int CT2 = D / 16;              // phase-2 column tiles
+    __shared__ __attribute__((aligned(16))) float xs[kRB * LX];
+    __shared__ __attribute__((aligned(16))) float hs[kRB * LH];
+    __shared__ __attribute__((aligned(16))) float ps[NW][kRB * D];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int r0 = blockIdx.x * kRB;
+    // every global operand of both GEMMs is requested up front (one memory latency
+    // for the whole block instead of one per K chunk): this wave's W1 columns and
+    // W2 K slice as MFMA operand quads, and the x tile
+    const int cbase = w * C1, kb = w * KS2;
+    f32x4 bw1[KC1][CT1], bw2[KC2][CT2];
+#pragma unroll
+    for (int kc = 0; kc < KC1; ++kc)
+#pragma unroll
+        for (int t = 0; t < CT1; ++t)
+            bw1[kc][t] = *reinterpret_cast<const f32x4 *>(w1 + (size_t)(cbase + 16 * t + li) * D + 16 * kc + 4 * lk);
+#pragma unroll
+    for (int kc = 0; kc < KC2; ++kc)
+#pragma unroll
+        for (int t = 0; t < CT2; ++t)
+            bw2[kc][t] = *reinterpret_cast<const f32x4 *>(w2 + (size_t)(16 * t + li) * HID + kb + 16 * kc + 4 * lk);
+    for (int q = tid; q < kRB * D / 4; q += NW * 64) {
+        const int r = q / (D / 4), c = (q % (D / 4)) * 4;
+        const f32x4 v = r0 + r < n ? *reinterpret_cast<const f32x4 *>(x + (size_t)(r0 + r) * D + c)
+                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+        *reinterpret_cast<f32x4 *>(xs + r * LX + c) = v;
+    }
+    __syncthreads();
+    // ---- phase 1: H = relu(x W1^T + b1), columns [cbase, cbase + C1)
+    {
+        f32x4 acc[CT1];
+#pragma unroll
+        for (int t = 0; t < CT1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC1; ++kc) {
+            const f32x4 a = *reinterpret_cast<const f32x4 *>(xs + li * LX + 16 * kc + 4 * lk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int t = 0; t < CT1; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bw1[kc][t][e], acc[t], 0, 0, 0);
+        }
+        // D layout: column li of the tile, rows 4lk .. 4lk+3
+#pragma unroll
+        for (int t = 0; t < CT1; ++t) {
+            const int c = cbase + 16 * t + li;
+            const float bb = b1[c];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * lk + e;
+                const float v = fmaxf(acc[t][e] + bb, 0.f);
+                hs[r * LH + c] = v;
+                if (r0 + r < n) Hout[(size_t)(r0 + r) * HID + c] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- phase 2: partial y over this wave's K slice, all column tiles
+    {
+        f32x4 acc[CT2];
+#pragma unroll
+        for (int t = 0; t < CT2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC2; ++kc) {
+            const f32x4 a = *reinterpret_cast<const f32x4 *>(hs + li * LH + kb + 16 * kc + 4 * lk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int t = 0; t < CT2; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bw2[kc][t][e], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < CT2; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ps[w][(4 * lk + e) * D + 16 * t + li] = acc[t][e];
+    }
+    __syncthreads();
+    // ---- phase 3: y = sum of the K slices (wave order) + b2; out = LN(dropout(y) + x)
+    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    constexpr int NPL = (D + 63) / 64;
+    for (int r = w; r < kRB; r += NW) {
+        const int gr = r0 + r;
+        if (gr >= n) break;
+        float s[NPL];
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            s[i] = 0.f;
+            if (c < D) {
+                const size_t o = (size_t)gr * D + c;
+                float v = ps[0][r * D + c];
+#pragma unroll
+                for (int q = 1; q < NW; ++q) v += ps[q][r * D + c];
+                v += b2[c];
+                yout[o] = v;
+                if (p_drop > 0.f) v = hsg_keep(seed, offset, o, thr) ? v * scale : 0.f;
+                s[i] = v + xs[r * LX + c];
+                acc += s[i];
+            }
+        }
+        const float mu = wsum(acc) / D;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NPL; ++i)
+            if (lane + 64 * i < D) { const float t = s[i] - mu; var = fmaf(t, t, var); }
+        const float rs = rsqrtf(wsum(var) / D + eps);
+#pragma unroll
+        for (int i = 0; i < NPL; ++i) {
+            const int c = lane + 64 * i;
+            if (c < D) out[(size_t)gr * D + c] = (s[i] - mu) * rs * gamma[c] + beta[c];
+        }
+        if (lane == 0) { mean[gr] = mu; rstd[gr] = rs; }
+    }
+}
+
+bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int hsg_ffn_small_supported(int d, int d_hid) { return (d == 64 && d_hid == 512) ? 1 : 0; }
+
+int hsg_ffn_small_fwd(int n, int d, int d_hid, const float *x, const float *w1, const float *b1, const float *w2,
+                      const float *b2, const float *gamma, const float *beta, float eps, float p_drop,
+                      const int64_t *seed, uint32_t offset, float *H, float *y, float *out, float *mean, float *rstd,
+                      void *stream) {
+    if (n < 0 || !hsg_ffn_small_supported(d, d_hid) || p_drop < 0.f || p_drop >= 1.f) return HSG_EINVAL;
+    if (!x || !w1 || !b1 || !w2 || !b2 || !gamma || !beta || !H || !y || !out || !mean || !rstd) return HSG_EINVAL;
+    if (p_drop > 0.f && !seed) return HSG_EINVAL;
+    if (!aligned16(x) || !aligned16(w1) || !aligned16(w2)) return HSG_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL((k_ffn_small_fwd<64, 512>), dim3((unsigned)((n + kRB - 1) / kRB)), dim3(512), 0,
+                       (hipStream_t)stream, n, x, w1, b1, w2, b2, gamma, beta, eps, p_drop, seed, offset, H, y, out,
+                       mean, rstd);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

@@ -20,24 +20,44 @@ whose backward writes the parameter gradients straight into their destination
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, row_tiles
+from .dense import gemm, get_gemm_dtype, row_tiles
 
 LN_EPS = 1e-5
+
+
+def _fused_ok(lib, x, w1, w2, b1, b2):
+    """The one-launch narrow FFN (hsg_ffn_small_fwd: the W2S FFN, d=64, d_hid=512)
+    covers this call: fp32 GEMM mode, contiguous operands, biases present."""
+    if os.environ.get("HSG_FFN_FUSED", "1") == "0" or get_gemm_dtype() != "f32":
+        return False
+    d_hid, d = w1.shape
+    return (b1 is not None and b2 is not None and bool(lib.hsg_ffn_small_supported(d, d_hid))
+            and x.is_contiguous() and w1.is_contiguous() and w2.is_contiguous())
 
 
 def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
     """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  Returns (out, saved)."""
     lib = load()
     n, d = x.shape
-    H = gemm(x, w1, b_t=True, bias=b1, relu=True)          # [n, d_hid]
-    y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
     out = torch.empty_like(x)
     mean = x.new_empty(n)
     rstd = x.new_empty(n)
+    if _fused_ok(lib, x, w1, w2, b1, b2):
+        H = x.new_empty(n, w1.shape[0])
+        y = torch.empty_like(x)
+        seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
+        check(lib.hsg_ffn_small_fwd(n, d, w1.shape[0], ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(gamma),
+                                    ptr(beta), float(eps), float(p_drop), ptr(seed_t), off, ptr(H), ptr(y),
+                                    ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ffn_small_fwd")
+        return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
+    H = gemm(x, w1, b_t=True, bias=b1, relu=True)          # [n, d_hid]
+    y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
     seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
     check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
                          ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")

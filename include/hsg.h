@@ -173,6 +173,17 @@ int hsg_ln_bwd_blocks(int n);
 int hsg_ffn_colsums(int rows_h, int d_hid, const float *hpart, float *db1, int rows_ln, int d,
                     const float *lnpart, float *dgamma, float *dbeta, float *db2, int accumulate,
                     void *stream);
+/* The whole FFN forward in one launch for the narrow W2S FFN (d = 64, d_hid = 512;
+ * hsg_ffn_small_supported(d, d_hid) says whether a shape is covered):
+ *   H = relu(x W1^T + b1) [n][d_hid],  y = H W2^T + b2 [n][d],
+ *   out = LN(dropout(y) + x) with mean / rstd -- the outputs of hsg_gemm_f32 x 2 +
+ *   hsg_ln_fwd (same dropout hash and index, so hsg_ln_bwd takes y, mean, rstd).
+ * w1 [d_hid][d], w2 [d][d_hid] row-major; x, w1, w2 16-byte aligned. */
+int hsg_ffn_small_supported(int d, int d_hid);
+int hsg_ffn_small_fwd(int n, int d, int d_hid, const float *x, const float *w1, const float *b1,
+                      const float *w2, const float *b2, const float *gamma, const float *beta, float eps,
+                      float p_drop, const int64_t *seed, uint32_t offset, float *H, float *y, float *out,
+                      float *mean, float *rstd, void *stream);
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
                float eps, float p_drop, const int64_t *seed, uint32_t offset,
                float *out, float *mean, float *rstd, void *stream);
