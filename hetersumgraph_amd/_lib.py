@@ -26,7 +26,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
            "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
-           "hsg_ffn_small_supported", "hsg_ffn_small_fwd")
+           "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -82,6 +82,8 @@ _SIGS = {
     "hsg_cnn_pool_bwd": [_I, _P, _P, _P, _P, _P, _I, _P],
     "hsg_ln_fwd": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_ffn_small_supported": [_I, _I],
+    "hsg_ffn_small_bwd_blocks": [_I],
+    "hsg_ffn_small_bwd": [_I, _I, _I] + [_P] * 9 + [_F, _P, ctypes.c_uint32] + [_P] * 6,
     "hsg_ffn_small_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P, _P,
                           _P],
     "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],

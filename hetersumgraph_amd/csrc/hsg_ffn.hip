@@ -173,6 +173,173 @@ __global__ __launch_bounds__(512) void k_ffn_small_fwd(int n, const float *__res
     }
 }
 
+// Backward of the same FFN up to the weight gradients, one block of 8 waves per 16
+// rows (the counterpart of hsg_ln_bwd + the dH and dx GEMMs of the split path):
+//   phase A  LN + dropout backward per row (2 rows per wave, lane = column):
+//            ds = dLN/ds (residual branch), dy = ds * mask / (1-p); block column
+//            partials of dgamma, dbeta and dy (= db2) -> lnpart[block][3][d]
+//   phase B  dH = (dy W2) * (H > 0)             wave w: columns [w*d_hid/8, ...)
+//            written to global (for dW1 = dH^T x) and kept in LDS; its block
+//            column sums -> hpart[block][d_hid] (db1)
+//   phase C  dx = ds + dH W1                    wave w: K slice [w*d_hid/8, ...),
+//            the eight partials added in wave order
+// W2 / W1 / H operands are requested at kernel start (scalar MFMA operands: the
+// reduction runs along the rows of W2 and W1).  dW1, dW2 stay hsg_gemm_f32 split-K
+// GEMMs and the partials go through hsg_ffn_colsums, as in the split path.
+template <int D, int HID>
+__global__ __launch_bounds__(512) void k_ffn_small_bwd(int n, const float *__restrict__ dout,
+                                                       const float *__restrict__ x, const float *__restrict__ H,
+                                                       const float *__restrict__ y, const float *__restrict__ w1,
+                                                       const float *__restrict__ w2,
+                                                       const float *__restrict__ gamma,
+                                                       const float *__restrict__ mean,
+                                                       const float *__restrict__ rstd, float p_drop,
+                                                       const int64_t *__restrict__ seedp, uint32_t offset,
+                                                       float *__restrict__ dy, float *__restrict__ dH,
+                                                       float *__restrict__ dx, float *__restrict__ lnpart,
+                                                       float *__restrict__ hpart) {
+    constexpr int NW = 8;
+    constexpr int LY = D + 4, LH = HID + 4;
+    constexpr int C1 = HID / NW, CT1 = C1 / 16, KC1 = D / 16;      // phase B
+    constexpr int KS2 = HID / NW, KC2 = KS2 / 16, CT2 = D / 16;   // phase C
+    static_assert(D == 64, "phase A maps one lane per column");
+    __shared__ __attribute__((aligned(16))) float dys[kRB * LY];
+    __shared__ __attribute__((aligned(16))) float dss[kRB * D];
+    __shared__ __attribute__((aligned(16))) float dhs[kRB * LH];
+    __shared__ __attribute__((aligned(16))) float ps[NW][kRB * D];
+    __shared__ float red[NW][3][D];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int r0 = blockIdx.x * kRB;
+    const int cb = w * C1, kb = w * KS2;
+    // operands of phases B and C, requested first
+    float bw2[KC1][CT1][4], bw1[KC2][CT2][4], hv[CT1][4];
+#pragma unroll
+    for (int kc = 0; kc < KC1; ++kc)
+#pragma unroll
+        for (int t = 0; t < CT1; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bw2[kc][t][e] = w2[(size_t)(16 * kc + 4 * lk + e) * HID + cb + 16 * t + li];
+#pragma unroll
+    for (int kc = 0; kc < KC2; ++kc)
+#pragma unroll
+        for (int t = 0; t < CT2; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bw1[kc][t][e] = w1[(size_t)(kb + 16 * kc + 4 * lk + e) * D + 16 * t + li];
+#pragma unroll
+    for (int t = 0; t < CT1; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int r = min(r0 + 4 * lk + e, n - 1);
+            hv[t][e] = H[(size_t)r * HID + cb + 16 * t + li];
+        }
+    // ---- phase A: LayerNorm + dropout backward, rows w and w + 8
+    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    const float gam = gamma[lane];
+    float dg = 0.f, db = 0.f, dyb = 0.f;
+#pragma unroll
+    for (int q = 0; q < kRB / NW; ++q) {
+        const int r = w + NW * q, gr = r0 + r;
+        const bool ok = gr < n;
+        const size_t o = (size_t)(ok ? gr : 0) * D + lane;
+        const float yv = y[o], xv = x[o], go = ok ? dout[o] : 0.f;
+        const float mu = mean[ok ? gr : 0], rs = rstd[ok ? gr : 0];
+        bool keep = true;
+        float v = yv;
+        if (p_drop > 0.f) {
+            keep = hsg_keep(seed, offset, o, thr);
+            v = keep ? v * scale : 0.f;
+        }
+        const float xh = (v + xv - mu) * rs;
+        const float g = go * gam;
+        const float mg = wsum(g) / D, mgx = wsum(g * xh) / D;
+        const float ds = ok ? rs * (g - mg - xh * mgx) : 0.f;
+        const float dyv = keep ? ds * scale : 0.f;
+        if (ok) {
+            dg = fmaf(go, xh, dg);
+            db += go;
+            dyb += dyv;
+            dy[o] = dyv;
+        }
+        dys[r * LY + lane] = dyv;
+        dss[r * D + lane] = ds;
+    }
+    red[w][0][lane] = dg;
+    red[w][1][lane] = db;
+    red[w][2][lane] = dyb;
+    __syncthreads();
+    if (tid < 3 * D) {
+        const int which = tid / D, c = tid - which * D;
+        float a = 0.f;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) a += red[q][which][c];
+        lnpart[(size_t)blockIdx.x * 3 * D + which * D + c] = a;
+    }
+    // ---- phase B: dH = (dy W2) * (H > 0), columns [cb, cb + C1)
+    {
+        f32x4 acc[CT1];
+#pragma unroll
+        for (int t = 0; t < CT1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC1; ++kc) {
+            const f32x4 a = *reinterpret_cast<const f32x4 *>(dys + li * LY + 16 * kc + 4 * lk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int t = 0; t < CT1; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bw2[kc][t][e], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < CT1; ++t) {
+            const int c = cb + 16 * t + li;
+            float cs = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int r = 4 * lk + e;
+                const float v = (r0 + r < n && hv[t][e] > 0.f) ? acc[t][e] : 0.f;
+                dhs[r * LH + c] = v;
+                if (r0 + r < n) dH[(size_t)(r0 + r) * HID + c] = v;
+                cs += v;
+            }
+            // rows 4lk..4lk+3 here; the four lk groups of a column are lanes li + 16 lk
+            cs += __shfl_xor(cs, 16);
+            cs += __shfl_xor(cs, 32);
+            if (lk == 0) hpart[(size_t)blockIdx.x * HID + c] = cs;
+        }
+    }
+    __syncthreads();
+    // ---- phase C: dx = ds + dH W1 (this wave's K slice, all column tiles)
+    {
+        f32x4 acc[CT2];
+#pragma unroll
+        for (int t = 0; t < CT2; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kc = 0; kc < KC2; ++kc) {
+            const f32x4 a = *reinterpret_cast<const f32x4 *>(dhs + li * LH + kb + 16 * kc + 4 * lk);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int t = 0; t < CT2; ++t)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bw1[kc][t][e], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < CT2; ++t)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) ps[w][(4 * lk + e) * D + 16 * t + li] = acc[t][e];
+    }
+    __syncthreads();
+    for (int q = tid; q < kRB * D; q += NW * 64) {
+        const int r = q / D, c = q - (q / D) * D;
+        if (r0 + r >= n) continue;
+        float v = ps[0][q];
+#pragma unroll
+        for (int k = 1; k < NW; ++k) v += ps[k][q];
+        dx[(size_t)(r0 + r) * D + c] = dss[q] + v;
+    }
+}
+
 bool aligned16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -193,6 +360,24 @@ int hsg_ffn_small_fwd(int n, int d, int d_hid, const float *x, const float *w1, 
     hipLaunchKernelGGL((k_ffn_small_fwd<64, 512>), dim3((unsigned)((n + kRB - 1) / kRB)), dim3(512), 0,
                        (hipStream_t)stream, n, x, w1, b1, w2, b2, gamma, beta, eps, p_drop, seed, offset, H, y, out,
                        mean, rstd);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int hsg_ffn_small_bwd_blocks(int n) { return n > 0 ? (n + kRB - 1) / kRB : 0; }
+
+int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x, const float *H, const float *y,
+                      const float *w1, const float *w2, const float *gamma, const float *mean, const float *rstd,
+                      float p_drop, const int64_t *seed, uint32_t offset, float *dy, float *dH, float *dx,
+                      float *lnpart, float *hpart, void *stream) {
+    if (n < 0 || !hsg_ffn_small_supported(d, d_hid) || p_drop < 0.f || p_drop >= 1.f) return HSG_EINVAL;
+    if (!dout || !x || !H || !y || !w1 || !w2 || !gamma || !mean || !rstd || !dy || !dH || !dx || !lnpart || !hpart)
+        return HSG_EINVAL;
+    if (p_drop > 0.f && !seed) return HSG_EINVAL;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL((k_ffn_small_bwd<64, 512>), dim3((unsigned)hsg_ffn_small_bwd_blocks(n)), dim3(512), 0,
+                       (hipStream_t)stream, n, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy, dH,
+                       dx, lnpart, hpart);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

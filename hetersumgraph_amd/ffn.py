@@ -31,14 +31,15 @@ from .dense import gemm, get_gemm_dtype, row_tiles
 LN_EPS = 1e-5
 
 
-def _fused_ok(lib, x, w1, w2, b1, b2):
-    """The one-launch narrow FFN (hsg_ffn_small_fwd: the W2S FFN, d=64, d_hid=512)
-    covers this call: fp32 GEMM mode, contiguous operands, biases present."""
+def _fused_ok(lib, x, w1, w2):
+    """The one-launch narrow FFN kernels (hsg_ffn_small_fwd / _bwd: the W2S FFN,
+    d=64, d_hid=512) cover this call: fp32 GEMM mode, contiguous operands.
+    HSG_FFN_FUSED=0 selects the split path (A/B tests)."""
     if os.environ.get("HSG_FFN_FUSED", "1") == "0" or get_gemm_dtype() != "f32":
         return False
     d_hid, d = w1.shape
-    return (b1 is not None and b2 is not None and bool(lib.hsg_ffn_small_supported(d, d_hid))
-            and x.is_contiguous() and w1.is_contiguous() and w2.is_contiguous())
+    return (bool(lib.hsg_ffn_small_supported(d, d_hid)) and x.is_contiguous() and w1.is_contiguous()
+            and w2.is_contiguous())
 
 
 def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
@@ -48,7 +49,7 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
     out = torch.empty_like(x)
     mean = x.new_empty(n)
     rstd = x.new_empty(n)
-    if _fused_ok(lib, x, w1, w2, b1, b2):
+    if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
         H = x.new_empty(n, w1.shape[0])
         y = torch.empty_like(x)
         seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
@@ -75,17 +76,27 @@ def ffn_bwd(saved, dout, dst):
     dout = dout.contiguous()
     n, d = x.shape
     st = stream_of(x)
-    nb = lib.hsg_ln_bwd_blocks(n)
     d_hid = H.shape[1]
     dy = torch.empty_like(x)
     dx = torch.empty_like(x)
-    part = x.new_empty(nb, 3, d)
-    check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
-                         ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
-    rt = row_tiles(n, d_hid, d)
-    hpart = x.new_empty(rt, d_hid)
-    dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
-    gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
+    if _fused_ok(lib, x, w1, w2) and H.is_contiguous() and y.is_contiguous():
+        # one launch: LN/dropout backward, dH = (dy W2) * relu'(H), dx = ds + dH W1
+        nb = rt = lib.hsg_ffn_small_bwd_blocks(n)
+        part = x.new_empty(nb, 3, d)
+        hpart = x.new_empty(rt, d_hid)
+        dH = x.new_empty(n, d_hid)
+        check(lib.hsg_ffn_small_bwd(n, d, d_hid, ptr(dout), ptr(x), ptr(H), ptr(y), ptr(w1), ptr(w2), ptr(gamma),
+                                    ptr(mean), ptr(rstd), p_drop, ptr(seed_t), off, ptr(dy), ptr(dH), ptr(dx),
+                                    ptr(part), ptr(hpart), st), "hsg_ffn_small_bwd")
+    else:
+        nb = lib.hsg_ln_bwd_blocks(n)
+        part = x.new_empty(nb, 3, d)
+        check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                             ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
+        rt = row_tiles(n, d_hid, d)
+        hpart = x.new_empty(rt, d_hid)
+        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
+        gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
     if dw2 is not None:
         gemm(dy, H, a_t=True, out=dw2, add=dw2 if acc_w2 else None)  # [d, d_hid]
     if dw1 is not None:

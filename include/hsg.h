@@ -184,6 +184,17 @@ int hsg_ffn_small_fwd(int n, int d, int d_hid, const float *x, const float *w1, 
                       const float *w2, const float *b2, const float *gamma, const float *beta, float eps,
                       float p_drop, const int64_t *seed, uint32_t offset, float *H, float *y, float *out,
                       float *mean, float *rstd, void *stream);
+/* Its backward up to the weight gradients, one launch (hsg_ln_bwd + the dH and dx
+ * GEMMs of the split path):  dy = LN/dropout backward of dout, dH = (dy W2) * (H > 0),
+ * dx = dLN/ds + dH W1;  lnpart [blocks][3][d] (dgamma, dbeta, db2 partials) and
+ * hpart [blocks][d_hid] (db1 partials) for hsg_ffn_colsums, blocks =
+ * hsg_ffn_small_bwd_blocks(n).  dW1 = dH^T x and dW2 = dy^T H stay hsg_gemm_f32. */
+int hsg_ffn_small_bwd_blocks(int n);
+int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x, const float *H,
+                      const float *y, const float *w1, const float *w2, const float *gamma,
+                      const float *mean, const float *rstd, float p_drop, const int64_t *seed,
+                      uint32_t offset, float *dy, float *dH, float *dx, float *lnpart, float *hpart,
+                      void *stream);
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
                float eps, float p_drop, const int64_t *seed, uint32_t offset,
                float *out, float *mean, float *rstd, void *stream);
