@@ -26,7 +26,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
            "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
-           "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd")
+           "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
+           "hsg_attn_params_stage", "hsg_attn_params_finish")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -58,6 +59,8 @@ _SIGS = {
     "hsg_attn_params_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_attn_params_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
     "hsg_attn_params_bwd_workspace_floats": [_I, _I],
+    "hsg_attn_params_stage": [_I, _I, _I, _P, _I, _P, _P, _I, _P],
+    "hsg_attn_params_finish": [_I, _I, _I] + [_P] * 9 + [_I, _P],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],

@@ -99,7 +99,8 @@ constexpr int kStage = 64;     // row ranges per slab
 
 __global__ __launch_bounds__(256) void k_colsum_stage(int rows0, int cols0, const float *__restrict__ p0, int rows1,
                                                       int cols1, const float *__restrict__ p1,
-                                                      float *__restrict__ out0, float *__restrict__ out1) {
+                                                      float *__restrict__ out0, float *__restrict__ out1,
+                                                      int accumulate) {
     const int y = blockIdx.y;
     const int rows = y ? rows1 : rows0, cols = y ? cols1 : cols0;
     const float *p = y ? p1 : p0;
@@ -114,7 +115,8 @@ __global__ __launch_bounds__(256) void k_colsum_stage(int rows0, int cols0, cons
             for (int q = 0; q < 4; ++q) s[q] += p[(size_t)(r + q) * cols + c];
         }
         for (; r < r1; ++r) s[0] += p[(size_t)r * cols + c];
-        out[(size_t)blockIdx.x * cols + c] = (s[0] + s[1]) + (s[2] + s[3]);
+        const float v = (s[0] + s[1]) + (s[2] + s[3]);
+        out[(size_t)blockIdx.x * cols + c] = accumulate ? out[(size_t)blockIdx.x * cols + c] + v : v;
     }
 }
 
@@ -135,11 +137,9 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
     const int tid = threadIdx.x, nt = blockDim.x;
     const int NTH = kNT * H;
     // d tau [11][H], summed over the stage rows in order
-    // (full unrolls here and below: all kStage slab loads of a thread are in flight
-    // before the in-order adds -- this kernel is one latency chain per block)
     for (int i = tid; i < NTH; i += nt) {
         float s = 0.f;
-#pragma unroll
+#pragma unroll 16
         for (int r = 0; r < kStage; ++r) s += dtau_st[r * NTH + i];
         dtau[i] = s;
     }
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
             const int kk = i / F, f = i - (i / F) * F;
             const float *wk = wf + (size_t)kk * D * F;
             float s = 0.f;
-#pragma unroll 32
+#pragma unroll 8
             for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
             vall[i] = s;
         }
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
             if (dbf) dbf[k * D + d] = (accumulate & 1) ? dbf[k * D + d] + a3s[d] * dc : a3s[d] * dc;
         }
         float g = 0.f;                             // d a1: stage rows in order
-#pragma unroll
+#pragma unroll 16
         for (int r = 0; r < kStage; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
         if (accumulate & 1) {
             dattn[k * D3 + d] += g;
@@ -234,14 +234,29 @@ int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_
     if (!dims_ok(H, D, F) || n_dtau_part < 0 || n_da1_part < 0 || !dtau_part || !da1_part || !attn || !wf ||
         !T || !dattn || !dwf || !dT || !workspace)
         return HSG_EINVAL;
-    hipStream_t st = (hipStream_t)stream;
-    float *s0 = workspace, *s1 = workspace + (size_t)kStage * kNT * H;
-    hipLaunchKernelGGL(k_colsum_stage, dim3(kStage, 2), dim3(256), 0, st, n_dtau_part, kNT * H, dtau_part,
-                       n_da1_part, H * D, da1_part, s0, s1);
-    int rc = status();
+    int rc = hsg_attn_params_stage(H, D, n_dtau_part, dtau_part, n_da1_part, da1_part, workspace, 0, stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_attn_params_bwd, dim3(H + 1), dim3(256), 0, st, H, D, F, s0, s1, attn, wf, bf, T, dattn,
-                       dwf, dbf, dT, accumulate);
+    return hsg_attn_params_finish(H, D, F, workspace, attn, wf, bf, T, dattn, dwf, dbf, dT, accumulate, stream);
+}
+
+int hsg_attn_params_stage(int H, int D, int n_dtau_part, const float *dtau_part, int n_da1_part,
+                          const float *da1_part, float *workspace, int accumulate, void *stream) {
+    if (H < 1 || H > kHMax || D < 1 || H * D > kDMax || n_dtau_part < 0 || n_da1_part < 0 || !dtau_part ||
+        !da1_part || !workspace)
+        return HSG_EINVAL;
+    float *s0 = workspace, *s1 = workspace + (size_t)kStage * kNT * H;
+    hipLaunchKernelGGL(k_colsum_stage, dim3(kStage, 2), dim3(256), 0, (hipStream_t)stream, n_dtau_part, kNT * H,
+                       dtau_part, n_da1_part, H * D, da1_part, s0, s1, accumulate);
+    return status();
+}
+
+int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const float *attn, const float *wf,
+                           const float *bf, const float *T, float *dattn, float *dwf, float *dbf, float *dT,
+                           int accumulate, void *stream) {
+    if (!dims_ok(H, D, F) || !workspace || !attn || !wf || !T || !dattn || !dwf || !dT) return HSG_EINVAL;
+    const float *s0 = workspace, *s1 = workspace + (size_t)kStage * kNT * H;
+    hipLaunchKernelGGL(k_attn_params_bwd, dim3(H + 1), dim3(256), 0, (hipStream_t)stream, H, D, F, s0, s1, attn, wf,
+                       bf, T, dattn, dwf, dbf, dT, accumulate);
     return status();
 }
 

@@ -94,22 +94,30 @@ class _GatAggregate(torch.autograd.Function):
         return dZ, da1, dtau, (dout if ctx.has_origin else None), None, None, None, None, None
 
 
-def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope):
+def attn_tables(attn, T, wf, bf, H, D):
+    """(a1 [H, D], tau [11, H]) of one layer's attention parameters: the source part
+    of attn_fc and the per-box edge term (hsg_attn_params_fwd).  They depend on the
+    parameters only, so every application of a layer in one step can share them."""
+    lib = load()
+    a1 = attn.new_empty(H, D)
+    tau = attn.new_empty(N_BOX + 1, H)
+    check(lib.hsg_attn_params_fwd(H, D, T.shape[1], ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(a1), ptr(tau),
+                                  stream_of(attn)), "hsg_attn_params_fwd")
+    return a1, tau
+
+
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None):
     """Forward of one multi-head application with the TF-IDF-table edge term:
-    3 launches (attention parameters -> tau table, sigma, edge pass).  Returns
-    (out, saved)."""
+    3 launches (attention parameters -> tau table, sigma, edge pass; 2 when
+    ``tables`` = :func:`attn_tables` of this layer is passed in).  Returns (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
     if Z.shape != (n_src, HD):
         raise ValueError(f"Z has shape {tuple(Z.shape)}, relation expects ({n_src}, {HD})")
     if origin is not None and origin.shape != (n_dst, HD):
         raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
-    F = T.shape[1]
     st = stream_of(Z)
-    a1 = Z.new_empty(H, D)
-    tau = Z.new_empty(N_BOX + 1, H)
-    check(lib.hsg_attn_params_fwd(H, D, F, ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(a1), ptr(tau), st),
-          "hsg_attn_params_fwd")
+    a1, tau = tables if tables is not None else attn_tables(attn, T, wf, bf, H, D)
     sigma = Z.new_empty(n_src, H)
     check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
@@ -123,11 +131,14 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope):
     return (out if origin is not None else h), saved
 
 
-def gat_table_bwd(saved, dout, dZ=True, dst=None):
+def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     """Backward of :func:`gat_table_fwd`: 3 launches (dst pass, src pass with the
     d a1 partials, parameter backward).  Returns dZ (None with dZ=False).  ``dst`` =
     (dattn, dwf, dbf, dT, acc_head, acc_T): gradient buffers written or added into
-    (dbf None on W2S).  The origin gradient is ``dout`` itself."""
+    (dbf None on W2S).  ``stage`` = (workspace, accumulate) instead: only reduce this
+    application's partials into a per-layer workspace (hsg_attn_params_stage); the
+    caller runs :func:`attn_params_finish` once for all applications of the layer.
+    The origin gradient is ``dout`` itself."""
     lib = load()
     Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin = saved
     dout = dout.contiguous()
@@ -146,13 +157,31 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None):
     check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
                               ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
           "hsg_gat_bwd_src")
-    if dst is not None:
+    if stage is not None:
+        ws, acc = stage
+        check(lib.hsg_attn_params_stage(H, D, nbd, ptr(dtp), nbs, ptr(da1p), ptr(ws), int(bool(acc)), st),
+              "hsg_attn_params_stage")
+    elif dst is not None:
         dattn, dwf, dbf, dT, acc_head, acc_T = dst
         ws = Z.new_empty(lib.hsg_attn_params_bwd_workspace_floats(H, D))
         check(lib.hsg_attn_params_bwd(H, D, T.shape[1], nbd, ptr(dtp), nbs, ptr(da1p), ptr(attn), ptr(wf),
                                       ptr(bf), ptr(T), ptr(dattn), ptr(dwf), ptr(dbf), ptr(dT), ptr(ws),
                                       int(bool(acc_head)) | (2 if acc_T else 0), st), "hsg_attn_params_bwd")
     return dZt if dZ else None
+
+
+def attn_params_workspace(Z, H, D):
+    """A stage workspace for :func:`gat_table_bwd` / :func:`attn_params_finish`."""
+    return Z.new_empty(load().hsg_attn_params_bwd_workspace_floats(H, D))
+
+
+def attn_params_finish(ws, attn, T, wf, bf, H, D, dst):
+    """Parameter gradients from a stage workspace (hsg_attn_params_finish); ``dst``
+    as in :func:`gat_table_bwd`."""
+    dattn, dwf, dbf, dT, acc_head, acc_T = dst
+    check(load().hsg_attn_params_finish(H, D, T.shape[1], ptr(ws), ptr(attn), ptr(wf), ptr(bf), ptr(T), ptr(dattn),
+                                        ptr(dwf), ptr(dbf), ptr(dT), int(bool(acc_head)) | (2 if acc_T else 0),
+                                        stream_of(ws)), "hsg_attn_params_finish")
 
 
 class _GatHeadsTable(torch.autograd.Function):

@@ -35,7 +35,8 @@ import torch
 from .dense import gemm
 from .ffn import ffn_bwd, ffn_fwd
 from .hproj import hproj_bwd, hproj_fwd
-from .ops import LEAKY_SLOPE, gat_table_bwd, gat_table_fwd
+from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
+                  gat_table_fwd)
 
 
 def _grad_dst(p):
@@ -85,24 +86,43 @@ class _Layer:
                             self.gamma, self.beta) if p is not None]
 
 
-def _apply_fwd(lay, rel, T, neighbor, origin):
-    """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59."""
+def _apply_fwd(lay, rel, T, neighbor, origin, tables=None):
+    """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59.
+    ``tables``: the layer's (a1, tau) from :func:`ops.attn_tables`, shared by its
+    applications within one forward."""
     H, D = lay.H, lay.D
     if lay.p_attn > 0:
         Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn)
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
-    x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE)
+    x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
                           lay.p_ffn, lay.eps)
     return out, (hsaved, neighbor, gsaved, fsaved)
 
 
-def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc):
+def _attn_dst(lay, T):
+    """(dattn, dwf, dbf, dT, acc_head, acc_T) for the attention-parameter backward of
+    ``lay``, or None when none of them needs a gradient (scratch for unneeded ones:
+    the kernel writes all four)."""
+    (dattn, dwf, dbf), a_h = _grad_group([lay.attn, lay.wf, lay.bf])
+    dT, a_T = _grad_dst(T)
+    if not any(t is not None for t in (dattn, dwf, dbf, dT)):
+        return None
+    dattn, dwf, dT = [t if t is not None else torch.empty_like(p)
+                      for t, p in ((dattn, lay.attn), (dwf, lay.wf), (dT, T))]
+    if lay.bf is not None and dbf is None:
+        dbf = torch.empty_like(lay.bf)
+    return dattn, dwf, dbf, dT, a_h, a_T
+
+
+def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None):
     """Backward of one application.  Parameter gradients go to p.grad; the
     neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
-    not None.  Returns the origin's gradient (the FFN's residual-branch dx)."""
+    not None.  ``stage`` = (workspace, accumulate): the attention-parameter partials
+    only go into the layer's stage workspace (finished once per layer by the caller).
+    Returns the origin's gradient (the FFN's residual-branch dx)."""
     hsaved, neighbor, gsaved, fsaved = saved
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     dw1, a_w1 = _grad_dst(lay.w1)
@@ -110,16 +130,11 @@ def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc):
     (db1, db2, dg, dbt), a_b = _grad_group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
                                 dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b))
-    (dattn, dwf, dbf), a_h = _grad_group([lay.attn, lay.wf, lay.bf])
-    dT, a_T = _grad_dst(T)
     need_dz = nb_grad is not None or lay.W.requires_grad
-    any_param = any(t is not None for t in (dattn, dwf, dbf, dT))
-    if any_param:                       # the kernel writes all four: scratch for unneeded ones
-        dattn, dwf, dT = [t if t is not None else torch.empty_like(p)
-                          for t, p in ((dattn, lay.attn), (dwf, lay.wf), (dT, T))]
-        if lay.bf is not None and dbf is None:
-            dbf = torch.empty_like(lay.bf)
-    dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=(dattn, dwf, dbf, dT, a_h, a_T) if any_param else None)
+    if stage is not None:
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage)
+    else:
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(lay, T))
     if need_dz:
         dW, a_W = _grad_dst(lay.W)
         if hsaved is not None:
@@ -141,10 +156,12 @@ class _GatStack(torch.autograd.Function):
         apps = []                               # (layer, saved, neighbour key, origin key)
 
         def run(lay, rel, nb, org, outk):
-            out, saved = _apply_fwd(lay, rel, T, states[nb], states[org])
+            out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[id(lay)])
             states[outk] = out
             apps.append((lay, saved, nb, org))
 
+        # the attention tables depend on the parameters only: once per layer
+        tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
         run(w2s, rw, ("w", 0), ("s", 0), ("s", 1))
         for i in range(n_iter):
             run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))
@@ -165,6 +182,9 @@ class _GatStack(torch.autograd.Function):
         skip = {("w", 0)} if not need_w0 else set()
         if not need_s0:
             skip.add(("s", 0))
+        # attention-parameter partials of all applications of a layer meet in one
+        # stage workspace; the parameter transform runs once per layer at the end
+        stages = {}
         for lay, saved, nb, org in reversed(ctx.apps):
             dout = grads.pop((org[0], org[1] + 1))
             nb_grad, nb_acc = None, False
@@ -174,13 +194,22 @@ class _GatStack(torch.autograd.Function):
                 else:
                     nb_grad = saved[1].new_empty(ctx.shapes[nb])
                     grads[nb] = nb_grad
-            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc)
+            if id(lay) not in stages:
+                stages[id(lay)] = (lay, attn_params_workspace(saved[2][0], lay.H, lay.D))
+                stage = (stages[id(lay)][1], False)
+            else:
+                stage = (stages[id(lay)][1], True)
+            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage)
             if org in skip:
                 continue
             if org in grads:
                 grads[org].add_(dx)
             else:
                 grads[org] = dx
+        for lay, ws in stages.values():
+            dst = _attn_dst(lay, T)
+            if dst is not None:
+                attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
         ctx.apps = None
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None

@@ -118,6 +118,19 @@ int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_
                         const float *da1_part, const float *attn, const float *wf, const float *bf,
                         const float *T, float *dattn, float *dwf, float *dbf, float *dT, float *workspace,
                         int accumulate, void *stream);
+/* The same backward in its two stages, so several applications of one layer can
+ * share the parameter transform: hsg_attn_params_stage reduces one application's
+ * partial slabs into the workspace (accumulate != 0: added to what the workspace
+ * holds -- the slabs of earlier applications of the same layer, in call order);
+ * hsg_attn_params_finish turns the accumulated workspace into the parameter
+ * gradients (accumulate flags as hsg_attn_params_bwd).  The transform is linear,
+ * so stage(a1) + stage(a2) -> finish equals finish(a1) + finish(a2) up to fp32
+ * summation order. */
+int hsg_attn_params_stage(int H, int D, int n_dtau_part, const float *dtau_part, int n_da1_part,
+                          const float *da1_part, float *workspace, int accumulate, void *stream);
+int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const float *attn, const float *wf,
+                           const float *bf, const float *T, float *dattn, float *dwf, float *dbf, float *dT,
+                           int accumulate, void *stream);
 size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 
 /* ---- dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32) ---------------------------
