@@ -42,22 +42,24 @@ def _fused_ok(lib, x, w1, w2):
             and w2.is_contiguous())
 
 
-def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
-    """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  Returns (out, saved)."""
+def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None):
+    """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  ``H_out``: a contiguous
+    [n, d_hid] buffer for the hidden activations (the fused stack hands in slices of
+    one per-layer buffer).  Returns (out, saved)."""
     lib = load()
     n, d = x.shape
     out = torch.empty_like(x)
     mean = x.new_empty(n)
     rstd = x.new_empty(n)
     if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
-        H = x.new_empty(n, w1.shape[0])
+        H = H_out if H_out is not None else x.new_empty(n, w1.shape[0])
         y = torch.empty_like(x)
         seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
         check(lib.hsg_ffn_small_fwd(n, d, w1.shape[0], ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(gamma),
                                     ptr(beta), float(eps), float(p_drop), ptr(seed_t), off, ptr(H), ptr(y),
                                     ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ffn_small_fwd")
         return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
-    H = gemm(x, w1, b_t=True, bias=b1, relu=True)          # [n, d_hid]
+    H = gemm(x, w1, b_t=True, bias=b1, relu=True, out=H_out)    # [n, d_hid]
     y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
     seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
     check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
@@ -65,11 +67,14 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS):
     return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
 
 
-def ffn_bwd(saved, dout, dst):
+def ffn_bwd(saved, dout, dst, act_grads=None):
     """Backward of :func:`ffn_fwd`.  ``dst`` = (dw1, acc_w1, dw2, acc_w2, db1, db2,
     dgamma, dbeta, acc_b): gradient buffers shaped [d_hid, d], [d, d_hid], [d_hid],
     [d], [d], [d] (None when not needed), each written or -- with its accumulate
-    flag -- added into.  Returns dx (a fresh tensor)."""
+    flag -- added into.  ``act_grads`` = (dy [n, d], dH [n, d_hid]) contiguous buffers
+    that receive the two activation gradients; the weight gradients (dw1 = dH^T x,
+    dw2 = dy^T H) are then left to the caller, which runs them once over all
+    applications of a layer (pass dw1 = dw2 = None).  Returns dx (a fresh tensor)."""
     lib = load()
     x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
@@ -77,14 +82,14 @@ def ffn_bwd(saved, dout, dst):
     n, d = x.shape
     st = stream_of(x)
     d_hid = H.shape[1]
-    dy = torch.empty_like(x)
+    dy = act_grads[0] if act_grads is not None else torch.empty_like(x)
     dx = torch.empty_like(x)
     if _fused_ok(lib, x, w1, w2) and H.is_contiguous() and y.is_contiguous():
         # one launch: LN/dropout backward, dH = (dy W2) * relu'(H), dx = ds + dH W1
         nb = rt = lib.hsg_ffn_small_bwd_blocks(n)
         part = x.new_empty(nb, 3, d)
         hpart = x.new_empty(rt, d_hid)
-        dH = x.new_empty(n, d_hid)
+        dH = act_grads[1] if act_grads is not None else x.new_empty(n, d_hid)
         check(lib.hsg_ffn_small_bwd(n, d, d_hid, ptr(dout), ptr(x), ptr(H), ptr(y), ptr(w1), ptr(w2), ptr(gamma),
                                     ptr(mean), ptr(rstd), p_drop, ptr(seed_t), off, ptr(dy), ptr(dH), ptr(dx),
                                     ptr(part), ptr(hpart), st), "hsg_ffn_small_bwd")
@@ -95,7 +100,8 @@ def ffn_bwd(saved, dout, dst):
                              ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
         rt = row_tiles(n, d_hid, d)
         hpart = x.new_empty(rt, d_hid)
-        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart)   # [n, d_hid] + db1 partials
+        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart,   # [n, d_hid] + db1 partials
+                  out=act_grads[1] if act_grads is not None else None)
         gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
     if dw2 is not None:
         gemm(dy, H, a_t=True, out=dw2, add=dw2 if acc_w2 else None)  # [d, d_hid]

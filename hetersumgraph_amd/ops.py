@@ -106,10 +106,11 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
-def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None):
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None):
     """Forward of one multi-head application with the TF-IDF-table edge term:
     3 launches (attention parameters -> tau table, sigma, edge pass; 2 when
-    ``tables`` = :func:`attn_tables` of this layer is passed in).  Returns (out, saved)."""
+    ``tables`` = :func:`attn_tables` of this layer is passed in).  ``out``: a contiguous
+    [n_dst, H*D] buffer for the result (with an origin).  Returns (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
     if Z.shape != (n_src, HD):
@@ -122,7 +123,10 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None):
     check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
     h = Z.new_empty(n_dst, HD)
-    out = Z.new_empty(n_dst, HD) if origin is not None else None
+    if origin is None:
+        out = None
+    elif out is None:
+        out = Z.new_empty(n_dst, HD)
     m = Z.new_empty(n_dst, H)
     l = Z.new_empty(n_dst, H)
     check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),

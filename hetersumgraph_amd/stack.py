@@ -86,19 +86,21 @@ class _Layer:
                             self.gamma, self.beta) if p is not None]
 
 
-def _apply_fwd(lay, rel, T, neighbor, origin, tables=None):
+def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None):
     """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59.
     ``tables``: the layer's (a1, tau) from :func:`ops.attn_tables`, shared by its
-    applications within one forward."""
+    applications within one forward; ``x_out`` / ``H_out``: this application's slots
+    of the layer's FFN-input and hidden-activation buffers."""
     H, D = lay.H, lay.D
     if lay.p_attn > 0:
         Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn)
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
-    x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables)
+    x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
+                              out=x_out)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
-                          lay.p_ffn, lay.eps)
+                          lay.p_ffn, lay.eps, H_out=H_out)
     return out, (hsaved, neighbor, gsaved, fsaved)
 
 
@@ -117,19 +119,25 @@ def _attn_dst(lay, T):
     return dattn, dwf, dbf, dT, a_h, a_T
 
 
-def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None):
+def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None):
     """Backward of one application.  Parameter gradients go to p.grad; the
     neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
     not None.  ``stage`` = (workspace, accumulate): the attention-parameter partials
     only go into the layer's stage workspace (finished once per layer by the caller).
-    Returns the origin's gradient (the FFN's residual-branch dx)."""
+    ``act_grads`` = (dy, dH) slots: the FFN's activation gradients go there and its
+    weight gradients are left to the caller (one GEMM per weight over all
+    applications).  Returns the origin's gradient (the FFN's residual-branch dx)."""
     hsaved, neighbor, gsaved, fsaved = saved
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
-    dw1, a_w1 = _grad_dst(lay.w1)
-    dw2, a_w2 = _grad_dst(lay.w2)
+    if act_grads is None:
+        dw1, a_w1 = _grad_dst(lay.w1)
+        dw2, a_w2 = _grad_dst(lay.w2)
+    else:
+        dw1, a_w1, dw2, a_w2 = None, False, None, False
     (db1, db2, dg, dbt), a_b = _grad_group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
-                                dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b))
+                                dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b),
+                 act_grads=act_grads)
     need_dz = nb_grad is not None or lay.W.requires_grad
     if stage is not None:
         dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage)
@@ -153,12 +161,25 @@ class _GatStack(torch.autograd.Function):
         G, w2s, s2w, T, n_iter = cfg
         rw, rs = G.relation("W2S"), G.relation("S2W")
         states = {("w", 0): w0.contiguous(), ("s", 0): s0.contiguous()}
-        apps = []                               # (layer, saved, neighbour key, origin key)
+        apps = []                               # (layer, saved, neighbour key, origin key, slot)
+        # every application of a layer writes its FFN input and hidden activations
+        # into one [applications, rows, width] buffer per layer, so the backward runs
+        # each FFN weight gradient as ONE GEMM over all applications' rows
+        n_app = {id(w2s): n_iter + 1, id(s2w): n_iter}
+        bufs, slot = {}, {id(w2s): 0, id(s2w): 0}
 
         def run(lay, rel, nb, org, outk):
-            out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[id(lay)])
+            key = id(lay)
+            if key not in bufs:
+                d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+                bufs[key] = (states[org].new_empty(n_app[key], rel.n_dst, d),
+                             states[org].new_empty(n_app[key], rel.n_dst, d_hid))
+            a = slot[key]
+            slot[key] += 1
+            out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],
+                                    H_out=bufs[key][1][a])
             states[outk] = out
-            apps.append((lay, saved, nb, org))
+            apps.append((lay, saved, nb, org, a))
 
         # the attention tables depend on the parameters only: once per layer
         tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
@@ -166,7 +187,7 @@ class _GatStack(torch.autograd.Function):
         for i in range(n_iter):
             run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))
             run(w2s, rw, ("w", i + 1), ("s", i + 1), ("s", i + 2))
-        ctx.cfg, ctx.apps = cfg, apps
+        ctx.cfg, ctx.apps, ctx.bufs = cfg, apps, bufs
         ctx.need = (w0.requires_grad, s0.requires_grad)
         ctx.shapes = {k: v.shape for k, v in states.items()}
         return states[("s", n_iter + 1)]
@@ -184,8 +205,8 @@ class _GatStack(torch.autograd.Function):
             skip.add(("s", 0))
         # attention-parameter partials of all applications of a layer meet in one
         # stage workspace; the parameter transform runs once per layer at the end
-        stages = {}
-        for lay, saved, nb, org in reversed(ctx.apps):
+        stages, gbufs = {}, {}
+        for lay, saved, nb, org, a in reversed(ctx.apps):
             dout = grads.pop((org[0], org[1] + 1))
             nb_grad, nb_acc = None, False
             if nb not in skip:
@@ -199,7 +220,11 @@ class _GatStack(torch.autograd.Function):
                 stage = (stages[id(lay)][1], False)
             else:
                 stage = (stages[id(lay)][1], True)
-            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage)
+            if id(lay) not in gbufs:
+                X, Hh = ctx.bufs[id(lay)]
+                gbufs[id(lay)] = (lay, torch.empty_like(X), torch.empty_like(Hh))
+            _, DY, DH = gbufs[id(lay)]
+            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]))
             if org in skip:
                 continue
             if org in grads:
@@ -210,7 +235,20 @@ class _GatStack(torch.autograd.Function):
             dst = _attn_dst(lay, T)
             if dst is not None:
                 attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
-        ctx.apps = None
+        # FFN weight gradients, one GEMM per weight over every application's rows:
+        # dW2 = dY^T H, dW1 = dH^T X with [applications * rows] as the reduction
+        for lay, DY, DH in gbufs.values():
+            X, Hh = ctx.bufs[id(lay)]
+            d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+            dw2, a_w2 = _grad_dst(lay.w2)
+            if dw2 is not None:
+                gemm(DY.view(-1, d), Hh.view(-1, d_hid), a_t=True, out=dw2.view(d, d_hid),
+                     add=dw2.view(d, d_hid) if a_w2 else None)
+            dw1, a_w1 = _grad_dst(lay.w1)
+            if dw1 is not None:
+                gemm(DH.view(-1, d_hid), X.view(-1, d), a_t=True, out=dw1.view(d_hid, d),
+                     add=dw1.view(d_hid, d) if a_w1 else None)
+        ctx.apps = ctx.bufs = None
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None
         n_params = len(ctx.needs_input_grad) - 3
