@@ -613,11 +613,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
                                                     float *__restrict__ G, float *__restrict__ dpre,
                                                     float *__restrict__ dtau_part) {
     __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
+    __shared__ float s_g[HSG_WAVES][512], s_gh[HSG_WAVES][512];   // G_v and G_v * h_v, flat (H*D <= 512)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
     const bool kact = k < H;
     float *sd = s_dtau[wid];
+    float *sg = s_g[wid], *sgh = s_gh[wid];
     if constexpr (TAU_MODE == HSG_TAU_TABLE) {
         for (int i = lane; i < HSG_NT * HSG_HMAX; i += 64) sd[i] = 0.f;
         wave_lds_sync();
@@ -637,20 +639,35 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
             t0 = tau_row<TAU_MODE>(R, beg + l);
             pre0 = sigma[u0 * H + k] + tau[t0 * H + k];
         }
+        // G = dOut * elu'(h) over the row with the flat lane mapping (every access a
+        // contiguous 256-B wave transaction), staged in LDS with G*h; the (k, l) lanes
+        // then pick their head's features from there
+        constexpr int NF = 8;                     // 64 * NF >= H*D (<= 512)
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int f = lane + 64 * i;
+            if (f < HD) {
+                const size_t o = (size_t)v * HD + f;
+                const float hv = hsv[o], dv = dout[o];
+                const float gv = origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv;
+                G[o] = gv;
+                sg[f] = gv;
+                sgh[f] = gv * hv;
+            }
+        }
+        wave_lds_sync();
         float g[NE];
         float rho = 0.f;
         const int kc = kact ? k : H - 1;
 #pragma unroll
-        for (int i = 0; i < NE; ++i) {           // clamped, unconditional loads; masked values
+        for (int i = 0; i < NE; ++i) {
             const int d = l + lph * i;
-            const size_t o = (size_t)v * HD + kc * D + min(d, D - 1);
-            const float hv = hsv[o], dv = dout[o];
             const bool ok = kact && d < D;
-            const float gv = ok ? (origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv) : 0.f;
-            if (ok) G[o] = gv;
-            g[i] = gv;
-            rho = fmaf(gv, hv, rho);
+            const int f = kc * D + min(d, D - 1);
+            g[i] = ok ? sg[f] : 0.f;
+            rho += ok ? sgh[f] : 0.f;
         }
+        wave_lds_sync();                          // the next destination rewrites the stage
         if (end == beg) continue;   // uniform per wave: no typed in-edge, no gradient
         rho = group_sum(rho, lph);
         const float inv = kact ? 1.f / lvv : 0.f;
