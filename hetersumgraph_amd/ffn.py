@@ -26,16 +26,17 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, get_gemm_dtype, row_tiles
+from .dense import gemm, row_tiles
 
 LN_EPS = 1e-5
 
 
 def _fused_ok(lib, x, w1, w2):
     """The one-launch narrow FFN kernels (hsg_ffn_small_fwd / _bwd: the W2S FFN,
-    d=64, d_hid=512) cover this call: fp32 GEMM mode, contiguous operands.
+    d=64, d_hid=512) cover this call: contiguous operands.  They compute in fp32 in
+    either GEMM mode (in the bf16 mode this small FFN simply stays exact).
     HSG_FFN_FUSED=0 selects the split path (A/B tests)."""
-    if os.environ.get("HSG_FFN_FUSED", "1") == "0" or get_gemm_dtype() != "f32":
+    if os.environ.get("HSG_FFN_FUSED", "1") == "0":
         return False
     d_hid, d = w1.shape
     return (bool(lib.hsg_ffn_small_supported(d, d_hid)) and x.is_contiguous() and w1.is_contiguous()
