@@ -27,7 +27,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
-           "hsg_attn_params_stage", "hsg_attn_params_finish")
+           "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
+           "hsg_hproj_fwd_logits")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -74,6 +75,8 @@ _SIGS = {
     "hsg_dropmask_scale": [_F],
     "hsg_dropmask": [_I, _I, _I, _F, _P, ctypes.c_uint32, _P, _P],
     "hsg_hproj_fwd": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
+    "hsg_hproj_fwd_logits_supported": [_I, _I],
+    "hsg_hproj_fwd_logits": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P],
     "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _I, _P],

@@ -125,11 +125,18 @@ __global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p,
 // Loads for chunk t+1 are issued before the MFMAs of chunk t.  All loads are
 // unconditional from clamped addresses followed by a select, so the compiler can
 // keep them in flight together.  VEC: in % 4 == 0 and 16-byte aligned rows.
+// Optional fused epilogue (a1 != nullptr): the source logits of the attention,
+// sigma[i, k] = <Z[i, kD:(k+1)D], a1_k> (module/GATLayer.py:91-92 / 130-131, the
+// hsg_attn_src_logits of the split path), from the Z values just stored: per slot a
+// 16-lane butterfly over the slot's columns, then the wave's slots of one head are
+// added in slot order.  Needs every head's slots inside one wave's slot group
+// (SG % SPH == 0, checked by the host).
 template <int SG, bool VEC>
 __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, const float *__restrict__ X,
                                                    int ldx, const float *__restrict__ W,
                                                    const uint32_t *__restrict__ bits, float scale,
-                                                   float *__restrict__ Z, int ldz) {
+                                                   float *__restrict__ Z, int ldz, const float *__restrict__ a1,
+                                                   float *__restrict__ sigma) {
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int SPH = (D + 15) / 16, NS = H * SPH, NG = (NS + SG - 1) / SG;
     const int lane = threadIdx.x & 63;
@@ -215,6 +222,34 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
         for (int r = 0; r < 4; ++r) {
             const int gi = i0 + lk * 4 + r;
             if (gi < n) Z[(long)gi * ldz + k * D + j] = acc[q][r] * scale;
+        }
+    }
+    if (a1) {
+        float sg[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < SG; ++q) {
+            const int slot = gq * SG + q;                    // wave-uniform
+            if (slot >= NS) break;
+            const int k = slot / SPH;
+            const int j = (slot - k * SPH) * 16 + li;
+            const float a = j < D ? a1[k * D + j] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = (acc[q][r] * scale) * a;
+                v += __shfl_xor(v, 1);
+                v += __shfl_xor(v, 2);
+                v += __shfl_xor(v, 4);
+                v += __shfl_xor(v, 8);
+                sg[r] += v;
+            }
+            if ((slot + 1) % SPH == 0) {                     // last slot of head k
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int gi = i0 + lk * 4 + r;
+                    if (li == 0 && gi < n) sigma[(long)gi * H + k] = sg[r];
+                    sg[r] = 0.f;
+                }
+            }
         }
     }
 }
@@ -521,7 +556,19 @@ int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t of
 
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W, const uint32_t *bits,
                   float p, float *Z, int ldz, void *stream) {
+    return hsg_hproj_fwd_logits(n, in, H, D, X, ldx, W, bits, p, Z, ldz, nullptr, nullptr, stream);
+}
+
+int hsg_hproj_fwd_logits_supported(int H, int D) {
+    const int sph = (D + 15) / 16;
+    return H >= 1 && D >= 1 && 4 % sph == 0 ? 1 : 0;                // SG = 4 slots hold whole heads
+}
+
+int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, const float *W, const uint32_t *bits,
+                         float p, float *Z, int ldz, const float *a1, float *sigma, void *stream) {
     if (n < 0 || in < 1 || H < 1 || D < 1 || ldx < in || !fits_buffers(n, in, H, D, ldx)) return HSG_EINVAL;
+    if ((a1 == nullptr) != (sigma == nullptr)) return HSG_EINVAL;
+    if (a1 && !hsg_hproj_fwd_logits_supported(H, D)) return HSG_EINVAL;
     if (n == 0) return 0;
     constexpr int SG = 4;
     const int ns = H * ((D + 15) / 16);
@@ -530,10 +577,10 @@ int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const fl
     const dim3 grid((unsigned)((tasks + 3) / 4));
     if (vec)
         hipLaunchKernelGGL((k_hproj_fwd<SG, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx, W,
-                           bits, drop_scale(p), Z, ldz);
+                           bits, drop_scale(p), Z, ldz, a1, sigma);
     else
         hipLaunchKernelGGL((k_hproj_fwd<SG, false>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx,
-                           W, bits, drop_scale(p), Z, ldz);
+                           W, bits, drop_scale(p), Z, ldz, a1, sigma);
     return status();
 }
 

@@ -18,8 +18,11 @@ from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
 
 
-def hproj_fwd(X, W, H, D, p):
-    """Z [n, H*D] and the state its backward needs.  X, W contiguous fp32."""
+def hproj_fwd(X, W, H, D, p, a1=None):
+    """Z [n, H*D] and the state its backward needs.  X, W contiguous fp32.  With
+    ``a1`` [H, D] (the attention's source part), also the source logits
+    sigma [n, H] from the same launch: returns (Z, saved, sigma); sigma is None when
+    the fused form does not cover (H, D) (the caller computes it separately)."""
     lib = load()
     n, d_in = X.shape
     st = stream_of(X)
@@ -27,9 +30,19 @@ def hproj_fwd(X, W, H, D, p):
     bits = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=X.device)
     check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
     Z = X.new_empty(n, H * D)
+    saved = (X, W, bits, H, D, float(p))
+    if a1 is not None:
+        if not lib.hsg_hproj_fwd_logits_supported(H, D):
+            check(lib.hsg_hproj_fwd(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D, st),
+                  "hsg_hproj_fwd")
+            return Z, saved, None
+        sigma = X.new_empty(n, H)
+        check(lib.hsg_hproj_fwd_logits(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D,
+                                       ptr(a1.contiguous()), ptr(sigma), st), "hsg_hproj_fwd_logits")
+        return Z, saved, sigma
     check(lib.hsg_hproj_fwd(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D, st),
           "hsg_hproj_fwd")
-    return Z, (X, W, bits, H, D, float(p))
+    return Z, saved
 
 
 def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False):

@@ -106,11 +106,12 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
-def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None):
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None):
     """Forward of one multi-head application with the TF-IDF-table edge term:
     3 launches (attention parameters -> tau table, sigma, edge pass; 2 when
     ``tables`` = :func:`attn_tables` of this layer is passed in).  ``out``: a contiguous
-    [n_dst, H*D] buffer for the result (with an origin).  Returns (out, saved)."""
+    [n_dst, H*D] buffer for the result (with an origin).  ``sigma``: the source logits
+    when the head projection already produced them.  Returns (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
     if Z.shape != (n_src, HD):
@@ -119,8 +120,9 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         raise ValueError(f"origin has shape {tuple(origin.shape)}, expected ({n_dst}, {HD})")
     st = stream_of(Z)
     a1, tau = tables if tables is not None else attn_tables(attn, T, wf, bf, H, D)
-    sigma = Z.new_empty(n_src, H)
-    check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
+    if sigma is None:                   # else: from the projection's epilogue (hsg_hproj_fwd_logits)
+        sigma = Z.new_empty(n_src, H)
+        check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
     h = Z.new_empty(n_dst, HD)
     if origin is None:

@@ -92,12 +92,15 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
     applications within one forward; ``x_out`` / ``H_out``: this application's slots
     of the layer's FFN-input and hidden-activation buffers."""
     H, D = lay.H, lay.D
-    if lay.p_attn > 0:
+    sigma = None
+    if lay.p_attn > 0 and tables is not None:     # source logits from the projection's epilogue
+        Z, hsaved, sigma = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, a1=tables[0])
+    elif lay.p_attn > 0:
         Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn)
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
-                              out=x_out)
+                              out=x_out, sigma=sigma)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
                           lay.p_ffn, lay.eps, H_out=H_out)

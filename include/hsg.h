@@ -237,6 +237,14 @@ int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t of
                  void *stream);
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                   const uint32_t *bits, float p, float *Z, int ldz, void *stream);
+/* hsg_hproj_fwd plus the attention's source logits sigma[i][k] = <Z[i, kD:(k+1)D], a1[k]>
+ * (a1 [H][D]; sigma [n][H]) from the same launch -- hsg_attn_src_logits fused into the
+ * projection's epilogue.  hsg_hproj_fwd_logits_supported(H, D): whether the fused form
+ * covers (H, D) (ceil(D/16) divides 4); a1 = sigma = NULL is hsg_hproj_fwd. */
+int hsg_hproj_fwd_logits_supported(int H, int D);
+int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, const float *W,
+                         const uint32_t *bits, float p, float *Z, int ldz, const float *a1, float *sigma,
+                         void *stream);
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
                  const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);

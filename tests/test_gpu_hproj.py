@@ -59,3 +59,33 @@ def test_masks_independent_across_heads_and_calls():
     # pairwise independence: P(keep_k and keep_j) ~ (1-p)^2
     both = (a[0] * a[1]).mean().item()
     assert abs(both - 0.81) < 0.01
+
+
+@pytest.mark.parametrize("n,d_in,H,D", [(19200 // 8, 300, 8, 8), (1120, 64, 6, 50), (333, 72, 3, 16), (77, 40, 2, 64),
+                                         (130, 20, 4, 5), (50, 16, 1, 33)])
+def test_fused_source_logits_match_split_kernel(n, d_in, H, D):
+    """hsg_hproj_fwd_logits: Z is bitwise the plain projection's, and sigma = <Z_k, a1_k>
+    agrees with the split hsg_attn_src_logits to fp32 summation-order noise; shapes
+    whose slots do not fit a wave's slot group (ceil(D/16) = 3) fall back (None)."""
+    from hetersumgraph_amd import _lib, rng
+    from hetersumgraph_amd.hproj import hproj_fwd
+    torch.manual_seed(n + D)
+    X = torch.randn(n, d_in, device="cuda")
+    W = torch.randn(H * D, d_in, device="cuda") / d_in ** 0.5
+    a1 = torch.randn(H, D, device="cuda")
+    rng.manual_seed(3)
+    Z0, _ = hproj_fwd(X, W, H, D, 0.1)
+    rng.manual_seed(3)
+    Z1, _, sigma = hproj_fwd(X, W, H, D, 0.1, a1=a1)
+    torch.cuda.synchronize()
+    assert torch.equal(Z0, Z1)
+    if (D + 15) // 16 == 3:
+        assert sigma is None
+        return
+    lib = _lib.load()
+    ref = torch.empty(n, H, device="cuda")
+    _lib.check(lib.hsg_attn_src_logits(n, H, D, Z0.data_ptr(), a1.data_ptr(), ref.data_ptr(),
+                                       torch.cuda.current_stream().cuda_stream), "logits")
+    torch.cuda.synchronize()
+    tol = 1e-5 * max(1.0, ref.abs().max().item())
+    assert (sigma - ref).abs().max().item() <= tol
