@@ -17,6 +17,7 @@
 // dw) or to the per-head product before it is accumulated (dx).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/hsg.h"
 #include "hsg_rng.h"
@@ -379,7 +380,9 @@ DwGeom dw_geom(int n, int in, int H, int D) {
     g.ctiles = (in + 63) / 64;
     g.sgroups = (ns + kDwSlots - 1) / kDwSlots;
     const int steps = (n + 31) / 32 > 0 ? (n + 31) / 32 : 1;
-    int want = 512 / (g.ctiles * g.sgroups);
+    int target = 512;                                   // blocks to aim for
+    if (const char *e = getenv("HSG_HPROJ_DWB")) target = atoi(e);     // dev sweep
+    int want = target / (g.ctiles * g.sgroups);
     if (want < 1) want = 1;
     if (want > steps) want = steps;
     const int per = (steps + want - 1) / want;    // 32-row steps per chunk
@@ -561,7 +564,7 @@ int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const fl
 
 int hsg_hproj_fwd_logits_supported(int H, int D) {
     const int sph = (D + 15) / 16;
-    return H >= 1 && D >= 1 && 4 % sph == 0 ? 1 : 0;                // SG = 4 slots hold whole heads
+    return H >= 1 && D >= 1 && 4 % sph == 0 ? 1 : 0;                // the slot group holds whole heads
 }
 
 int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, const float *W, const uint32_t *bits,
@@ -570,17 +573,29 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
     if ((a1 == nullptr) != (sigma == nullptr)) return HSG_EINVAL;
     if (a1 && !hsg_hproj_fwd_logits_supported(H, D)) return HSG_EINVAL;
     if (n == 0) return 0;
-    constexpr int SG = 4;
-    const int ns = H * ((D + 15) / 16);
-    const long tasks = (long)((n + 15) / 16) * ((ns + SG - 1) / SG);
+    const int sph = (D + 15) / 16;
+    const int ns = H * sph;
     const bool vec = in % 4 == 0 && ldx % 4 == 0 && aligned16(X) && aligned16(W);
-    const dim3 grid((unsigned)((tasks + 3) / 4));
-    if (vec)
-        hipLaunchKernelGGL((k_hproj_fwd<SG, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx, W,
-                           bits, drop_scale(p), Z, ldz, a1, sigma);
-    else
-        hipLaunchKernelGGL((k_hproj_fwd<SG, false>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, ldx,
-                           W, bits, drop_scale(p), Z, ldz, a1, sigma);
+    // slot-group size: 2 when a head has at most 2 slots (W2S, D = 8: 28.6 us against
+    // 32.1 us at SG = 4, rocprofv3 kernel trace), else 4 (whole heads per wave)
+    int sg = sph <= 2 ? 2 : 4;
+    if (const char *e = getenv("HSG_HPROJ_SG")) {                     // dev A/B
+        const int v = atoi(e);
+        sg = (v == 1 && sph == 1) ? 1 : (v == 2 && sph <= 2) ? 2 : 4;
+    }
+#define HSG_HF(SG_)                                                                                              \
+    {                                                                                                            \
+        const long tasks = (long)((n + 15) / 16) * ((ns + SG_ - 1) / SG_);                                       \
+        const dim3 grid((unsigned)((tasks + 3) / 4));                                                            \
+        if (vec)                                                                                                 \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, \
+                               ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
+        else                                                                                                     \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, false>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, \
+                               ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
+    }
+    if (sg == 1) HSG_HF(1) else if (sg == 2) HSG_HF(2) else HSG_HF(4)
+#undef HSG_HF
     return status();
 }
 
@@ -593,8 +608,21 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const long rtiles = (n + 15) / 16;
     // wide wave tiles (16 x 64) when that still gives >= 2048 waves, else 16 x 16
     const long wide = rtiles * ((in + 63) / 64);
-    if (wide >= 2048) {
-        hipLaunchKernelGGL((k_hproj_dx<4, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D, dZ,
+    if (const char *e = getenv("HSG_HPROJ_DX")) {                     // dev sweep: CT*10 + HF
+        const int v = atoi(e), ct = v / 10, hf = v % 10;
+        const long tiles = rtiles * ((in + 16 * ct - 1) / (16 * ct));
+        const dim3 g((unsigned)((tiles + 3) / 4));
+#define HSG_DXV(CT_, HF_)                                                                                       \
+    if (ct == CT_ && hf == HF_) {                                                                               \
+        hipLaunchKernelGGL((k_hproj_dx<CT_, HF_>), g, dim3(256), 0, st, n, in, H, D, dZ, ldz, W, bits, s, dX, ldx, \
+                           accumulate);                                                                         \
+        return status();                                                                                        \
+    }
+        HSG_DXV(4, 1) HSG_DXV(4, 4) HSG_DXV(2, 2)
+#undef HSG_DXV
+    }
+    if (wide >= 2048) {                  // HF = 1: 26.9 us vs 28.0 (HF = 2) on the W2S shape
+        hipLaunchKernelGGL((k_hproj_dx<4, 1>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D, dZ,
                            ldz, W, bits, s, dX, ldx, accumulate);
     } else {
         const long narrow = rtiles * ((in + 15) / 16);
