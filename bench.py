@@ -307,11 +307,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; ranks beyond the visible devices share them (only for the
+    # single-GPU rehearsal of the multi-rank path with HSG_DIST_BACKEND=gloo)
+    ndev = max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("HSG_DIST_BACKEND", "nccl")       # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from hetersumgraph_amd import _lib
     _lib.load()
     from hetersumgraph_amd.dense import set_gemm_dtype
