@@ -149,19 +149,34 @@ class HSumGraph(nn.Module):
         return ngram_feature, cnn_feature
 
     def _sent_lstm_feature(self, features, glen):
-        pad_seq = rnn.pad_sequence(features, batch_first=True)
-        lstm_input = rnn.pack_padded_sequence(pad_seq, glen, batch_first=True)
+        """HiGraph.py:135-142 on the per-document feature list (see _sent_lstm_rows)."""
+        return self._sent_lstm_rows(torch.cat(features, dim=0) if len(features) != 1 else features[0], glen)
+
+    def _sent_lstm_rows(self, ngram, glen):
+        """HiGraph.py:135-142 on the documents' sentence rows laid end to end.  The
+        padding to [docs, max_len] and the gather of the valid rows back are one index
+        scatter and one index gather (positions cached) instead of a copy per document
+        each way; the same values move, so the result is the reference's bit for bit."""
+        n_doc, max_len = len(glen), max(glen)
+        key = ("lstm_index", tuple(glen))
+        idx = getattr(self, "_lstm_idx", None)
+        if idx is None or idx[0] != key or idx[1].device != ngram.device:
+            doc = torch.repeat_interleave(torch.arange(n_doc), torch.tensor(glen))
+            pos = torch.cat([torch.arange(g) for g in glen])
+            idx = (key, (doc * max_len + pos).to(ngram.device))
+            self._lstm_idx = idx
+        flat = idx[1]
+        pad_seq = ngram.new_zeros(n_doc * max_len, ngram.shape[1]).index_copy(0, flat, ngram)
+        lstm_input = rnn.pack_padded_sequence(pad_seq.view(n_doc, max_len, -1), glen, batch_first=True)
         lstm_output, _ = self.lstm(lstm_input)
-        unpacked, unpacked_len = rnn.pad_packed_sequence(lstm_output, batch_first=True)
-        lstm_embedding = [unpacked[i][:unpacked_len[i]] for i in range(len(unpacked))]
-        return self.lstm_proj(torch.cat(lstm_embedding, dim=0))
+        unpacked, _ = rnn.pad_packed_sequence(lstm_output, batch_first=True, total_length=max_len)
+        return self.lstm_proj(unpacked.reshape(n_doc * max_len, -1).index_select(0, flat))
 
     def set_snfeature(self, graph):
         snode_id = node_ids(graph, "dtype", 1.0)
         ngram_feature, cnn_feature = self._sent_cnn_feature(graph, snode_id)
         glen = sentence_counts(graph)
-        features = list(torch.split(ngram_feature, glen, dim=0))
-        lstm_feature = self._sent_lstm_feature(features, glen)
+        lstm_feature = self._sent_lstm_rows(ngram_feature, glen)
         return torch.cat([cnn_feature, lstm_feature], dim=1)
 
 

@@ -40,7 +40,7 @@ def step(n):
     ngram, cnn = model._sent_cnn_feature(G, snode_id)
     t = tick("cnn", t)
     glen = HiGraph.sentence_counts(G)
-    lstm = model._sent_lstm_feature(list(torch.split(ngram, glen, dim=0)), glen)
+    lstm = model._sent_lstm_rows(ngram, glen)
     t = tick("lstm", t)
     s = model.n_feature_proj(torch.cat([cnn, lstm], dim=1))
     st = model.gat_stack(G, w, s)
