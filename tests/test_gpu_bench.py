@@ -19,3 +19,31 @@ def test_e2e_train_step_runs(config):
     G.to(dev)
     dt = bench.time_train_step(G, config, 2, steps=2, warmup=1, dev=dev)
     assert np.isfinite(dt) and dt > 0
+
+
+def test_bench_json_contract(tmp_path):
+    """`python bench.py` prints ONE JSON line with the driver's keys, the roofline and
+    cpu_baseline objects, and a value consistent with its own step time (short run,
+    bounded CPU sample)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
+                          "--no-e2e", "--cpu-docs", "1", "--cpu-steps", "1", "--kernel-reps", "5"],
+                         cwd=root, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert abs(d["value"] - d["config"]["graph_edges_per_gpu"] / (d["ms_per_step"] * 1e-3)) <= 1e-6 * d["value"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    c = d["cpu_baseline"]
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
