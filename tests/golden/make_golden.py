@@ -167,8 +167,8 @@ class HPS:
         self.__dict__.update(d)
 
 
-def model_case(HiGraph, docs, seed, cls_name):
-    hps = HPS()
+def model_case(HiGraph, docs, seed, cls_name, **hps_kw):
+    hps = HPS(**hps_kw)
     res = {}
     for dt in (torch.float32, torch.float64):
         torch.manual_seed(seed)
@@ -201,11 +201,30 @@ def model_case(HiGraph, docs, seed, cls_name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="regenerate one fixture (file stem), e.g. model_hsg_cfg1")
     args = ap.parse_args()
     torch.set_num_threads(8)
     HiGraph, GAT = import_reference(args.ref)
     meta = {"ref_hash." + k: np.array(v) for k, v in ref_hashes(args.ref).items()}
     meta["torch"] = np.array(torch.__version__)
+
+    def want(stem):
+        return args.only is None or args.only == stem
+
+    if want("model_hsg_cfg1"):
+        # 4 config-1-shaped documents (N=30, W=400, k=20; 12,000 graph edges) through
+        # the whole HSumGraph: logit parity beyond the 2-doc toy fixture
+        rng = np.random.default_rng(15)
+        cdocs = sort_by_sentences([synth.make_hsg_doc(rng, N=30, W=400, k=20, vocab_size=2000)
+                                   for _ in range(4)])
+        res = model_case(HiGraph, cdocs, 6, "HSumGraph", vocab_size=2000)
+        extra = {"sent_words": np.concatenate([d.words for d in cdocs]).astype(np.int32),
+                 "sent_label": np.concatenate([d.label for d in cdocs]).astype(np.int8),
+                 "vocab_size": np.array(2000)}
+        np.savez_compressed(os.path.join(HERE, "model_hsg_cfg1.npz"), **graph_arrays(cdocs), **compact(res),
+                            **extra, **meta)
+    if args.only is not None:
+        return
 
     # edge-case graph: zero-typed sentences (phantoms only), isolated words,
     # every tf-idf box 0..9, degree-1 words

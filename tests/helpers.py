@@ -93,3 +93,17 @@ def seeded_gat_params(seed_w2s, seed_s2w):
     w2s = weights.seed_module(WSWGAT(300, 64, 8, 0.1, 512, 0.1, 50, "W2S"), seed_w2s)
     s2w = weights.seed_module(WSWGAT(64, 300, 6, 0.1, 512, 0.1, 50, "S2W"), seed_s2w)
     return w2s.eval(), s2w.eval()
+
+
+def synth_fixture(docs):
+    """Fixture-like dict from synth DocArrays (no reference outputs)."""
+    offs = np.cumsum([0] + [d.n_nodes for d in docs])
+    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
+    z = {"g_n_nodes": np.array([d.n_nodes for d in docs]), "g_n_edges": np.array([len(d.src) for d in docs]),
+         "g_unit": cat(lambda d, o: d.unit), "g_ndtype": cat(lambda d, o: d.ndtype),
+         "g_wid": cat(lambda d, o: d.wid), "g_src": cat(lambda d, o: d.src + o),
+         "g_dst": cat(lambda d, o: d.dst + o), "g_tffrac": cat(lambda d, o: d.tffrac),
+         "g_edtype": cat(lambda d, o: d.edtype)}
+    z["n_w"] = int((z["g_unit"] == 0).sum())
+    z["n_s"] = int((z["g_unit"] == 1).sum())
+    return z

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from helpers import (build_graph, concat_arrays, gat_inputs, load_fixture, projections,
-                     seeded_gat_params, upstream)
+                     seeded_gat_params, synth_fixture, upstream)
 
 pytestmark = pytest.mark.gpu
 
@@ -115,20 +115,6 @@ def oracle_gat(z, seed):
     R1, R2 = upstream(seed, o1.shape, o2.shape)
     ((o1 * R1.double()).sum() + (o2 * R2.double()).sum()).backward()
     return dict(o1=o1, o2=o2, Xw=Xw, Xs=Xs, T=T, p1=p1, p2=p2, n_w=n_w, n_s=n_s)
-
-
-def synth_fixture(docs):
-    """Fixture-like dict from synth DocArrays (no reference outputs)."""
-    offs = np.cumsum([0] + [d.n_nodes for d in docs])
-    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
-    z = {"g_n_nodes": np.array([d.n_nodes for d in docs]), "g_n_edges": np.array([len(d.src) for d in docs]),
-         "g_unit": cat(lambda d, o: d.unit), "g_ndtype": cat(lambda d, o: d.ndtype),
-         "g_wid": cat(lambda d, o: d.wid), "g_src": cat(lambda d, o: d.src + o),
-         "g_dst": cat(lambda d, o: d.dst + o), "g_tffrac": cat(lambda d, o: d.tffrac),
-         "g_edtype": cat(lambda d, o: d.edtype)}
-    z["n_w"] = int((z["g_unit"] == 0).sum())
-    z["n_s"] = int((z["g_unit"] == 1).sum())
-    return z
 
 
 def random_docs(kind, seed):

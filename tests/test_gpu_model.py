@@ -25,9 +25,9 @@ class HPS:
         self.__dict__.update(d)
 
 
-def build_model(cls_name, seed):
+def build_model(cls_name, seed, vocab_size=500):
     from hetersumgraph_amd import HiGraph
-    hps = HPS()
+    hps = HPS(vocab_size=int(vocab_size))
     torch.manual_seed(seed)
     embed = torch.nn.Embedding(hps.vocab_size, 300, padding_idx=0)
     model = getattr(HiGraph, cls_name)(hps, embed)
@@ -35,19 +35,25 @@ def build_model(cls_name, seed):
     return model.eval().cuda()
 
 
-@pytest.mark.parametrize("name,cls,seed", [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5)])
+MODEL_CASES = [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5),
+               # 4 config-1-shaped documents (N=30, W=400, k=20; 12,000 graph edges)
+               ("model_hsg_cfg1", "HSumGraph", 6)]
+
+
+@pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
 def test_model_logits_match_reference(name, cls, seed):
     from hetersumgraph_amd import graph as hg
     z = load_fixture(name)
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))                      # in-place, train.py:112
-    model = build_model(cls, seed)
+    model = build_model(cls, seed, z.get("vocab_size", 500))
     # MIOpen (like cuDNN) has no RNN backward in eval mode; train-mode LSTM with
     # its inter-layer dropout set to 0 is numerically the eval LSTM
     model.lstm.train()
     model.lstm.dropout = 0.0
     logits = model(G)
     err = np.abs(logits.detach().cpu().double().numpy() - z["logits"]).max()
+    print(f"{name}: logit max |diff| vs reference fp32 = {err:.3e}")
     assert err <= 1e-4, f"logit max |diff| {err:.3e}"
     err64 = np.abs(logits.detach().cpu().double().numpy() - z["logits64"]).max()
     assert err64 <= 1e-4
@@ -103,7 +109,7 @@ def test_train_step_runs_and_learns():
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("name,cls,seed", [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5)])
+@pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
 def test_model_logits_bf16_gemm_error_budget(name, cls, seed):
     """Config-5 precision mode (bf16 GEMM operands, fp32 accumulate and storage): the
     logits stay within the SURVEY §8c bf16 budget (2e-2) of the reference fp64 run.
@@ -112,7 +118,7 @@ def test_model_logits_bf16_gemm_error_budget(name, cls, seed):
     z = load_fixture(name)
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))
-    model = build_model(cls, seed)
+    model = build_model(cls, seed, z.get("vocab_size", 500))
     model.lstm.train()
     model.lstm.dropout = 0.0
     with gemm_dtype("bf16"):

@@ -1,0 +1,147 @@
+"""Parity of the TIMED path -- the fused WSWGAT stack (hetersumgraph_amd.stack,
+W2S + n_iter x (S2W, W2S), HiGraph.py:99-106) -- against the fp64 CPU oracle
+(oracle/fused.py, pinned to the reference's golden vectors) chained the same way,
+at the BASELINE.json workload sizes:
+
+* cfg2 -- 32 CNN/DM-shaped docs (N=35, W=600, k=36; 159,040 graph edges), the
+  bench workload;
+* cfg4 -- 32 Multi-News-shaped HDSG examples (3 docs x 15 sentences, doc nodes);
+* cfg5 -- 32 NYT50-shaped docs (N=80, W=900, k=14; 160 phantom in-edges per
+  sentence), in fp32 and in the bf16-GEMM-operand mode BASELINE.json names for it.
+
+Eval mode (dropout cannot match the oracle draw for draw); outputs and the
+gradients of both input states, the shared _TFembed table and every parameter
+(reference key names) after ``s.backward(R)``.
+
+Tolerances (written here):
+* outputs: fp32 <= 2e-5 absolute (LayerNorm outputs are O(1)); bf16-GEMM <= 2e-2;
+* state gradients (Xw, Xs, _TFembed), fp32: per row |err| <= 2e-4 * max|ref|
+  except at most 0.5 % of rows (fp32 ReLU-gate flips at near-zero
+  pre-activations, which the reference's own fp32 and fp64 runs disagree on too);
+  those rows must still stay within 1e-2 * max|ref|, so an indexing bug cannot
+  hide inside the allowance; the other rows' relative Frobenius error <= 2e-4;
+* parameter gradients (sums over all nodes, so a gate flip moves every entry a
+  little): Frobenius error <= 5e-4 and largest entry <= 5e-3 relative (fp32);
+* bf16-GEMM mode (a reduced-precision mode, not the 1e-4 contract): every
+  gradient within 5e-2 relative Frobenius and 1e-1 of max|ref| per entry.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import build_graph, concat_arrays, gat_inputs, seeded_gat_params, synth_fixture
+
+pytestmark = pytest.mark.gpu
+
+N_ITER = 2
+
+
+def _f64(t):
+    return torch.as_tensor(np.asarray(t.detach().cpu() if torch.is_tensor(t) else t), dtype=torch.float64)
+
+
+def grad_stats(got, ref, rtol=2e-4, scale_ref=None):
+    """fro: relative Frobenius error over the rows within ``rtol`` * max|ref| (the
+    bulk); worst: largest row error / max|ref|; bad_rows: rows beyond rtol.
+    ``scale_ref``: the tensor whose magnitude sets the scale instead of ``ref``."""
+    got, ref = _f64(got), _f64(ref)
+    sref = ref if scale_ref is None else _f64(scale_ref)
+    if got.dim() == 1:
+        got, ref = got.unsqueeze(1), ref.unsqueeze(1)
+    got, ref = got.reshape(got.shape[0], -1), ref.reshape(ref.shape[0], -1)
+    scale = max(sref.abs().max().item(), 1e-12)
+    row = (got - ref).abs().max(1).values
+    good = row <= rtol * scale
+    fro = ((got - ref)[good].norm() / max(sref.norm().item(), 1e-30)).item()
+    return dict(fro=fro, worst=row.max().item() / scale, bad_rows=int((~good).sum().item()),
+                rows=int(got.shape[0]))
+
+
+def check_grad(fails, name, got, ref, fro_tol, bad_frac, worst_tol, scale_ref=None):
+    # bf16 mode (bad_frac 1): every row is in the Frobenius bound
+    s = grad_stats(got, ref, rtol=2e-4 if bad_frac < 1 else worst_tol, scale_ref=scale_ref)
+    print(f"  {name:40s} fro {s['fro']:.2e} worst {s['worst']:.2e} bad {s['bad_rows']}/{s['rows']}")
+    if s["fro"] > fro_tol or s["worst"] > worst_tol or s["bad_rows"] > max(2, int(bad_frac * s["rows"])):
+        fails.append((name, s))
+
+
+def oracle_stack(z, seed):
+    """fp64 oracle: s1 = W2S(w0, s0); then n_iter x (w = S2W(w, s); s = W2S(w, s))."""
+    from oracle import fused
+    a = concat_arrays(z)
+    rws = fused.typed_relation("W2S", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    rsw = fused.typed_relation("S2W", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    Xw, Xs, T = gat_inputs(seed, rsw["n_dst"], rws["n_dst"])
+    Xw, Xs, T = (t.double().requires_grad_() for t in (Xw, Xs, T))
+    w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
+    p1, p2 = fused.as_params(w2s), fused.as_params(s2w)
+    w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T)
+    for _ in range(N_ITER):
+        w = fused.wswgat_layer("S2W", rsw, w, s, p2, T)
+        s = fused.wswgat_layer("W2S", rws, w, s, p1, T)
+    R = torch.from_numpy(np.random.default_rng(seed).standard_normal(tuple(s.shape)))
+    (s * R).sum().backward()
+    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, p1=p1, p2=p2, R=R)
+
+
+def gpu_stack(z, seed, R):
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    from hetersumgraph_amd.stack import fused_stack_ok, gat_stack
+    dev = torch.device("cuda")
+    G = build_graph(z).to(dev)
+    n_w, n_s = int(z["n_w"]), int(z["n_s"])
+    Xw, Xs, T = gat_inputs(seed, n_w, n_s)
+    Xw, Xs = Xw.to(dev).requires_grad_(), Xs.to(dev).requires_grad_()
+    T = T.to(dev).requires_grad_()
+    register_tfidf_table(G, T)
+    w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
+    w2s, s2w = w2s.to(dev), s2w.to(dev)
+    assert fused_stack_ok(G, w2s, s2w, T, Xw, Xs)
+    s = gat_stack(G, w2s, s2w, T, Xw, Xs, N_ITER)
+    assert type(s.grad_fn).__name__.startswith("_GatStack")        # the timed node, not the layer path
+    s.backward(R.to(dev, torch.float32))
+    torch.cuda.synchronize()
+    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w)
+
+
+CASES = [("cfg2", "f32", 31), ("cfg4", "f32", 32), ("cfg5", "f32", 33), ("cfg5", "bf16", 33)]
+
+
+@pytest.mark.parametrize("config,dtype,seed", CASES)
+def test_stack_vs_oracle_full_size(config, dtype, seed):
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.dense import gemm_dtype
+    from hetersumgraph_amd.module.GATStackLayer import reference_named_grads
+    docs = synth.make_batch_docs(config, seed=0)
+    z = synth_fixture(docs)
+    n_edges = int(z["g_n_edges"].sum())
+    o = oracle_stack(z, seed)
+    with gemm_dtype(dtype):
+        r = gpu_stack(z, seed, o["R"])
+    out_tol, fro_tol, worst_tol = (2e-5, 2e-4, 1e-2) if dtype == "f32" else (2e-2, 5e-2, 1e-1)
+    err = (_f64(r["s"]) - o["s"]).abs().max().item()
+    print(f"{config} {dtype}: {len(docs)} docs, {n_edges} edges, output max|diff| {err:.3e}")
+    assert err <= out_tol
+    bad_frac = 0.005 if dtype == "f32" else 1.0
+    fails = []
+    check_grad(fails, "Xs", r["Xs"], o["Xs"], fro_tol, bad_frac, worst_tol)
+    check_grad(fails, "Xw", r["Xw"], o["Xw"], fro_tol, bad_frac, worst_tol)
+    check_grad(fails, "_TFembed", r["T"], o["T"], fro_tol, bad_frac, worst_tol)
+    n = 0
+    for tag, mod, pd in (("w2s", r["w2s"], o["p1"]), ("s2w", r["s2w"], o["p2"])):
+        for k, g in reference_named_grads(mod):
+            # a weight gradient sums over every node, so one gate flip moves all of it
+            # a little: bounded as a whole (Frobenius and largest entry, relative),
+            # 1e-3 as the golden tests' parameter bound (test_gpu_gat.py)
+            pfro, pworst = (5e-4, 5e-3) if dtype == "f32" else (fro_tol, worst_tol)
+            # S2W feat_fc.bias: d bf_k = a3_k * sum_e dpre_e, and over a destination
+            # without phantom in-edges (every word) the softmax makes sum_e dpre_e
+            # cancel to the leaky-ReLU regime mix -- a small difference of large
+            # terms.  Its error is bounded on the scale of those terms: the same
+            # head's feat_fc.weight gradient (a3_k x sum_e dpre_e T[t_e]).
+            sref = pd[k[:-4] + "weight"].grad if k.endswith("feat_fc.bias") else None
+            check_grad(fails, f"{tag}.{k}", g, pd[k].grad, pfro, 0.999 if dtype == "f32" else 1.0, pworst,
+                       scale_ref=sref)
+            n += 1
+    assert n == 8 * 3 + 6 * 4 + 12
+    assert not fails, fails
