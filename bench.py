@@ -136,15 +136,16 @@ def workload_shape(config):
 def make_shard(config, rank, world, seed):
     """The global batch (32 docs per GPU, seeded) split by document across ranks
     (hetersumgraph_amd.parallel.shard_documents); returns this rank's docs, its
-    batched graph and the global edge count."""
+    batched graph, the global edge count and this rank's share of the documents
+    (the weight of its per-rank-mean gradient in the global mean)."""
     from hetersumgraph_amd import graph as hg
     from hetersumgraph_amd import synth
-    from hetersumgraph_amd.parallel import shard_documents
+    from hetersumgraph_amd.parallel import shard_documents, shard_fraction
     per_gpu = synth.CONFIGS[config][1]
     docs_all = synth.make_batch_docs(config, seed=seed, n_docs=per_gpu * world)
     docs = shard_documents(docs_all, rank, world)
     G = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
-    return docs, G, int(sum(len(d.src) for d in docs_all))
+    return docs, G, int(sum(len(d.src) for d in docs_all)), shard_fraction(docs_all, rank, world)
 
 
 class Stack(torch.nn.Module):
@@ -324,7 +325,7 @@ def main():
     from hetersumgraph_amd.dense import set_gemm_dtype
     set_gemm_dtype(args.dtype)
 
-    docs, G, E_global = make_shard(args.config, rank, world, args.seed)
+    docs, G, E_global, frac = make_shard(args.config, rank, world, args.seed)
     E_total = G.number_of_edges()
     G.to(dev)
     torch.manual_seed(args.seed)                       # identical replicas on every rank
@@ -344,9 +345,10 @@ def main():
         s.backward(R)                  # d/ds of sum(s * R): the upstream gradient of the stack output
 
     def allreduce():
-        # the data-parallel exchange: bucketed mean all-reduce over RCCL
+        # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL,
+        # in 2 MiB buckets issued back to back asynchronously, then waited
         from hetersumgraph_amd.parallel import allreduce_gradients
-        allreduce_gradients(params)
+        allreduce_gradients(params, scale=frac)
 
     def zero():
         # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients

@@ -2,10 +2,18 @@
 
 The batched graph is a disjoint union of documents (reference dataloader.py:480,
 ``dgl.batch``), so the path shards by document with no data-path collective; the
-one exchange per step is the mean all-reduce of parameter gradients after
-backward, done in flat buckets over RCCL (``torch.distributed`` backend "nccl" on
-ROCm = RCCL over xGMI).  Parameters must start identical on every rank (same seed
-or a broadcast), as the reference's replicated Adam assumes.
+one exchange per step is the all-reduce of parameter gradients after backward,
+done in buckets over RCCL (``torch.distributed`` backend "nccl" on ROCm = RCCL
+over xGMI), then ``clip_grad_norm_`` on the reduced gradients and a replicated
+Adam step (train.py:130-135).  Parameters must start identical on every rank
+(same seed or a broadcast).
+
+The reference's loss is a mean over the batch's documents (train.py:118-119:
+``dgl.sum_nodes(G, "loss").mean()``).  A rank's loss is the mean over ITS
+documents, so the global-batch gradient is sum_r (n_r / N) grad_r, not the plain
+average of the per-rank gradients unless every rank holds the same number of
+documents.  :func:`shard_fraction` gives n_r / N from the deterministic shard
+(no communication), and both reducers below take it as ``scale``.
 """
 from __future__ import annotations
 
@@ -13,21 +21,41 @@ import torch
 import torch.distributed as dist
 
 
-def shard_documents(docs, rank, world, weight=None):
-    """Deterministic balanced split of ``docs`` into ``world`` shards; returns this
-    rank's list.  Greedy longest-processing-time by ``weight(doc)`` (default: the
-    document's edge count, ``doc.n_edges`` or ``len(doc.src)``), ties by index."""
-    if weight is None:
-        def weight(d):
-            return getattr(d, "n_edges", None) or len(d.src)
+def _doc_weight(d):
+    return getattr(d, "n_edges", None) or len(d.src)
+
+
+def shard_owners(docs, world, weight=None):
+    """Owner rank of every document: greedy longest-processing-time by
+    ``weight(doc)`` (default: the document's edge count), ties by index, with the
+    document COUNT balanced first -- shards differ by at most one document, and
+    among the least-filled ranks the one with the fewest edges takes the next
+    (largest remaining) document."""
+    weight = weight or _doc_weight
     order = sorted(range(len(docs)), key=lambda i: (-weight(docs[i]), i))
     load = [0] * world
+    count = [0] * world
     owner = [0] * len(docs)
     for i in order:
-        r = min(range(world), key=lambda q: (load[q], q))
+        r = min(range(world), key=lambda q: (count[q], load[q], q))
         owner[i] = r
         load[r] += weight(docs[i])
+        count[r] += 1
+    return owner
+
+
+def shard_documents(docs, rank, world, weight=None):
+    """This rank's documents of a deterministic balanced split (:func:`shard_owners`),
+    in their original order."""
+    owner = shard_owners(docs, world, weight)
     return [docs[i] for i in range(len(docs)) if owner[i] == rank]
+
+
+def shard_fraction(docs, rank, world, weight=None):
+    """n_rank / N: this rank's share of the global batch's documents -- the factor
+    its per-rank-mean gradient carries in the global-mean gradient."""
+    owner = shard_owners(docs, world, weight)
+    return sum(1 for o in owner if o == rank) / max(len(docs), 1)
 
 
 def _buckets(tensors, bucket_bytes):
@@ -43,24 +71,106 @@ def _buckets(tensors, bucket_bytes):
         yield cur
 
 
-def allreduce_gradients(params, group=None, bucket_bytes=8 << 20):
-    """Average ``p.grad`` over the process group, in flat buckets of at most
-    ``bucket_bytes`` (one all-reduce each).  Parameters without a gradient are
-    skipped (every rank must agree on which those are).  RCCL averages natively;
-    gloo sums, then the bucket is divided by the world size."""
+def _launch(bucket, scale, world, group):
+    """Start one bucket's all-reduce; returns (work, flat, bucket)."""
+    flat = torch.cat([g.reshape(-1) for g in bucket])
+    if scale is not None:
+        flat.mul_(scale)                       # weighted sum = global-batch mean
+        op = dist.ReduceOp.SUM
+    elif dist.get_backend(group) == "nccl":
+        op = dist.ReduceOp.AVG                 # RCCL averages natively
+    else:
+        op = dist.ReduceOp.SUM                 # gloo: sum, divided after the wait
+    work = dist.all_reduce(flat, op=op, group=group, async_op=True)
+    return work, flat, bucket, (scale is None and op == dist.ReduceOp.SUM)
+
+
+def _finish(pending, world):
+    for work, flat, bucket, divide in pending:
+        work.wait()
+        if divide:
+            flat.div_(world)
+        torch._foreach_copy_(bucket, [v.view_as(g) for v, g in
+                                      zip(torch.split(flat, [g.numel() for g in bucket]), bucket)])
+
+
+def allreduce_gradients(params, group=None, bucket_bytes=2 << 20, scale=None):
+    """Reduce ``p.grad`` over the process group in flat buckets of at most
+    ``bucket_bytes`` (all issued asynchronously, then waited): the mean when
+    ``scale`` is None (equal shards), else sum_r scale_r * grad_r with this rank's
+    ``scale`` = :func:`shard_fraction`.  Parameters without a gradient are skipped
+    (every rank must agree on which those are)."""
     if not dist.is_available() or not dist.is_initialized():
         return
     world = dist.get_world_size(group)
     if world == 1:
         return
     grads = [p.grad for p in params if p.grad is not None]
-    use_avg = dist.get_backend(group) == "nccl"
-    for bucket in _buckets(grads, bucket_bytes):
-        flat = torch.cat([g.reshape(-1) for g in bucket])
-        if use_avg:
-            dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
-        else:
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-            flat.div_(world)
-        torch._foreach_copy_(bucket, [v.view_as(g) for v, g in
-                                      zip(torch.split(flat, [g.numel() for g in bucket]), bucket)])
+    pending = [_launch(b, scale, world, group) for b in _buckets(grads, bucket_bytes)]
+    _finish(pending, world)
+
+
+class GradientReducer:
+    """Bucketed gradient all-reduce overlapped with the backward (DDP-style, for
+    the eager train step, train.py:114-135).
+
+    Parameters are bucketed in REVERSE registration order (the order backward
+    finalises them: the classifier head and the GAT stack before the sentence
+    encoder).  A post-accumulate-grad hook marks a parameter ready; when every
+    parameter of a bucket is ready its all-reduce is launched asynchronously on
+    the communicator's stream while autograd carries on with the rest of the
+    backward.  Buckets are launched strictly in bucket order (a ready bucket waits
+    for its predecessors), so every rank issues the same collective sequence even
+    if hooks fire in a different order.  :meth:`finish` waits for the outstanding
+    buckets, writes the reduced values back into ``p.grad`` and returns the
+    parameters, so the caller clips (``clip_grad_norm_``) and steps the optimizer
+    on the reduced gradients.
+
+    The fused WSWGAT stack returns its parameter gradients through autograd
+    (hetersumgraph_amd/stack.py), so its hooks fire when the stack node's backward
+    ends -- before the encoder's backward runs.
+    """
+
+    def __init__(self, params, group=None, bucket_bytes=2 << 20, scale=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.group, self.scale = group, scale
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.buckets = list(_buckets(list(reversed(self.params)), bucket_bytes))
+        self.where = {}
+        for bi, b in enumerate(self.buckets):
+            for p in b:
+                self.where[id(p)] = bi
+        self.ready = [0] * len(self.buckets)
+        self.next = 0                        # next bucket to launch
+        self.pending = []
+        self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
+            if self.world > 1 else []
+
+    def _launch_next(self):
+        b = self.buckets[self.next]
+        live = [q.grad for q in b if q.grad is not None]
+        if live:
+            self.pending.append(_launch(live, self.scale, self.world, self.group))
+        self.next += 1
+
+    def _on_grad(self, p):
+        self.ready[self.where[id(p)]] += 1
+        while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next]):
+            self._launch_next()
+
+    def finish(self):
+        """Launch the buckets still outstanding (e.g. one holding a parameter that
+        got no gradient this step), in order; wait for all; reset for the next step."""
+        if self.world > 1:
+            while self.next < len(self.buckets):
+                self._launch_next()
+            _finish(self.pending, self.world)
+        self.pending = []
+        self.next = 0
+        self.ready = [0] * len(self.buckets)
+        return self.params
+
+    def remove(self):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []

@@ -4,7 +4,10 @@ Masks are a stateless hash of (seed, offset, element) (csrc/hsg_rng.h).  ``seed`
 lives in device memory so a captured HIP graph sees a new one after every
 ``advance()``; ``offset`` is a host-side counter, one value per dropout call, so
 calls within a step draw independent masks.  Forward and backward of a call share
-(seed, offset) and therefore the mask.
+(seed, offset) and therefore the mask: ``take()`` hands out a device-side SNAPSHOT
+of the seed (one 8-byte copy per seed value, taken at the first call after an
+``advance()`` / ``manual_seed()``), so reseeding or advancing between a forward and
+its backward (recompute, interleaved forwards) cannot change the backward's mask.
 """
 from __future__ import annotations
 
@@ -19,15 +22,19 @@ class DropoutRNG:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.seed = torch.tensor([seed], dtype=torch.int64, device=device)
         self.offset = 0
+        self._snap = None
 
     def take(self):
-        """(seed tensor, offset) for one dropout call."""
+        """(seed snapshot tensor, offset) for one dropout call."""
+        if self._snap is None:
+            self._snap = self.seed.clone()        # device copy: graph-capturable
         self.offset = (self.offset + 1) & 0xFFFFFFFF
-        return self.seed, self.offset
+        return self._snap, self.offset
 
     def advance(self):
         """New masks for the next step (device-side add: graph-capturable)."""
         self.seed.add_(1)
+        self._snap = None
 
 
 def get(device) -> DropoutRNG:
@@ -43,6 +50,7 @@ def manual_seed(seed, device=None):
     device = device or torch.device("cuda", torch.cuda.current_device())
     r = get(device)
     r.seed.fill_(int(seed))
+    r._snap = None
     r.offset = 0
 
 

@@ -12,19 +12,21 @@ same C-ABI kernels in the same order (so dropout masks, drawn in call order, are
 the per-layer path's), and the backward walks the applications in reverse and
 lets the kernels do the sums in their epilogues:
 
-* parameter gradients go straight into ``p.grad`` -- written by the first
-  contribution when ``p.grad`` is None, added by every later one (GEMM ADD
-  epilogue, and the ``accumulate`` flag of hsg_hproj_dw / hsg_attn_params_bwd /
-  hsg_ffn_colsums), the same semantics as autograd's AccumulateGrad;
+* a parameter's gradient buffer is written by its first contribution and added
+  into by every later application of the same layer (GEMM ADD epilogue, and the
+  ``accumulate`` flag of hsg_hproj_dw / hsg_attn_params_bwd / hsg_ffn_colsums);
+  the buffers are then RETURNED to autograd like any Function's input gradients,
+  so ``AccumulateGrad`` installs them (``zero_grad(set_to_none=True)``: the buffer
+  becomes ``p.grad`` with no copy) or adds them, and ``torch.autograd.grad``,
+  ``backward(inputs=...)``, tensor / post-accumulate hooks and DDP-style reducers
+  see an ordinary autograd node;
 * a state's gradient starts as the FFN backward's residual-branch ``dx`` of the
   layer it was the origin of, and the head-projection backward of the layer it
   was the neighbour of adds into it (hsg_hproj_dx accumulate).
 
-Parameters are inputs of the node (so autograd tracks them) but their returned
-gradients are None: they were already stored.  Gradient hooks registered on the
-parameters therefore do not fire on this path; ``HSumGraph`` falls back to the
-per-layer path (module/GAT.py) for anything it does not cover (CPU tensors, a
-foreign ``tfidfembed`` column, HSG_CHECK_NAN=1).
+``HSumGraph`` falls back to the per-layer path (module/GAT.py) for anything this
+node does not cover (CPU tensors, a foreign ``tfidfembed`` column,
+HSG_CHECK_NAN=1).
 """
 from __future__ import annotations
 
@@ -39,33 +41,43 @@ from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_t
                   gat_table_fwd)
 
 
-def _grad_dst(p):
-    """(buffer, accumulate) for p's gradient: p.grad (accumulate) or a new tensor
-    installed as p.grad (written).  (None, False) if p needs no gradient."""
-    if p is None or not p.requires_grad:
-        return None, False
-    if p.grad is None:
-        p.grad = torch.empty_like(p)
-        return p.grad, False
-    return p.grad, True
+class _Grads:
+    """The parameter-gradient buffers of one backward of the stack, keyed by
+    parameter: created (written, not zero-filled) by a parameter's first
+    contribution, added into by the later ones.  Returned to autograd at the end."""
 
+    def __init__(self):
+        self.buf = {}
 
-def _grad_group(ps):
-    """Buffers for parameters whose gradients one kernel writes together under one
-    accumulate flag: all fresh -> written; otherwise missing ones start at zero."""
-    live = [p for p in ps if p is not None and p.requires_grad]
-    if not live:
-        return [None] * len(ps), False
-    if all(p.grad is None for p in live):
-        for p in live:
-            p.grad = torch.empty_like(p)
-        acc = False
-    else:
-        for p in live:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-        acc = True
-    return [p.grad if (p is not None and p.requires_grad) else None for p in ps], acc
+    def dst(self, p):
+        """(buffer, accumulate) for p's gradient; (None, False) if p needs none."""
+        if p is None or not p.requires_grad:
+            return None, False
+        g = self.buf.get(id(p))
+        if g is None:
+            g = self.buf[id(p)] = torch.empty_like(p)
+            return g, False
+        return g, True
+
+    def group(self, ps):
+        """Buffers for parameters whose gradients one kernel writes together under
+        one accumulate flag: all fresh -> written; otherwise missing ones start at 0."""
+        live = [p for p in ps if p is not None and p.requires_grad]
+        if not live:
+            return [None] * len(ps), False
+        if all(id(p) not in self.buf for p in live):
+            for p in live:
+                self.buf[id(p)] = torch.empty_like(p)
+            acc = False
+        else:
+            for p in live:
+                if id(p) not in self.buf:
+                    self.buf[id(p)] = torch.zeros_like(p)
+            acc = True
+        return [self.buf[id(p)] if (p is not None and p.requires_grad) else None for p in ps], acc
+
+    def get(self, p):
+        return self.buf.get(id(p))
 
 
 class _Layer:
@@ -107,12 +119,12 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
     return out, (hsaved, neighbor, gsaved, fsaved)
 
 
-def _attn_dst(lay, T):
+def _attn_dst(grads, lay, T):
     """(dattn, dwf, dbf, dT, acc_head, acc_T) for the attention-parameter backward of
     ``lay``, or None when none of them needs a gradient (scratch for unneeded ones:
     the kernel writes all four)."""
-    (dattn, dwf, dbf), a_h = _grad_group([lay.attn, lay.wf, lay.bf])
-    dT, a_T = _grad_dst(T)
+    (dattn, dwf, dbf), a_h = grads.group([lay.attn, lay.wf, lay.bf])
+    dT, a_T = grads.dst(T)
     if not any(t is not None for t in (dattn, dwf, dbf, dT)):
         return None
     dattn, dwf, dT = [t if t is not None else torch.empty_like(p)
@@ -122,8 +134,8 @@ def _attn_dst(lay, T):
     return dattn, dwf, dbf, dT, a_h, a_T
 
 
-def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None):
-    """Backward of one application.  Parameter gradients go to p.grad; the
+def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None):
+    """Backward of one application.  Parameter gradients go to ``grads``; the
     neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
     not None.  ``stage`` = (workspace, accumulate): the attention-parameter partials
     only go into the layer's stage workspace (finished once per layer by the caller).
@@ -133,11 +145,11 @@ def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None)
     hsaved, neighbor, gsaved, fsaved = saved
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     if act_grads is None:
-        dw1, a_w1 = _grad_dst(lay.w1)
-        dw2, a_w2 = _grad_dst(lay.w2)
+        dw1, a_w1 = grads.dst(lay.w1)
+        dw2, a_w2 = grads.dst(lay.w2)
     else:
         dw1, a_w1, dw2, a_w2 = None, False, None, False
-    (db1, db2, dg, dbt), a_b = _grad_group([lay.b1, lay.b2, lay.gamma, lay.beta])
+    (db1, db2, dg, dbt), a_b = grads.group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
                                 dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b),
                  act_grads=act_grads)
@@ -145,9 +157,9 @@ def _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None)
     if stage is not None:
         dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage)
     else:
-        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(lay, T))
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(grads, lay, T))
     if need_dz:
-        dW, a_W = _grad_dst(lay.W)
+        dW, a_W = grads.dst(lay.W)
         if hsaved is not None:
             hproj_bwd(hsaved, dZ, dX=nb_grad, dX_acc=nb_acc, dW=dW, dW_acc=a_W)
         else:                                   # eval-mode projection Z = neighbor W^T
@@ -191,6 +203,7 @@ class _GatStack(torch.autograd.Function):
             run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))
             run(w2s, rw, ("w", i + 1), ("s", i + 1), ("s", i + 2))
         ctx.cfg, ctx.apps, ctx.bufs = cfg, apps, bufs
+        ctx.params = params
         ctx.need = (w0.requires_grad, s0.requires_grad)
         ctx.shapes = {k: v.shape for k, v in states.items()}
         return states[("s", n_iter + 1)]
@@ -209,6 +222,7 @@ class _GatStack(torch.autograd.Function):
         # attention-parameter partials of all applications of a layer meet in one
         # stage workspace; the parameter transform runs once per layer at the end
         stages, gbufs = {}, {}
+        pgrads = _Grads()
         for lay, saved, nb, org, a in reversed(ctx.apps):
             dout = grads.pop((org[0], org[1] + 1))
             nb_grad, nb_acc = None, False
@@ -227,7 +241,7 @@ class _GatStack(torch.autograd.Function):
                 X, Hh = ctx.bufs[id(lay)]
                 gbufs[id(lay)] = (lay, torch.empty_like(X), torch.empty_like(Hh))
             _, DY, DH = gbufs[id(lay)]
-            dx = _apply_bwd(lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]))
+            dx = _apply_bwd(pgrads, lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]))
             if org in skip:
                 continue
             if org in grads:
@@ -235,7 +249,7 @@ class _GatStack(torch.autograd.Function):
             else:
                 grads[org] = dx
         for lay, ws in stages.values():
-            dst = _attn_dst(lay, T)
+            dst = _attn_dst(pgrads, lay, T)
             if dst is not None:
                 attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
         # FFN weight gradients, one GEMM per weight over every application's rows:
@@ -243,19 +257,20 @@ class _GatStack(torch.autograd.Function):
         for lay, DY, DH in gbufs.values():
             X, Hh = ctx.bufs[id(lay)]
             d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
-            dw2, a_w2 = _grad_dst(lay.w2)
+            dw2, a_w2 = pgrads.dst(lay.w2)
             if dw2 is not None:
                 gemm(DY.view(-1, d), Hh.view(-1, d_hid), a_t=True, out=dw2.view(d, d_hid),
                      add=dw2.view(d, d_hid) if a_w2 else None)
-            dw1, a_w1 = _grad_dst(lay.w1)
+            dw1, a_w1 = pgrads.dst(lay.w1)
             if dw1 is not None:
                 gemm(DH.view(-1, d_hid), X.view(-1, d), a_t=True, out=dw1.view(d_hid, d),
                      add=dw1.view(d_hid, d) if a_w1 else None)
         ctx.apps = ctx.bufs = None
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None
-        n_params = len(ctx.needs_input_grad) - 3
-        return (None, dw0, ds0) + (None,) * n_params
+        out = tuple(pgrads.get(p) for p in ctx.params)
+        ctx.params = None
+        return (None, dw0, ds0) + out
 
 
 def fused_stack_ok(G, word2sent, sent2word, T, w, s):

@@ -2,7 +2,11 @@
 (DESIGN.md §5): document sharding + bucketed mean all-reduce of the
 parameter gradients.  The model on CPU is the fp64 oracle of one WSWGAT layer
 (the product kernels need a GPU), so the check is exactly the data-parallel
-algebra: mean over ranks of per-shard gradients == full-batch gradient."""
+algebra: the doc-weighted sum over ranks of per-shard gradients == full-batch
+gradient -- with equal shards (plain mean) and with skewed document sizes and an
+odd document count (shards of 3 and 2 docs: weights n_r / N), through the
+after-backward reducer and through the hook-driven GradientReducer that overlaps
+the buckets with the backward.  tests/test_gpu_dist.py runs the HIP stack itself."""
 import os
 import socket
 
@@ -19,9 +23,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _docs():
+def _docs(skewed=False):
     from hetersumgraph_amd import synth
     rng = np.random.default_rng(11)
+    if skewed:       # edge weights far apart and 5 docs: the shards hold 3 and 2 docs
+        return [synth.make_hsg_doc(rng, N=n, W=w, k=k) for n, w, k in
+                ((12, 60, 10), (2, 10, 3), (3, 12, 4), (2, 9, 2), (6, 30, 7))]
     return [synth.make_hsg_doc(rng, N=5, W=24, k=6) for _ in range(4)]
 
 
@@ -47,24 +54,34 @@ def _loss(docs, params, T, seed_base=0):
     return total / len(docs)
 
 
-def _worker(rank, world, port, bucket_bytes):
+def _worker(rank, world, port, bucket_bytes, skewed, hooks):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from hetersumgraph_amd.parallel import allreduce_gradients, shard_documents
+        from hetersumgraph_amd.parallel import (GradientReducer, allreduce_gradients, shard_documents,
+                                                shard_fraction)
         torch.set_num_threads(2)
-        docs = _docs()
+        docs = _docs(skewed)
         T = torch.randn(10, 50, generator=torch.Generator().manual_seed(5), dtype=torch.float64)
         # full batch on every rank (the expected result)
         full = _params()
         _loss(docs, full, T).backward()
         # this rank's shard
         mine = shard_documents(docs, rank, world)
-        assert len(mine) == len(docs) // world
+        frac = shard_fraction(docs, rank, world)
+        assert len(mine) in ((2, 3) if skewed else (len(docs) // world,))
+        assert frac == len(mine) / len(docs)
         local = _params()
-        _loss(mine, local, T).backward()
-        allreduce_gradients(list(local.values()), bucket_bytes=bucket_bytes)
+        scale = frac if skewed else None
+        if hooks:
+            red = GradientReducer(list(local.values()), bucket_bytes=bucket_bytes, scale=scale)
+            _loss(mine, local, T).backward()
+            red.finish()
+            red.remove()
+        else:
+            _loss(mine, local, T).backward()
+            allreduce_gradients(list(local.values()), bucket_bytes=bucket_bytes, scale=scale)
         for k in full:
             a, b = local[k].grad, full[k].grad
             assert torch.allclose(a, b, rtol=1e-9, atol=1e-12), (k, (a - b).abs().max().item())
@@ -76,10 +93,11 @@ def _worker(rank, world, port, bucket_bytes):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_bytes", [8 << 20, 4096])
-def test_sharded_allreduce_equals_full_batch(bucket_bytes):
+@pytest.mark.parametrize("bucket_bytes,skewed,hooks", [(8 << 20, False, False), (4096, False, False),
+                                                       (4096, True, False), (65536, True, True)])
+def test_sharded_allreduce_equals_full_batch(bucket_bytes, skewed, hooks):
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), bucket_bytes), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, skewed, hooks), nprocs=world, join=True)
 
 
 def test_shard_documents_balanced_and_deterministic():
@@ -92,6 +110,10 @@ def test_shard_documents_balanced_and_deterministic():
     docs = [D(e) for e in (50, 10, 40, 30, 20, 60, 5, 45)]
     shards = [shard_documents(docs, r, 3) for r in range(3)]
     assert sorted(id(d) for s in shards for d in s) == sorted(id(d) for d in docs)
+    assert sorted(len(s) for s in shards) == [2, 3, 3]          # counts balanced first
     loads = [sum(len(d.src) for d in s) for s in shards]
     assert max(loads) - min(loads) <= 60
+    # skewed sizes: still 2 + 2 docs, not 1 + 3
+    two = [shard_documents([D(e) for e in (100, 10, 10, 10)], r, 2) for r in range(2)]
+    assert [len(s) for s in two] == [2, 2]
     assert [shard_documents(docs, r, 3) for r in range(3)] == shards

@@ -128,3 +128,75 @@ def test_fused_stack_is_used_by_hsumgraph(monkeypatch):
     monkeypatch.setenv("HSG_FUSED_STACK", "0")
     s = HSumGraph.gat_stack(m, G, Xw, Xs)
     assert not type(s.grad_fn).__name__.startswith("_GatStack")
+
+
+def _eval_setup(seed=5):
+    G = _graph("hsg", seed)
+    w2s, s2w, T = _modules(seed + 4, 0.1)
+    rel_w, rel_s = G.relation("W2S"), G.relation("S2W")
+    gen = torch.Generator(device="cuda").manual_seed(seed)
+    Xw = (0.4 * torch.randn(rel_s.n_dst, 300, device="cuda", generator=gen)).requires_grad_()
+    Xs = torch.randn(rel_w.n_dst, 64, device="cuda", generator=gen).requires_grad_()
+    R = torch.randn(rel_w.n_dst, 64, device="cuda", generator=gen)
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    register_tfidf_table(G, T)
+    return G, w2s, s2w, T, Xw, Xs, R
+
+
+def test_fused_stack_is_an_ordinary_autograd_node(monkeypatch):
+    """Parameter gradients come back through autograd: autograd.grad
+    leaves every .grad untouched and matches the layer-wise path, backward(inputs=)
+    writes only the requested leaves, and post-accumulate-grad hooks fire."""
+    from hetersumgraph_amd.stack import gat_stack
+    G, w2s, s2w, T, Xw, Xs, R = _eval_setup()
+    for m in (w2s, s2w):
+        m.eval()
+    params = list(w2s.parameters()) + list(s2w.parameters()) + [T]
+    want = [Xs, w2s.ffn.w_1.weight, s2w.layer.fc_weight, T]
+    s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
+    got = torch.autograd.grad((s * R).sum(), want)
+    assert all(p.grad is None for p in params) and Xw.grad is None and Xs.grad is None
+    monkeypatch.setenv("HSG_FUSED_STACK", "0")
+    w, s = Xw, w2s(G, Xw, Xs)
+    for _ in range(2):
+        w = s2w(G, w, s)
+        s = w2s(G, w, s)
+    ref = torch.autograd.grad((s * R).sum(), want)
+    for a, b in zip(got, ref):
+        assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1.0)
+    monkeypatch.setenv("HSG_FUSED_STACK", "1")
+    s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
+    s.backward(R, inputs=[Xs])
+    assert Xs.grad is not None and all(p.grad is None for p in params) and Xw.grad is None
+    fired = []
+    hs = [p.register_post_accumulate_grad_hook(lambda p: fired.append(id(p))) for p in params]
+    s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
+    s.backward(R)
+    for h in hs:
+        h.remove()
+    assert sorted(fired) == sorted(id(p) for p in params)
+    assert torch.equal(Xs.grad, 2 * got[0]) or (Xs.grad - 2 * got[0]).abs().max().item() <= 1e-5
+
+
+def test_dropout_masks_survive_reseed_between_forward_and_backward():
+    """The backward regenerates the FFN dropout masks from a seed SNAPSHOT taken at
+    forward time: advancing or reseeding the stream between forward and
+    backward leaves every gradient bitwise unchanged."""
+    from hetersumgraph_amd import rng
+    from hetersumgraph_amd.stack import gat_stack
+    G, w2s, s2w, T, Xw, Xs, R = _eval_setup(6)
+    params = list(w2s.parameters()) + list(s2w.parameters()) + [T]
+    grads = []
+    for meddle in (False, True):
+        for p in params + [Xw, Xs]:
+            p.grad = None
+        rng.manual_seed(4321)
+        s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
+        if meddle:
+            rng.advance_all()
+            rng.manual_seed(99)
+            gat_stack(G, w2s, s2w, T, Xw.detach(), Xs.detach(), 2)    # an unrelated forward in between
+        s.backward(R)
+        grads.append([p.grad.clone() for p in params] + [Xw.grad.clone(), Xs.grad.clone()])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)

@@ -13,7 +13,7 @@ from hetersumgraph_amd import HiGraph  # noqa: E402
 from hetersumgraph_amd import graph as hg  # noqa: E402
 
 dev = torch.device("cuda", 0)
-docs, G, _ = bench.make_shard(sys.argv[1] if len(sys.argv) > 1 else "cfg2", 0, 1, 0)
+docs, G, _, _ = bench.make_shard(sys.argv[1] if len(sys.argv) > 1 else "cfg2", 0, 1, 0)
 G.to(dev)
 hps = bench._HPS(2)
 torch.manual_seed(1)

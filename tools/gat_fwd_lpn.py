@@ -12,7 +12,7 @@ import bench  # noqa: E402
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
-docs, G, _ = bench.make_shard("cfg2", 0, 1, 0)
+docs, G, _, _ = bench.make_shard("cfg2", 0, 1, 0)
 G.to(dev)
 torch.manual_seed(0)
 stack = bench.Stack(0.1, 2).to(dev)

@@ -9,7 +9,7 @@ from hetersumgraph_amd.HiGraph import register_tfidf_table
 from hetersumgraph_amd.ops import gat_heads_table
 
 dev = torch.device("cuda", 0)
-docs, G, _ = bench.make_shard("cfg2", 0, 1, 0)
+docs, G, _, _ = bench.make_shard("cfg2", 0, 1, 0)
 G.to(dev)
 torch.manual_seed(0)
 stack = bench.Stack(0.1, 2).to(dev)

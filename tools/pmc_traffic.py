@@ -44,7 +44,7 @@ def run():
         a.copy_(b)
     torch.cuda.synchronize()
     del a, b
-    docs, G, _ = bench.make_shard("cfg2", 0, 1, 0)
+    docs, G, _, _ = bench.make_shard("cfg2", 0, 1, 0)
     G.to(dev)
     torch.manual_seed(0)
     stack = bench.Stack(0.1, 2).to(dev)
