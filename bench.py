@@ -33,7 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-FP32_MFMA_PEAK_TFLOPS = 157.3
+FP32_MFMA_PEAK_TFLOPS = 157.3  # v_mfma_f32_32x32x2_f32 dense (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
 
 
 def parse():
@@ -48,8 +49,10 @@ def parse():
     ap.add_argument("--dropout", type=float, default=0.1)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-docs", type=int, default=4, help="docs in the bounded CPU-baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-docs", type=int, default=0,
+                    help="docs in the CPU-baseline sample (0: the whole per-GPU batch)")
+    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--kernel-steps", type=int, default=10, help="eager steps of the in-step kernel timing")
     ap.add_argument("--kernel-reps", type=int, default=50)
     ap.add_argument("--no-e2e", action="store_true", help="skip the secondary end-to-end train-step line")
     ap.add_argument("--e2e-steps", type=int, default=10)
@@ -173,73 +176,98 @@ class Stack(torch.nn.Module):
         return s
 
 
-def algorithmic_bytes_fwd(rel, H, D):
-    """Compulsory HBM bytes of one hsg_gat_fwd launch: read Z, sigma
-    (n_src rows), CSR + box (int32 + uint8 per edge), phantom, origin; write h, out,
-    m, l."""
-    HD = H * D
-    return (4 * rel.n_src * (HD + H) + 4 * (rel.n_dst + 1) + 5 * rel.n_typed + 4 * rel.n_dst
-            + 3 * 4 * rel.n_dst * HD + 8 * rel.n_dst * H)
+# ------------------------------------------------------------------ roofline --
+def edge_bytes_fwd(rel, H, D):
+    """SURVEY §8(d) compulsory HBM bytes of one edge forward (hsg_gat_fwd) with
+    D = H*D the concatenated width: read Z and sigma (n_src rows), the CSR offsets
+    and phantom counts (8 B / destination), 5 B per typed edge (int32 source +
+    uint8 tf box), write the aggregate and the softmax state m, l (2H)."""
+    W = H * D
+    return 4 * rel.n_src * (W + H) + 8 * rel.n_dst + 4 + 5 * rel.n_typed + 4 * rel.n_dst * (W + 2 * H)
 
 
-def time_fwd_kernel(G, stack, Xw, Xs, reps):
-    """Average duration of the dominant edge kernel (S2W hsg_gat_fwd), HIP events
-    recorded on the stream the kernel is launched on."""
-    import ctypes
-    from hetersumgraph_amd import _lib
-    from hetersumgraph_amd.module.GATLayer import edge_tau
-    lib = _lib.load()
-    rel = G.relation("S2W")
-    layer = stack.sent2word.layer
-    H, D = layer.num_heads, layer.head_dim
-    with torch.no_grad():
-        W, attn, wf, bf = layer.fused_params()
-        a1, a3 = attn[:, :D], attn[:, 2 * D:]
-        Z = torch.nn.functional.linear(Xs, W).contiguous()
-        tau, mode = edge_tau(G, rel, a3, wf, bf)
-        sigma = Z.new_empty(rel.n_src, H)
-        h = Xw.new_empty(rel.n_dst, H * D)
-        out = torch.empty_like(h)
-        m = Z.new_empty(rel.n_dst, H)
-        l = Z.new_empty(rel.n_dst, H)
-        st = torch.cuda.current_stream()
-        relp = ctypes.byref(rel.cstruct())
-        _lib.check(lib.hsg_attn_src_logits(rel.n_src, H, D, Z.data_ptr(), a1.contiguous().data_ptr(),
-                                           sigma.data_ptr(), st.cuda_stream), "sigma")
-        args = (relp, H, D, mode, 0.01, Z.data_ptr(), sigma.data_ptr(), tau.contiguous().data_ptr(),
-                Xw.data_ptr(), h.data_ptr(), out.data_ptr(), m.data_ptr(), l.data_ptr(), st.cuda_stream)
-        for _ in range(5):
-            _lib.check(lib.hsg_gat_fwd(*args), "fwd")
-        ms_mean = _batched_ms(st, lambda: lib.hsg_gat_fwd(*args), reps)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-        torch.cuda.synchronize()
-        for e0, e1 in evs:
-            e0.record(st)
-            lib.hsg_gat_fwd(*args)
-            e1.record(st)
-        torch.cuda.synchronize()
-        ms = [e0.elapsed_time(e1) for e0, e1 in evs]
-    return ms_mean, float(np.median(ms)), algorithmic_bytes_fwd(rel, H, D)
+def edge_bytes_bwd(rel, H, D):
+    """SURVEY §8(d) compulsory bytes of one edge backward (dst + src passes): read
+    dOut and the saved state, gather Z / write dZ and dsigma over the sources, the
+    CSR + CSC edge arrays (10 B / typed edge) and offsets."""
+    W = H * D
+    return (4 * (2 * rel.n_dst * W + 2 * rel.n_dst * H) + 8 * rel.n_src * (W + H) + 10 * rel.n_typed
+            + 8 * (rel.n_dst + rel.n_src) + 8)
 
 
-def _batched_ms(st, launch, reps):
-    """Average launch duration: ``reps`` back-to-back launches between two HIP events
-    on the launching stream (per-launch event pairs would add the event overhead to
-    every launch; this is the figure the rocprofv3 kernel-trace average checks)."""
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record(st)
-    for _ in range(reps):
-        launch()
-    e1.record(st)
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+def epilogue_bytes_fwd(rel, H, D):
+    """Bytes the fused forward moves beyond §8(d): the ELU + residual epilogue's
+    origin read (GAT.py:56-57; a separate elementwise kernel would read h and origin
+    and write out)."""
+    return 4 * rel.n_dst * H * D
+
+
+def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False):
+    """Per-step work items (name, bytes, flops, peak TFLOP/s) of the timed stack
+    (W2S + n_iter x (S2W, W2S), fwd + bwd) for the full-stack floor
+    sum_k max(B_k / BW, F_k / peak_k).  Dense bytes are the GEMM
+    operands and results (fp32); the FFN and head-projection flops are exact."""
+    dense_peak = BF16_MFMA_PEAK_TFLOPS if gemm_dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    items = []
+    layers = {"W2S": (rel_w, 300, 8, 8, 64), "S2W": (rel_s, 64, 6, 50, 300)}
+    apps = ["W2S"] + ["S2W", "W2S"] * n_iter
+    for i, kind in enumerate(apps):
+        rel, d_in, H, D, d = layers[kind]
+        HD = H * D
+        items.append((f"edge_fwd_{kind}", edge_bytes_fwd(rel, H, D), 0.0, None))
+        items.append((f"edge_bwd_{kind}", edge_bytes_bwd(rel, H, D), 0.0, None))
+        n = rel.n_src
+        proj = 2.0 * n * d_in * HD
+        nb_grad = word_grad or i > 0          # app 0's neighbour is the frozen word embedding
+        items.append((f"hproj_{kind}", 4.0 * (n * d_in + HD * d_in + n * HD) * (3 if nb_grad else 2),
+                      proj * (3 if nb_grad else 2), FP32_MFMA_PEAK_TFLOPS))
+        m, dh = rel.n_dst, 512
+        # W2S (d = 64) FFN stays fp32 in every mode (one-launch kernel)
+        peak = FP32_MFMA_PEAK_TFLOPS if kind == "W2S" else dense_peak
+        ffn = 2.0 * m * d * dh
+        items.append((f"ffn_{kind}", 4.0 * (m * d + m * dh) * 2 * 3, 6 * ffn, peak))
+    return items
+
+
+def full_stack_floor(items):
+    """(floor seconds, edge-floor s, dense-floor s, dense GFLOP)."""
+    edge = sum(b / (HBM_PEAK_GBS * 1e9) for _, b, f, _ in items if f == 0)
+    dense = sum(max(b / (HBM_PEAK_GBS * 1e9), f / (pk * 1e12)) for _, b, f, pk in items if f > 0)
+    return edge + dense, edge, dense, sum(f for _, _, f, _ in items) / 1e9
+
+
+def time_edge_kernels_in_step(step, zero, n_steps):
+    """Average duration of every edge-kernel launch INSIDE eager training steps:
+    HIP events on the launching stream around each hsg_gat_fwd and each
+    (hsg_gat_bwd_dst + hsg_gat_bwd_src) pair (hetersumgraph_amd._lib.KernelClock),
+    so each launch runs with the caches its real predecessors in the step leave.
+    Returns tag -> (mean ms, launches per step)."""
+    from hetersumgraph_amd._lib import KernelClock
+    with KernelClock() as clk:
+        for _ in range(n_steps):
+            zero()
+            step()
+        d = clk.durations_ms()
+    return {t: (float(np.mean(v)), len(v) / n_steps) for t, v in d.items()}
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
+    FETCH_SIZE / WRITE_SIZE passes over in-step launches (tools/pmc_traffic.py), or
+    None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+            return d["traffic_bytes"], os.path.relpath(path, ROOT), d
+    except (OSError, KeyError, ValueError):
+        return None, None, None
 
 
 def time_dense_kernel(stack, n_rows, reps):
-    """Average duration of the dominant dense kernel: the S2W FFN first GEMM
-    (x W1^T + b1, ReLU; [n_w, 300] x [300, 512]) on the stack's own weights, HIP
-    events on the launching stream.  Returns (ms, flops per launch)."""
+    """Average duration of the S2W FFN first GEMM (x W1^T + b1, ReLU;
+    [n_w, 300] x [300, 512]) on the stack's own weights, back-to-back launches
+    between HIP events on the launching stream.  Returns (ms, flops per launch)."""
     from hetersumgraph_amd.dense import gemm
     ffn = stack.sent2word.ffn
     w1, b1 = ffn.w_1.weight.detach().squeeze(-1).contiguous(), ffn.w_1.bias.detach()
@@ -248,31 +276,44 @@ def time_dense_kernel(stack, n_rows, reps):
     st = torch.cuda.current_stream()
     for _ in range(5):
         gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
-    ms = _batched_ms(st, lambda: gemm(x, w1, b_t=True, bias=b1, relu=True, out=out), reps)
-    return ms, 2.0 * n_rows * w1.shape[0] * w1.shape[1]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(st)
+    for _ in range(reps):
+        gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
+    e1.record(st)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, 2.0 * n_rows * w1.shape[0] * w1.shape[1]
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3
-    FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# ------------------------------------------------------------- CPU baseline --
+def cpu_threads():
+    """(threads to use, host cores visible): every core this process may run on --
+    the affinity mask, capped by the cgroup CPU quota when one is set (a container's
+    CPU share; more threads than the quota only time-slice)."""
+    visible = len(os.sched_getaffinity(0))
+    quota = None
     try:
-        with open(path) as fh:
-            return json.load(fh)["traffic_bytes"], os.path.relpath(path, ROOT)
-    except (OSError, KeyError, ValueError):
-        return None, None
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return (min(visible, quota) if quota else visible), visible, quota
 
 
-def cpu_baseline(docs_all, args, stack):
-    """The DGL-UDF-structured CPU port (oracle/dgl_udf.py) on a bounded sample of
-    the same workload, on this host's cores."""
+def cpu_baseline(docs, args, stack):
+    """The DGL-UDF-structured CPU port (oracle/dgl_udf.py) on the same workload's
+    documents, on every core this process may use; median of ``--cpu-steps``
+    fwd+bwd steps after one warm-up.  ``--cpu-docs`` (default: all of this rank's
+    documents) bounds the sample."""
     from oracle import dgl_udf, fused
-    cores = len(os.sched_getaffinity(0))
-    threads = min(cores, 16)
+    threads, visible, quota = cpu_threads()
     torch.set_num_threads(threads)
-    docs = docs_all[: args.cpu_docs]
-    offs = np.cumsum([0] + [d.n_nodes for d in docs])
-    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
+    n_docs = len(docs) if args.cpu_docs <= 0 else min(args.cpu_docs, len(docs))
+    sample = docs[:n_docs]
+    offs = np.cumsum([0] + [d.n_nodes for d in sample])
+    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(sample, offs[:-1])])
     g = dgl_udf.UdfGraph(cat(lambda d, o: d.src + o), cat(lambda d, o: d.dst + o), cat(lambda d, o: d.unit),
                          cat(lambda d, o: d.tffrac), cat(lambda d, o: d.edtype))
     n_w, n_s = int((g.unit == 0).sum()), int((g.unit == 1).sum())
@@ -290,15 +331,19 @@ def cpu_baseline(docs_all, args, stack):
         s.sum().backward()
 
     step()  # warm-up
-    t0 = time.perf_counter()
+    times = []
     for _ in range(args.cpu_steps):
+        t0 = time.perf_counter()
         step()
-    dt = (time.perf_counter() - t0) / args.cpu_steps
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
     return {"value": E / dt, "unit": "graph-edges/s", "cores": threads, "kind": "port",
-            "sample": f"{args.cpu_docs} of the {len(docs_all)} {args.config} docs ({E} edges), "
-                      f"{args.cpu_steps} fwd+bwd steps of the same stack, fp32, torch CPU, "
-                      f"{cpu_model()}; oracle/dgl_udf.py (DGL-0.4 UDF structure)",
-            "ms_per_step": dt * 1e3}
+            "host_cores_visible": visible, "cgroup_cpu_quota": quota,
+            "sample": f"{n_docs} of the {len(docs)} {args.config} docs of this GPU's batch ({E} of "
+                      f"{sum(len(d.src) for d in docs)} graph edges), median of {args.cpu_steps} fwd+bwd steps "
+                      f"of the same stack (W2S + {args.n_iter}x(S2W, W2S), train mode), fp32, torch CPU on "
+                      f"{threads} threads, {cpu_model()}; oracle/dgl_udf.py (DGL-0.4 UDF structure)",
+            "ms_per_step": dt * 1e3, "step_ms_all": [t * 1e3 for t in times]}
 
 
 def main():
@@ -416,11 +461,27 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = E_global / (dt / args.steps)
 
-    # dominant edge kernel: average launch duration with HIP events on its stream
-    k_ms_mean, k_ms_med, k_bytes = time_fwd_kernel(G, stack, Xw.detach(), Xs.detach(), args.kernel_reps)
-    achieved = k_bytes / (k_ms_mean * 1e-3) / 1e9
-    # the committed PMC passes are of the cfg2 launch: quoted for cfg2 only
-    traffic, traffic_src = pmc_traffic() if args.config == "cfg2" else (None, None)
+    # edge kernels timed inside eager steps (HIP events on their stream), after the
+    # timed region so they cannot perturb it
+    kt = time_edge_kernels_in_step(step, zero, args.kernel_steps)
+    Hs, Ds = stack.sent2word.layer.num_heads, stack.sent2word.layer.head_dim
+    Hw, Dw = stack.word2sent.layer.num_heads, stack.word2sent.layer.head_dim
+    shapes = {"S2W": (rel_s, Hs, Ds), "W2S": (rel_w, Hw, Dw)}
+    k_ms = kt[("gat_fwd", "S2W")][0]
+    k_bytes = edge_bytes_fwd(rel_s, Hs, Ds)
+    achieved = k_bytes / (k_ms * 1e-3) / 1e9
+    e_bytes = e_ms = 0.0
+    edge_rows = {}
+    for (what, kind), (ms, per_step) in sorted(kt.items()):
+        rel, H, D = shapes[kind]
+        b = (edge_bytes_fwd if what == "gat_fwd" else edge_bytes_bwd)(rel, H, D)
+        e_bytes += b * per_step
+        e_ms += ms * per_step
+        edge_rows[f"{what}_{kind}"] = {"avg_launch_us": ms * 1e3, "launches_per_step": per_step,
+                                       "bytes_per_launch": b, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    traffic, traffic_src, traffic_rec = pmc_traffic() if args.config == "cfg2" else (None, None, None)
+    items = step_work(rel_w, rel_s, args.n_iter, args.dtype)
+    floor_s, edge_floor_s, dense_floor_s, gflop = full_stack_floor(items)
     d_ms, d_flops = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
     d_tf = d_flops / (d_ms * 1e-3) / 1e12
 
@@ -449,14 +510,30 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": k_bytes, "avg_launch_us": k_ms_mean * 1e3,
-                     "median_launch_us_event_pairs": k_ms_med * 1e3},
+                     "algorithmic_bytes_per_launch": k_bytes,
+                     "bytes_formula": "SURVEY 8(d) B_f = 4 n_src (HD+H) + 8 n_dst + 4 + 5 E_T + 4 n_dst (HD+2H)",
+                     "epilogue_bytes_per_launch": epilogue_bytes_fwd(rel_s, Hs, Ds),
+                     "avg_launch_us": k_ms * 1e3,
+                     "timing": f"HIP events around each launch on its stream inside {args.kernel_steps} eager "
+                               "training steps (in-step cache state); cross-check: rocprofv3 kernel trace "
+                               "of the same command under profiles/"},
+        "edge_aggregate": {"bytes_per_step": e_bytes, "time_us_per_step": e_ms * 1e3,
+                           "achieved": e_bytes / (e_ms * 1e-3) / 1e9, "unit": "GB/s",
+                           "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernels": edge_rows},
+        "full_stack": {"floor_us": floor_s * 1e6, "edge_floor_us": edge_floor_s * 1e6,
+                       "dense_floor_us": dense_floor_s * 1e6, "dense_gflop_per_step": gflop,
+                       "frac": floor_s / (ms_per_step * 1e-3),
+                       "formula": "sum_k max(B_k/8 TB/s, F_k/peak_k) / t_step over the step's edge, head-"
+                                  "projection and FFN work (bench.step_work)"},
         "roofline_dense": {"kernel": "hsg_gemm_f32 (S2W FFN x W1^T + b1, ReLU; "
                                      f"{rel_s.n_dst}x300 @ 300x512)", "bound": "mfma",
                            "achieved": d_tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": d_tf / FP32_MFMA_PEAK_TFLOPS, "flops_per_launch": d_flops,
                            "avg_launch_us": d_ms * 1e3},
     }
+    if traffic_rec is not None:
+        out["roofline"]["traffic_detail"] = {k: traffic_rec[k] for k in ("fetch_bytes", "write_bytes", "launches")
+                                             if k in traffic_rec}
     if world == 1 and not args.no_e2e:
         try:
             dt = time_train_step(G, args.config, args.n_iter, args.e2e_steps, 3, dev)

@@ -135,3 +135,42 @@ def check(rc: int, what: str):
 
 def version() -> str:
     return load().hsg_version().decode()
+
+
+class KernelClock:
+    """In-step kernel timing for bench.py: while a clock is active (``with
+    KernelClock() as clk``), tagged launches are bracketed by HIP events recorded on
+    the launching stream, inside an ordinary (eager) training step -- so each
+    kernel runs after the step's real predecessors, with the caches they leave.
+    Off (the default), the hook costs one global read per launch."""
+
+    def __init__(self):
+        self.events = {}
+
+    def __enter__(self):
+        global CLOCK
+        CLOCK = self
+        return self
+
+    def __exit__(self, *exc):
+        global CLOCK
+        CLOCK = None
+
+    def start(self, tag, device):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream(device))
+        return (tag, e)
+
+    def stop(self, token, device):
+        tag, e0 = token
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream(device))
+        self.events.setdefault(tag, []).append((e0, e1))
+
+    def durations_ms(self):
+        """tag -> list of per-launch durations (ms); synchronises."""
+        torch.cuda.synchronize()
+        return {t: [a.elapsed_time(b) for a, b in evs] for t, evs in self.events.items()}
+
+
+CLOCK = None

@@ -21,6 +21,16 @@ import torch
 
 from . import _lib
 from ._lib import HSG_TAU_PER_EDGE, HSG_TAU_TABLE, check, load, ptr, stream_of
+
+
+def _clock_start(tag, t):
+    clk = _lib.CLOCK
+    return None if clk is None else clk.start(tag, t.device)
+
+
+def _clock_stop(tok, t):
+    if tok is not None:
+        _lib.CLOCK.stop(tok, t.device)
 from .relation import N_BOX
 
 LEAKY_SLOPE = 0.01   # F.leaky_relu default (GATLayer.py:92, 131)
@@ -131,8 +141,10 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         out = Z.new_empty(n_dst, HD)
     m = Z.new_empty(n_dst, H)
     l = Z.new_empty(n_dst, H)
+    tok = _clock_start(("gat_fwd", rel.kind), Z)
     check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
                           ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+    _clock_stop(tok, Z)
     saved = (Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, origin is not None)
     return (out if origin is not None else h), saved
 
@@ -154,15 +166,17 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     dpre = Z.new_empty(rel.n_typed, H)
     nbd = lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
-    check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
-                              ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                              ptr(dtp), st), "hsg_gat_bwd_dst")
     dZt = torch.empty_like(Z)
     nbs = lib.hsg_gat_bwd_src_blocks(relp)
     da1p = Z.new_empty(nbs, H * D)
+    tok = _clock_start(("gat_bwd", rel.kind), Z)
+    check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
+                              ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                              ptr(dtp), st), "hsg_gat_bwd_dst")
     check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
                               ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
           "hsg_gat_bwd_src")
+    _clock_stop(tok, Z)
     if stage is not None:
         ws, acc = stage
         check(lib.hsg_attn_params_stage(H, D, nbd, ptr(dtp), nbs, ptr(da1p), ptr(ws), int(bool(acc)), st),

@@ -1,0 +1,43 @@
+"""bench.py's roofline arithmetic against SURVEY §8(d)'s published figures for
+config 2 (CPU only: relation sizes from the oracle's host-side restatement)."""
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def cfg2_rels():
+    from types import SimpleNamespace
+    from hetersumgraph_amd import synth
+    from oracle import fused
+    docs = synth.make_batch_docs("cfg2", seed=0)
+    offs = np.cumsum([0] + [d.n_nodes for d in docs])
+    cat = lambda f: np.concatenate([f(d, o) for d, o in zip(docs, offs[:-1])])
+    src, dst, unit = cat(lambda d, o: d.src + o), cat(lambda d, o: d.dst + o), cat(lambda d, o: d.unit)
+    tf, et = cat(lambda d, o: d.tffrac), cat(lambda d, o: d.edtype)
+    rels = [fused.typed_relation(k, src, dst, unit, tf, et) for k in ("W2S", "S2W")]
+    return [SimpleNamespace(n_src=r["n_src"], n_dst=r["n_dst"], n_typed=len(r["e_src"])) for r in rels]
+
+
+def test_edge_bytes_match_survey(cfg2_rels):
+    import bench
+    rw, rs = cfg2_rels
+    assert (rw.n_src, rw.n_dst, rw.n_typed) == (19200, 1120, 40320)
+    mb = lambda b: round(b / 1e6, 2)
+    assert mb(bench.edge_bytes_fwd(rw, 8, 8)) == 6.10
+    assert mb(bench.edge_bytes_bwd(rw, 8, 8)) == 12.27
+    assert mb(bench.edge_bytes_fwd(rs, 6, 50)) == 25.69
+    assert mb(bench.edge_bytes_bwd(rs, 6, 50)) == 50.31
+    step = 3 * (bench.edge_bytes_fwd(rw, 8, 8) + bench.edge_bytes_bwd(rw, 8, 8)) + \
+        2 * (bench.edge_bytes_fwd(rs, 6, 50) + bench.edge_bytes_bwd(rs, 6, 50))
+    assert round(step / 1e6, 1) == 207.1
+
+
+def test_full_stack_floor(cfg2_rels):
+    """Dense work ≈79 GFLOP per step at cfg2 (>= 0.50 ms at the f32 peak)."""
+    import bench
+    rw, rs = cfg2_rels
+    items = bench.step_work(rw, rs, 2, "f32")
+    floor, edge, dense, gflop = bench.full_stack_floor(items)
+    assert 74 <= gflop <= 80
+    assert 0.45e-3 <= dense <= 0.52e-3
+    assert abs(edge - 207.1e6 / 8e12) < 1e-7

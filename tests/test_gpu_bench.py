@@ -31,7 +31,8 @@ def test_bench_json_contract(tmp_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1",
-                          "--no-e2e", "--cpu-docs", "1", "--cpu-steps", "1", "--kernel-reps", "5"],
+                          "--no-e2e", "--cpu-docs", "1", "--cpu-steps", "1", "--kernel-reps", "5",
+                          "--kernel-steps", "2"],
                          cwd=root, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
@@ -45,5 +46,11 @@ def test_bench_json_contract(tmp_path):
     r = d["roofline"]
     assert r["bound"] == "hbm" and r["unit"] == "GB/s" and 0 < r["frac"] < 1
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
+    assert r["algorithmic_bytes_per_launch"] < r["algorithmic_bytes_per_launch"] + r["epilogue_bytes_per_launch"]
+    e = d["edge_aggregate"]
+    assert 0 < e["frac"] < 1 and set(e["kernels"]) == {"gat_fwd_W2S", "gat_fwd_S2W", "gat_bwd_W2S", "gat_bwd_S2W"}
+    assert e["kernels"]["gat_fwd_S2W"]["launches_per_step"] == 2 and e["kernels"]["gat_fwd_W2S"]["launches_per_step"] == 3
+    f = d["full_stack"]
+    assert 0 < f["frac"] < 1 and f["floor_us"] > f["dense_floor_us"] > 0
     c = d["cpu_baseline"]
-    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0
+    assert c["kind"] == "port" and c["cores"] >= 1 and c["value"] > 0 and c["host_cores_visible"] >= c["cores"]
