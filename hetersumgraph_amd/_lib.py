@@ -21,7 +21,7 @@ HSG_TAU_PER_EDGE = 1
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
            "hsg_gat_bwd_src_blocks", "hsg_attn_src_logits", "hsg_attn_params_fwd", "hsg_attn_params_bwd",
-           "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_bf16", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_ffn_colsums",
+           "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_f32_mfma", "hsg_gemm_bf16", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_ffn_colsums",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
            "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
@@ -66,6 +66,7 @@ _SIGS = {
     "hsg_version": [],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_bf16": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
+    "hsg_gemm_f32_mfma": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_row_tiles": [_I, _I, _I, _I],
     "hsg_ffn_colsums": [_I, _I, _P, _P, _I, _I, _P, _P, _P, _P, _I, _P],
     "hsg_gemm_workspace_floats": [_I, _I, _I, _I],

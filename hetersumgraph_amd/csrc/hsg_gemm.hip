@@ -25,6 +25,18 @@
 // fragments are read from LDS, v_mfma_f32_32x32x16_bf16 with fp32 accumulation.
 // Split-K (grid.z > 1) writes fp32 partial slabs, reduced (with the epilogue) by
 // k_splitk_reduce in split order -> deterministic.
+//
+// k_gemm3 (hsg_gemm_f32's default path): fp32 operands, fp32-ACCURATE products on the
+// bf16 matrix cores.  Each operand element is split into three bf16 limbs,
+// x = x0 + x1 + x2 (x0 = RNE(x), x1 = RNE(x - x0), x2 = RNE(x - x0 - x1); both
+// differences are exact in fp32), when its tile is staged into LDS, and
+// sum_k a*b is accumulated in fp32 from the six limb products whose order is
+// <= 2^-16 relative (a0b0, a0b1, a1b0, a0b2, a1b1, a2b0; bf16 x bf16 products are
+// exact in fp32).  The dropped terms (a1b2, a2b1, a2b2, and the limb residual) are
+// <= ~3 * 2^-24 of |a b|: the error class of an fp32 fmaf chain (measured against
+// fp64 in tests/test_gpu_gemm.py).  Six v_mfma_f32_32x32x16_bf16 (32 cycles each)
+// replace eight v_mfma_f32_32x32x2_f32 (64 cycles) per 16-deep k step: a 2.67x
+// higher MFMA ceiling than the exact-f32 instruction (gfx950 has no xf32).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -371,6 +383,244 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
 #endif
 }
 
+// ------------------------------------------------- 3-limb bf16 split (k_gemm3) --
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// bf16 per LDS row of a limb plane: BK k + 8 pad (row stride 16 B mod 64: the 16-lane
+// ds_read_b128 groups hit 64 distinct banks)
+template <int BK> struct Ldh { static constexpr int v = BK + 8; };
+
+__device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &x2) {
+    x0 = (__bf16)x;                       // v_cvt_pk_bf16_f32, RNE
+    const float r = x - (float)x0;        // exact
+    x1 = (__bf16)r;
+    x2 = (__bf16)(r - (float)x1);         // exact difference, then RNE
+}
+
+// One operand tile for k_gemm3: ROWS (M or N) x BK (K) from global into registers,
+// then into NL bf16 limb planes [ROWS][BK + 8] in LDS (always k-contiguous, so the
+// MFMA fragments are single ds_read_b128s whatever the global layout).
+//   KC:  a thread covers (row, 4 consecutive k)            -> NL x ds_write_b64
+//   !KC: a thread covers (4 consecutive rows, 2 consecutive k) from two float4 loads
+//        of adjacent k rows (the transpose happens in registers) -> 4 NL x ds_write_b32
+template <bool KC, int ROWS, int BK, int NL>
+struct Stage3 {
+    static constexpr int LD = Ldh<BK>::v;
+    static constexpr int NU = KC ? ROWS * BK / 1024 : ROWS * BK / 2048;    // units per thread
+    f32x4 v[KC ? NU : 2 * NU];
+
+    __device__ __forceinline__ static f32x4 ld4(const float *__restrict__ g, int ld, int gr, int gc, int lim_r,
+                                                int lim_c) {
+        f32x4 x = {0.f, 0.f, 0.f, 0.f};
+        if (gr < lim_r) {
+            const float *src = g + (size_t)gr * ld + gc;
+            if (gc + 3 < lim_c) {
+                x = *reinterpret_cast<const f32x4 *>(src);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (gc + e < lim_c) x[e] = src[e];
+            }
+        }
+        return x;
+    }
+
+    __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int r0, int nr, int k0, int nk) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            if constexpr (KC) {
+                const int row = idx / (BK / 4), col = (idx % (BK / 4)) * 4;
+                v[i] = ld4(g, ld, r0 + row, k0 + col, nr, nk);
+            } else {
+                const int rq = idx % (ROWS / 4), kp = idx / (ROWS / 4);
+                v[2 * i] = ld4(g, ld, k0 + 2 * kp, r0 + 4 * rq, nk, nr);
+                v[2 * i + 1] = ld4(g, ld, k0 + 2 * kp + 1, r0 + 4 * rq, nk, nr);
+            }
+        }
+    }
+
+    __device__ __forceinline__ void store(__bf16 (*s)[ROWS * LD]) const {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int idx = threadIdx.x + 256 * i;
+            if constexpr (KC) {
+                const int row = idx / (BK / 4), col = (idx % (BK / 4)) * 4;
+                bf16x4 x0, x1, x2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (NL == 3) {
+                        __bf16 a, b, c;
+                        split3(v[i][e], a, b, c);
+                        x0[e] = a; x1[e] = b; x2[e] = c;
+                    } else {
+                        x0[e] = (__bf16)v[i][e];
+                    }
+                }
+                const int o = row * LD + col;
+                *reinterpret_cast<bf16x4 *>(&s[0][o]) = x0;
+                if constexpr (NL == 3) {
+                    *reinterpret_cast<bf16x4 *>(&s[1][o]) = x1;
+                    *reinterpret_cast<bf16x4 *>(&s[2][o]) = x2;
+                }
+            } else {
+                const int rq = idx % (ROWS / 4), kp = idx / (ROWS / 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bf16x2 x0, x1, x2;
+#pragma unroll
+                    for (int q = 0; q < 2; ++q) {
+                        if constexpr (NL == 3) {
+                            __bf16 a, b, c;
+                            split3(v[2 * i + q][e], a, b, c);
+                            x0[q] = a; x1[q] = b; x2[q] = c;
+                        } else {
+                            x0[q] = (__bf16)v[2 * i + q][e];
+                        }
+                    }
+                    const int o = (4 * rq + e) * LD + 2 * kp;
+                    *reinterpret_cast<bf16x2 *>(&s[0][o]) = x0;
+                    if constexpr (NL == 3) {
+                        *reinterpret_cast<bf16x2 *>(&s[1][o]) = x1;
+                        *reinterpret_cast<bf16x2 *>(&s[2][o]) = x2;
+                    }
+                }
+            }
+        }
+    }
+};
+
+// Block = 256 threads (2x2 waves), tile BM x BN x BK, one LDS buffer of limb planes;
+// the next PF K tiles are prefetched into registers (PF = 2: the loads of tile kt+2
+// are issued while tile kt is multiplied, two tiles of MFMA work to hide their
+// latency).  Two barriers per K tile.  NL = 1 is a bf16-operand probe of the same
+// pipeline (dev only).  The epilogue (and split-K / column partials) is k_gemm's.
+template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL>
+__global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
+    constexpr int LD = Ldh<BK>::v;
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    __shared__ __attribute__((aligned(16))) __bf16 sA[NL][BM * LD];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[NL][BN * LD];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int li = lane & 31, h = lane >> 5;
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_mn = tiles_n * tiles_m;
+    const int kt_total = (p.K + BK - 1) / BK;
+    const int total = tiles_mn * p.splits;
+    Stage3<AK, BM, BK, NL> ra[PF];
+    Stage3<BKC, BN, BK, NL> rb[PF];
+    for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    const int lt = p.xcd ? xcd_tile(t, total) : t;
+    const int tx = lt % tiles_n, ty = (lt / tiles_n) % tiles_m, tz = lt / tiles_mn;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int kt0 = tz * p.k_tiles_per_split;
+    const int kt1 = min(kt_total, kt0 + p.k_tiles_per_split);
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+        if (kt0 + q < kt1) {
+            ra[q].load(p.A, p.lda, m0, p.M, (kt0 + q) * BK, p.K);
+            rb[q].load(p.B, p.ldb, n0, p.N, (kt0 + q) * BK, p.K);
+        }
+    for (int kt = kt0; kt < kt1; kt += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+        const int k = kt + q;
+        if (k >= kt1) break;
+        __syncthreads();                      // every wave is done with the previous tile
+        ra[q].store(sA);
+        rb[q].store(sB);
+        __syncthreads();
+        if (k + PF < kt1) {                   // tile k+PF's loads overlap the next PF tiles' MFMAs
+            ra[q].load(p.A, p.lda, m0, p.M, (k + PF) * BK, p.K);
+            rb[q].load(p.B, p.ldb, n0, p.N, (k + PF) * BK, p.K);
+        }
+#pragma unroll
+        for (int s16 = 0; s16 < BK / 16; ++s16) {
+            bf16x8 a[NL][TM], b[NL][TN];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    a[l][i] = *reinterpret_cast<const bf16x8 *>(
+                        &sA[l][(wm * WM + i * 32 + li) * LD + 16 * s16 + 8 * h]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    b[l][j] = *reinterpret_cast<const bf16x8 *>(
+                        &sB[l][(wn * WN + j * 32 + li) * LD + 16 * s16 + 8 * h]);
+            }
+            // smallest limb products first, a0*b0 last
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (NL == 3) {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+                    }
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+                }
+        }
+    }
+    }
+
+    // epilogue: lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
+    const bool split = p.splits > 1;
+    float csum[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) csum[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WN + j * 32 + li;
+            if (n >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m >= p.M) continue;
+                if (split) {
+                    p.ws[((size_t)tz * p.M + m) * p.N + n] = acc[i][j][r];
+                } else {
+                    const float v = epi_apply(acc[i][j][r], m, n, p);
+                    p.C[(size_t)m * p.ldc + n] = v;
+                    csum[j] += v;
+                }
+            }
+        }
+    if (p.colpart && !split) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
+        __syncthreads();
+        float *red = reinterpret_cast<float *>(&sA[0][0]);
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + li] = csum[j];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < BN; c += 256) {
+            const int n = n0 + c;
+            if (n < p.N) p.colpart[(size_t)ty * p.N + n] = red[c] + red[BN + c];
+        }
+    }
+    __syncthreads();                          // LDS is refilled by the next tile
+    }
+}
+
 // Sums the split slabs in split order (deterministic).  The slab loads are issued 8
 // at a time ahead of the adds, so a thread has 8 independent loads in flight instead
 // of one dependent load per split; the addition order is unchanged.
@@ -441,6 +691,33 @@ int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
+template <int BM, int BN, int BK = 32, int PF = 1, int NL = 3>
+int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
+    const int kt_total = (p.K + BK - 1) / BK;
+    p.k_tiles_per_split = (kt_total + splits - 1) / splits;
+    p.splits = splits;
+    long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
+    if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
+    dim3 grid((unsigned)g);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+// k_gemm3 tile plan: 0 = 64x64, 1 = 128x64, 2 = 64x128, 3 = 128x128 (measured on the
+// WSWGAT shapes, tools/gemm3_sweep.py: 64x64 for narrow outputs and for N-aligned
+// K-contiguous weights, 128x64 otherwise; the wide tiles never won).  GEMMs that emit
+// column partials use 64-row tiles in every mode (hsg_gemm_row_tiles).
+int plan3(int M, int N, int K, int splits, bool colpart, bool bk) {
+    (void)M; (void)K; (void)splits;
+    if (colpart) return 0;
+    if (N <= 64 || (bk && N % 128 == 0)) return 0;
+    return 1;
+}
+
 // Plan: 64x64 tiles with a single LDS buffer (up to 8 resident blocks per CU)
 // measured fastest on the WSWGAT shapes except long-K tall GEMMs, where 128x64
 // single-buffer tiles amortise their prologue better (tools/gemm_tiles.py).
@@ -476,17 +753,17 @@ size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits) {
 }
 
 int hsg_gemm_row_tiles(int M, int N, int K, int splits) {
-    if (splits == 0) splits = plan_splits(M, N, K);
-    const int t = plan_tile(M, N, K, splits < 1 ? 1 : splits);
-    const int bm = (t == 0 || t == 1 || t == 3 || t == 4 || t == 7 || t == 9) ? 128 : 64;
-    return (M + bm - 1) / bm;
+    (void)N; (void)K; (void)splits;
+    return (M + 63) / 64;            // GEMMs with column partials run 64-row tiles in every mode
 }
 
 }  // extern "C"
 
 namespace {
 
-int gemm_impl(bool bf16, int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+enum { MODE_F32_MFMA = 0, MODE_BF16 = 1, MODE_F32_SPLIT = 2 };
+
+int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
               int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
               int relu, int splits, float *workspace, float *colsum_part, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C) return HSG_EINVAL;
@@ -506,11 +783,36 @@ int gemm_impl(bool bf16, int M, int N, int K, const float *A, int lda, int a_kco
                (kt_total + splits - 1) / splits, workspace, colsum_part, splits, 1};
     if (const char *x = getenv("HSG_GEMM_XCD")) p.xcd = atoi(x);        // dev A/B switch
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
-    int best = plan_tile(M, N, K, splits);
+    int best = colsum_part ? 5 : plan_tile(M, N, K, splits);     // column partials: 64-row tiles
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
         if (!colsum_part) best = atoi(f);
     int rc;
-    if (bf16) {
+    // both operands M/N-contiguous (the weight gradients dW = dY^T X): the in-register
+    // transposes of the split staging cost more than the MFMA saves -> exact-f32 MFMA
+    if (mode == MODE_F32_SPLIT && !ak && !bk && !getenv("HSG_GEMM3_TILE")) mode = MODE_F32_MFMA;
+    if (mode == MODE_F32_SPLIT) {
+        int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
+        if (const char *f = getenv("HSG_GEMM3_TILE"))      // dev override
+            if (!colsum_part) t3 = atoi(f);
+        int var = 0;                                        // dev variants (tools/gemm3_sweep.py)
+        if (const char *f = getenv("HSG_GEMM3_VAR")) var = atoi(f);
+        if (var == 1) {                                     // 2-deep register prefetch
+            if (t3 == 1) rc = launch3<128, 64, 32, 2>(p, ak, bk, splits, st);
+            else rc = launch3<64, 64, 32, 2>(p, ak, bk, splits, st);
+        } else if (var == 2) {                              // BK = 64
+            if (t3 == 1) rc = launch3<128, 64, 64, 1>(p, ak, bk, splits, st);
+            else rc = launch3<64, 64, 64, 1>(p, ak, bk, splits, st);
+        } else if (var == 3) {                              // one limb (bf16 probe, not f32-accurate)
+            if (t3 == 1) rc = launch3<128, 64, 32, 1, 1>(p, ak, bk, splits, st);
+            else rc = launch3<64, 64, 32, 1, 1>(p, ak, bk, splits, st);
+        } else if (var == 4) {                              // one limb, 2-deep prefetch
+            if (t3 == 1) rc = launch3<128, 64, 32, 2, 1>(p, ak, bk, splits, st);
+            else rc = launch3<64, 64, 32, 2, 1>(p, ak, bk, splits, st);
+        } else if (t3 == 3) rc = launch3<128, 128>(p, ak, bk, splits, st);
+        else if (t3 == 1) rc = launch3<128, 64>(p, ak, bk, splits, st);
+        else if (t3 == 2) rc = launch3<64, 128>(p, ak, bk, splits, st);
+        else rc = launch3<64, 64>(p, ak, bk, splits, st);
+    } else if (mode == MODE_BF16) {
         // bf16 operands: the two single-buffer plans (the K loop is load-bound, so the
         // deeper tiles of the f32 plan table do not pay)
         if (best == 4) rc = launch_tiles<128, 64, 1, kBK, true>(p, ak, bk, splits, st);
@@ -543,14 +845,24 @@ extern "C" {
 int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
                  int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
                  int relu, int splits, float *workspace, float *colsum_part, void *stream) {
-    return gemm_impl(false, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
+    int mode = MODE_F32_SPLIT;
+    if (const char *e = getenv("HSG_GEMM_F32"))          // dev A/B: "mfma" = exact-f32 instruction
+        if (e[0] == 'm') mode = MODE_F32_MFMA;
+    return gemm_impl(mode, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
+}
+
+int hsg_gemm_f32_mfma(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                      int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
+                      int relu, int splits, float *workspace, float *colsum_part, void *stream) {
+    return gemm_impl(MODE_F32_MFMA, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi,
+                     relu, splits, workspace, colsum_part, stream);
 }
 
 int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
                   int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
                   int relu, int splits, float *workspace, float *colsum_part, void *stream) {
-    return gemm_impl(true, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
+    return gemm_impl(MODE_BF16, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
 }
 

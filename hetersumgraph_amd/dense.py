@@ -5,10 +5,15 @@
 projection need (bias, ReLU, ReLU-backward mask, accumulate).  Everything is
 enqueued on the current stream; no host synchronisation.
 
-Operand precision: fp32 (hsg_gemm_f32, the default and the parity contract) or,
-for the bf16 configuration (config 5), fp32 storage with bf16-rounded
-MFMA operands and fp32 accumulation (hsg_gemm_bf16) -- chosen process-wide with
-:func:`set_gemm_dtype` / :func:`gemm_dtype` or ``HSG_GEMM_DTYPE=bf16``.
+Operand precision, chosen process-wide with :func:`set_gemm_dtype` /
+:func:`gemm_dtype` or ``HSG_GEMM_DTYPE``:
+* 'f32' (default, the parity contract): hsg_gemm_f32 -- fp32 operands and
+  fp32-accurate products from three bf16 limbs per operand (six limb products on
+  the bf16 matrix cores, fp32 accumulation; include/hsg.h);
+* 'f32mfma': hsg_gemm_f32_mfma -- the exact-f32 MFMA instruction (one fmaf rounding
+  per product), kept for A/B checks;
+* 'bf16' (config 5's reduced-precision mode): fp32 storage with
+  bf16-rounded operands and fp32 accumulation (hsg_gemm_bf16).
 """
 from __future__ import annotations
 
@@ -22,14 +27,16 @@ from ._lib import HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr
 
 
 _GEMM_DTYPE = os.environ.get("HSG_GEMM_DTYPE", "f32")
+_FNS = {"f32": "hsg_gemm_f32", "f32mfma": "hsg_gemm_f32_mfma", "bf16": "hsg_gemm_bf16"}
 
 
 def set_gemm_dtype(dtype):
-    """'f32' (exact fp32 MFMA) or 'bf16' (bf16 operands, fp32 accumulate) for every
-    GEMM issued through :func:`gemm` (FFN, sentence CNN)."""
+    """'f32' (fp32-accurate, 3-limb bf16 split), 'f32mfma' (exact-f32 instruction) or
+    'bf16' (bf16 operands, fp32 accumulate) for every GEMM issued through
+    :func:`gemm` (FFN, sentence CNN)."""
     global _GEMM_DTYPE
-    if dtype not in ("f32", "bf16"):
-        raise ValueError(f"gemm dtype must be 'f32' or 'bf16', not {dtype!r}")
+    if dtype not in _FNS:
+        raise ValueError(f"gemm dtype must be one of {sorted(_FNS)}, not {dtype!r}")
     _GEMM_DTYPE = dtype
 
 
@@ -60,10 +67,10 @@ def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=
     A [M,K] (or [K,M] with a_t), B [K,N] (or [N,K] with b_t), fp32 on the GPU.
     ``add`` may be ``out`` itself (accumulate).  ``colsum_part``: a tensor of
     ``row_tiles(M, N, K) * N`` floats that receives per-tile-row column sums of C
-    (unsplit GEMMs).  ``dtype``: 'f32' / 'bf16' operands (default: the process-wide
+    (unsplit GEMMs).  ``dtype``: 'f32' / 'f32mfma' / 'bf16' (default: the process-wide
     setting)."""
     lib = load()
-    fn = lib.hsg_gemm_bf16 if (dtype or _GEMM_DTYPE) == "bf16" else lib.hsg_gemm_f32
+    fn = getattr(lib, _FNS[dtype or _GEMM_DTYPE])
     if not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
         raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
     M, K = (A.shape[1], A.shape[0]) if a_t else (A.shape[0], A.shape[1])

@@ -133,9 +133,15 @@ int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const fl
                            int accumulate, void *stream);
 size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 
-/* ---- dense fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32) ---------------------------
+/* ---- dense fp32 GEMM on the matrix cores ---------------------------------------
  * Replaces the torch GEMMs of the head projection fc (GATLayer.py:110 / 146) and of
  * PositionwiseFeedForward (Conv1d k=1 = GEMM, GATLayer.py:39) plus their backward.
+ * hsg_gemm_f32: fp32 operands and result, fp32-accurate products computed as six
+ * bf16 limb products per element pair (each operand split into three bf16 limbs when
+ * its tile is staged; v_mfma_f32_32x32x16_bf16, fp32 accumulation; dropped terms
+ * <= ~3*2^-24 |a b|, the error class of an fp32 fmaf chain).
+ * hsg_gemm_f32_mfma: same contract on the exact-f32 instruction v_mfma_f32_32x32x2_f32
+ * (one fmaf rounding per product; 2.67x lower MFMA ceiling).
  *   C[m][n] = epi( sum_k A(m,k) B(k,n) )
  *   A(m,k) = a_kcontig ? A[m*lda+k] : A[k*lda+m];  B(k,n) = b_kcontig ? B[n*ldb+k] : B[k*ldb+n]
  * epi: HSG_EPI_STORE    v (+bias[n]) then relu if `relu`
@@ -158,6 +164,10 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
  * C, [hsg_gemm_row_tiles(M,N,K,splits)][N] -- e.g. the bias gradient of the FFN's
  * first layer taken from the dH epilogue instead of a second pass over dH. */
 int hsg_gemm_row_tiles(int M, int N, int K, int splits);
+int hsg_gemm_f32_mfma(int M, int N, int K, const float *A, int lda, int a_kcontig,
+                      const float *B, int ldb, int b_kcontig, float *C, int ldc,
+                      const float *bias, const float *aux, int ldaux, int epi, int relu,
+                      int splits, float *workspace, float *colsum_part, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,

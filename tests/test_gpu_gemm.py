@@ -1,5 +1,8 @@
-"""hsg_gemm_f32 (v_mfma_f32_32x32x2_f32) against an fp64 torch reference: every
-operand layout, ragged shapes, each epilogue, split-K."""
+"""hsg_gemm_f32 (fp32-accurate 3-limb bf16 split on v_mfma_f32_32x32x16_bf16) and
+hsg_gemm_f32_mfma (exact-f32 v_mfma_f32_32x32x2_f32) against an fp64 torch
+reference: every operand layout, ragged shapes, each epilogue, split-K, and the
+split path's error class (per element, in units of sum_k |a||b|, no worse than
+the exact-f32 instruction's)."""
 import pytest
 import torch
 
@@ -23,12 +26,13 @@ def mk(rows, cols):
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("a_t,b_t", [(False, False), (False, True), (True, False), (True, True)])
-def test_layouts(M, N, K, a_t, b_t):
+@pytest.mark.parametrize("dtype", ["f32", "f32mfma"])
+def test_layouts(M, N, K, a_t, b_t, dtype):
     from hetersumgraph_amd.dense import gemm
     torch.manual_seed(M + N + K)
     A = mk(K, M) if a_t else mk(M, K)
     B = mk(N, K) if b_t else mk(K, N)
-    C = gemm(A, B, a_t, b_t)
+    C = gemm(A, B, a_t, b_t, dtype=dtype)
     R = ref(A, B, a_t, b_t)
     err = (C.double() - R).abs().max().item()
     assert err <= 1e-5 * max(1.0, K ** 0.5) * 4, err
@@ -131,3 +135,26 @@ def test_bf16_epilogue_and_split_k():
     Hr = torch.relu(bf16_ref(X, W, False, True) + b.double())
     assert (H.double() - Hr).abs().max().item() < 1e-4
     assert (C.double() - bf16_ref(A, B, True, False)).abs().max().item() < 2e-3
+
+
+@pytest.mark.parametrize("M,N,K,a_t,b_t", [(19200, 512, 300, False, True), (19200, 300, 512, False, True),
+                                           (19200, 512, 300, False, False), (4000, 300, 512, False, False),
+                                           (777, 64, 300, False, True), (3000, 1350, 300, False, True)])
+def test_split_is_fp32_class(M, N, K, a_t, b_t):
+    """Per output element, |C - C_fp64| / sum_k |a_k b_k| of the 3-limb split path is
+    within 1.5x of the exact-f32 instruction's and below 2e-6 (fp32 unit roundoff is
+    6e-8 per rounding), on operands with a wide dynamic range."""
+    from hetersumgraph_amd.dense import gemm
+    torch.manual_seed(K)
+    A = (mk(K, M) if a_t else mk(M, K)) * torch.exp(2 * torch.randn(1, device="cuda"))
+    B = mk(N, K) if b_t else mk(K, N)
+    A = A * torch.exp(torch.randn_like(A))               # entries spread over many binades
+    a64 = (A.t() if a_t else A).double()
+    b64 = (B.t() if b_t else B).double()
+    ref, unit = a64 @ b64, a64.abs() @ b64.abs()
+    e = {}
+    for dt in ("f32", "f32mfma"):
+        C = gemm(A, B, a_t, b_t, dtype=dt)
+        e[dt] = ((C.double() - ref).abs() / unit).max().item()
+    print(f"{M}x{N}x{K}: split {e['f32']:.2e}, f32 mfma {e['f32mfma']:.2e}")
+    assert e["f32"] <= 1.5 * e["f32mfma"] + 1e-8 and e["f32"] < 2e-6
