@@ -42,6 +42,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 __device__ __forceinline__ float leaky(float x, float slope) { return x > 0.f ? x : x * slope; }
 
+// F.elu (GAT.py:56): x for x > 0, else exp(x) - 1 on v_exp_f32.  Absolute error
+// <= ~2e-7 against expm1 (the reference's elu), far inside the 1e-5 fp64 parity
+// bound; 4 VALU instead of the ~30 of a libm expm1f.
+__device__ __forceinline__ float elu1(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+
+// f / D for 0 <= f < 2^12, D >= 1, without an integer division: (f + 0.5) / D sits
+// at least 0.5 / D away from the next integer, far more than the float rounding.
+__device__ __forceinline__ int div_small(int f, float inv_d) { return (int)(((float)f + 0.5f) * inv_d); }
+
 // merge two online-softmax partials (max, sum); -inf/-inf stays (-inf, 0)
 __device__ __forceinline__ void lse_merge(float &m, float &s, float om, float os) {
     float M = fmaxf(m, om);
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lp
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
         const int f = lane + 64 * i;
-        fh[i] = f < HD ? f / D : 0;
+        fh[i] = f < HD ? div_small(f, 1.f / (float)D) : 0;
         fo[i] = f < HD ? f : HD - 1;
     }
     float *sa = s_alpha[wid];
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lp
                     const size_t o = (size_t)v * HD + f;
                     const float hv = acc[i];
                     hout[o] = hv;
-                    if (origin) out[o] = (hv > 0.f ? hv : expm1f(hv)) + org[i];
+                    if (origin) out[o] = elu1(hv) + org[i];
                 }
             }
             if (kact && l == 0) {
@@ -283,7 +292,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, in
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
         const int f = gl + LPN * i;
-        fh[i] = f < HD ? f / D : 0;
+        fh[i] = f < HD ? div_small(f, 1.f / (float)D) : 0;
         fo[i] = f < HD ? f : HD - 1;
     }
     float *sa = s_alpha[grp];
@@ -349,7 +358,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, in
                 const size_t o = (size_t)v * HD + f;
                 const float hv = acc[i];
                 hout[o] = hv;
-                if (origin) out[o] = (hv > 0.f ? hv : expm1f(hv)) + org[i];
+                if (origin) out[o] = elu1(hv) + org[i];
             }
         }
         if (kact && l == 0) {
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H,
             if (origin) {
                 f32x4_t y;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) y[j] = (acc[i][j] > 0.f ? acc[i][j] : expm1f(acc[i][j])) + org[i][j];
+                for (int j = 0; j < 4; ++j) y[j] = elu1(acc[i][j]) + org[i][j];
                 *reinterpret_cast<f32x4_t *>(out + o) = y;
             }
         }
@@ -760,7 +769,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, in
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
         const int f = lane + 64 * i;
-        fh[i] = f < HD ? f / D : 0;
+        fh[i] = f < HD ? div_small(f, 1.f / (float)D) : 0;
         fo[i] = f < HD ? f : HD - 1;
     }
     float *sa = s_alpha[wid];

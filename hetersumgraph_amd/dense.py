@@ -113,3 +113,28 @@ def splits_for(M, N, K, n_cu=256):
     kt = (K + 31) // 32
     s = max(1, min(kt // 4, (2 * n_cu) // max(tiles, 1)))
     return s
+
+
+class _Linear(torch.autograd.Function):
+    """Z = X W^T on hsg_gemm_f32 with its backward (dX = dZ W, dW = dZ^T X): the
+    eval-mode head projection fc (GATLayer.py:110 / 146) without a vendor GEMM."""
+
+    @staticmethod
+    def forward(ctx, X, W):
+        ctx.save_for_backward(X, W)
+        return gemm(X, W, b_t=True)
+
+    @staticmethod
+    def backward(ctx, dZ):
+        X, W = ctx.saved_tensors
+        dZ = dZ.contiguous()
+        dX = gemm(dZ, W) if ctx.needs_input_grad[0] else None
+        dW = gemm(dZ, X, a_t=True) if ctx.needs_input_grad[1] else None
+        return dX, dW
+
+
+def linear(X, W):
+    """X [n, in] @ W[out, in]^T with autograd, fp32 on the device (native GEMM)."""
+    if not X.is_cuda or X.dtype != torch.float32:
+        raise RuntimeError("hetersumgraph_amd linear runs only on a ROCm device in fp32 (no CPU fallback)")
+    return _Linear.apply(X.contiguous(), W.contiguous())

@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ffn import ffn_forward
+from ..dense import linear as native_linear
 from ..hproj import head_projection_dropout
 from ..ops import LEAKY_SLOPE, gat_aggregate, gat_heads_table, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
 from ..relation import N_BOX
@@ -152,7 +153,7 @@ def fused_heads(g, h, params, kind, origin=None, dropout=None):
     if dropout is not None and dropout.training and dropout.p > 0:
         Z = head_projection_dropout(h, W, H, D, dropout.p)               # per-head masks, fused
     else:
-        Z = F.linear(h, W)
+        Z = native_linear(h, W)                                          # hsg_gemm_f32 (no vendor GEMM)
     T = table_weight(g)
     if T is not None and T.shape[1] == wf.shape[2]:
         return gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, LEAKY_SLOPE)

@@ -53,13 +53,15 @@ class MultiHeadLayer(nn.Module):
         self._register_load_state_dict_pre_hook(_from_reference_keys, with_module=True)
 
     def head_views(self, k):
-        """Per-head tensors (views of the fused parameters) under reference names."""
+        """Per-head tensors (views of the fused parameters) under reference names, in
+        the reference's registration order (fc, feat_fc, attn_fc: GATLayer.py:84-87 /
+        123-126), so state_dict() lists keys exactly as the reference does."""
         D = self.head_dim
         out = {"fc.weight": self.fc_weight[k * D:(k + 1) * D],
-               "feat_fc.weight": self.feat_weight[k],
-               "attn_fc.weight": self.attn_weight[k:k + 1]}
+               "feat_fc.weight": self.feat_weight[k]}
         if self.feat_bias is not None:
             out["feat_fc.bias"] = self.feat_bias[k]
+        out["attn_fc.weight"] = self.attn_weight[k:k + 1]
         return out
 
     def reference_named_grads(self, prefix=""):

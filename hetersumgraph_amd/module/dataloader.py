@@ -10,7 +10,10 @@ collate_fn=graph_collate_fn)`` (train.py:345-367) run unchanged:
   per-document word lists of multi-document examples;
 * ``ExampleSet.__getitem__`` / ``MultiExampleSet.__getitem__`` -> ``(G, index)``;
 * ``graph_collate_fn`` (dataloader.py:472-481): sort by sentence count (the
-  reference's ``torch.sort(..., descending=True)``) and ``dgl.batch``.
+  reference's ``torch.sort(..., descending=True)``) and ``dgl.batch``;
+* ``LoadHiExampleSet`` (dataloader.py:426-440): a directory of cached
+  ``<index>.graph.bin`` graphs read with ``load_graphs`` -- this build's on-disk
+  format (hetersumgraph_amd/dgl/data/utils.py), not DGL's binary one.
 
 One difference: the reference's stop-word list comes from nltk
 (``stopwords.words('english')``, dataloader.py:48), which is not installed here;
@@ -20,6 +23,7 @@ filter words are applied as in the reference).
 from __future__ import annotations
 
 import json
+import os
 
 import numpy as np
 import torch
@@ -190,3 +194,21 @@ def graph_collate_fn(samples):
     sorted_len, sorted_index = torch.sort(torch.LongTensor(graph_len), dim=0, descending=True)
     batched_graph = hg.batch([graphs[idx] for idx in sorted_index])
     return batched_graph, [index[idx] for idx in sorted_index]
+
+
+class LoadHiExampleSet(torch.utils.data.Dataset):
+    """dataloader.py:426-440: item ``index`` is graph 0 of ``<data_root>/<index>.graph.bin``
+    (written by ``save_graphs``), returned as ``(G, index)`` like ExampleSet."""
+
+    def __init__(self, data_root):
+        super().__init__()
+        self.data_root = data_root
+        self.gfiles = [f for f in os.listdir(self.data_root) if f.endswith("graph.bin")]
+
+    def __getitem__(self, index):
+        from ..dgl.data.utils import load_graphs
+        g, _labels = load_graphs(os.path.join(self.data_root, "%d.graph.bin" % index))
+        return g[0], index
+
+    def __len__(self):
+        return len(self.gfiles)
