@@ -386,6 +386,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm(GemmArgs p) {
 // ------------------------------------------------- 3-limb bf16 split (k_gemm3) --
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short v4s16 __attribute__((ext_vector_type(4)));
 
 // bf16 per LDS row of a limb plane: BK k + 8 pad (row stride 16 B mod 64: the 16-lane
 // ds_read_b128 groups hit 64 distinct banks)
@@ -399,16 +400,19 @@ __device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &
 }
 
 // One operand tile for k_gemm3: ROWS (M or N) x BK (K) from global into registers,
-// then into NL bf16 limb planes [ROWS][BK + 8] in LDS (always k-contiguous, so the
-// MFMA fragments are single ds_read_b128s whatever the global layout).
-//   KC:  a thread covers (row, 4 consecutive k)            -> NL x ds_write_b64
-//   !KC: a thread covers (4 consecutive rows, 2 consecutive k) from two float4 loads
-//        of adjacent k rows (the transpose happens in registers) -> 4 NL x ds_write_b32
+// then into NL bf16 limb planes in LDS, in the operand's own global orientation:
+//   KC:  [ROWS][BK + 8] (k-contiguous rows): a thread covers (row, 4 consecutive k)
+//        -> NL x ds_write_b64; fragments are single ds_read_b128s;
+//   !KC: [BK][ROWS + 8] (k-major, as the M/N-contiguous operand sits in memory): a
+//        thread covers (k, 4 consecutive rows) -> NL x ds_write_b64, and fragments
+//        come back k-contiguous through the hardware transpose read
+//        ds_read_b64_tr_b16 (two per fragment) -- no in-register transpose.
 template <bool KC, int ROWS, int BK, int NL>
 struct Stage3 {
-    static constexpr int LD = Ldh<BK>::v;
-    static constexpr int NU = KC ? ROWS * BK / 1024 : ROWS * BK / 2048;    // units per thread
-    f32x4 v[KC ? NU : 2 * NU];
+    static constexpr int LD = KC ? Ldh<BK>::v : ROWS + 8;     // bf16 per image row
+    static constexpr int IMG = KC ? ROWS * LD : BK * LD;      // bf16 per limb plane
+    static constexpr int NU = ROWS * BK / 1024;               // float4 units per thread
+    f32x4 v[NU];
 
     __device__ __forceinline__ static f32x4 ld4(const float *__restrict__ g, int ld, int gr, int gc, int lim_r,
                                                 int lim_c) {
@@ -434,59 +438,58 @@ struct Stage3 {
                 const int row = idx / (BK / 4), col = (idx % (BK / 4)) * 4;
                 v[i] = ld4(g, ld, r0 + row, k0 + col, nr, nk);
             } else {
-                const int rq = idx % (ROWS / 4), kp = idx / (ROWS / 4);
-                v[2 * i] = ld4(g, ld, k0 + 2 * kp, r0 + 4 * rq, nk, nr);
-                v[2 * i + 1] = ld4(g, ld, k0 + 2 * kp + 1, r0 + 4 * rq, nk, nr);
+                const int kk = idx / (ROWS / 4), mq = idx % (ROWS / 4);
+                v[i] = ld4(g, ld, k0 + kk, r0 + 4 * mq, nk, nr);
             }
         }
     }
 
-    __device__ __forceinline__ void store(__bf16 (*s)[ROWS * LD]) const {
+    __device__ __forceinline__ void store(__bf16 (*s)[IMG]) const {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
             const int idx = threadIdx.x + 256 * i;
-            if constexpr (KC) {
-                const int row = idx / (BK / 4), col = (idx % (BK / 4)) * 4;
-                bf16x4 x0, x1, x2;
+            const int o = KC ? (idx / (BK / 4)) * LD + (idx % (BK / 4)) * 4
+                             : (idx / (ROWS / 4)) * LD + (idx % (ROWS / 4)) * 4;
+            bf16x4 x0, x1, x2;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    if constexpr (NL == 3) {
-                        __bf16 a, b, c;
-                        split3(v[i][e], a, b, c);
-                        x0[e] = a; x1[e] = b; x2[e] = c;
-                    } else {
-                        x0[e] = (__bf16)v[i][e];
-                    }
-                }
-                const int o = row * LD + col;
-                *reinterpret_cast<bf16x4 *>(&s[0][o]) = x0;
+            for (int e = 0; e < 4; ++e) {
                 if constexpr (NL == 3) {
-                    *reinterpret_cast<bf16x4 *>(&s[1][o]) = x1;
-                    *reinterpret_cast<bf16x4 *>(&s[2][o]) = x2;
-                }
-            } else {
-                const int rq = idx % (ROWS / 4), kp = idx / (ROWS / 4);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    bf16x2 x0, x1, x2;
-#pragma unroll
-                    for (int q = 0; q < 2; ++q) {
-                        if constexpr (NL == 3) {
-                            __bf16 a, b, c;
-                            split3(v[2 * i + q][e], a, b, c);
-                            x0[q] = a; x1[q] = b; x2[q] = c;
-                        } else {
-                            x0[q] = (__bf16)v[2 * i + q][e];
-                        }
-                    }
-                    const int o = (4 * rq + e) * LD + 2 * kp;
-                    *reinterpret_cast<bf16x2 *>(&s[0][o]) = x0;
-                    if constexpr (NL == 3) {
-                        *reinterpret_cast<bf16x2 *>(&s[1][o]) = x1;
-                        *reinterpret_cast<bf16x2 *>(&s[2][o]) = x2;
-                    }
+                    __bf16 a, b, c;
+                    split3(v[i][e], a, b, c);
+                    x0[e] = a; x1[e] = b; x2[e] = c;
+                } else {
+                    x0[e] = (__bf16)v[i][e];
                 }
             }
+            *reinterpret_cast<bf16x4 *>(&s[0][o]) = x0;
+            if constexpr (NL == 3) {
+                *reinterpret_cast<bf16x4 *>(&s[1][o]) = x1;
+                *reinterpret_cast<bf16x4 *>(&s[2][o]) = x2;
+            }
+        }
+    }
+
+    // MFMA 32x32x16 operand fragment of rows [row0, row0 + 32), k step s16: lane
+    // (li = lane & 31, h = lane >> 5) gets rows row0 + li, k = 16 s16 + 8h + 0..7
+    __device__ __forceinline__ static bf16x8 frag(const __bf16 *plane, int row0, int s16, int lane) {
+        if constexpr (KC) {
+            return *reinterpret_cast<const bf16x8 *>(&plane[(row0 + (lane & 31)) * LD + 16 * s16 + 8 * (lane >> 5)]);
+        } else {
+            // 16-lane group: lane 4q + p addresses image row (k) q, columns 4p..4p+3
+            // of its 4 x 16 block; lane i of the group receives column i, rows 0..3
+            const int i = lane & 15, q = i >> 2, p = i & 3;
+            const int kb = 16 * s16 + 8 * (lane >> 5);
+            const int col = row0 + 16 * ((lane >> 4) & 1) + 4 * p;
+            typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
+            const v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_v4s16 *)(const_cast<__bf16 *>(&plane[(kb + q) * LD + col])));
+            const v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_v4s16 *)(const_cast<__bf16 *>(&plane[(kb + 4 + q) * LD + col])));
+            // whole-vector reinterpretation (element-wise short -> __bf16 casts were
+            // lowered to wrong lane selects)
+            typedef short v8s16 __attribute__((ext_vector_type(8)));
+            const v8s16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+            return __builtin_bit_cast(bf16x8, r);
         }
     }
 };
@@ -498,11 +501,10 @@ struct Stage3 {
 // pipeline (dev only).  The epilogue (and split-K / column partials) is k_gemm's.
 template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL>
 __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
-    constexpr int LD = Ldh<BK>::v;
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 32, TN = WN / 32;
-    __shared__ __attribute__((aligned(16))) __bf16 sA[NL][BM * LD];
-    __shared__ __attribute__((aligned(16))) __bf16 sB[NL][BN * LD];
+    __shared__ __attribute__((aligned(16))) __bf16 sA[NL][Stage3<AK, BM, BK, NL>::IMG];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[NL][Stage3<BKC, BN, BK, NL>::IMG];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wm = wid >> 1, wn = wid & 1;
     const int li = lane & 31, h = lane >> 5;
@@ -552,13 +554,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
 #pragma unroll
             for (int l = 0; l < NL; ++l) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    a[l][i] = *reinterpret_cast<const bf16x8 *>(
-                        &sA[l][(wm * WM + i * 32 + li) * LD + 16 * s16 + 8 * h]);
+                for (int i = 0; i < TM; ++i) a[l][i] = Stage3<AK, BM, BK, NL>::frag(sA[l], wm * WM + i * 32, s16, lane);
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    b[l][j] = *reinterpret_cast<const bf16x8 *>(
-                        &sB[l][(wn * WN + j * 32 + li) * LD + 16 * s16 + 8 * h]);
+                for (int j = 0; j < TN; ++j) b[l][j] = Stage3<BKC, BN, BK, NL>::frag(sB[l], wn * WN + j * 32, s16, lane);
             }
             // smallest limb products first, a0*b0 last
 #pragma unroll
@@ -787,9 +785,12 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
         if (!colsum_part) best = atoi(f);
     int rc;
-    // both operands M/N-contiguous (the weight gradients dW = dY^T X): the in-register
-    // transposes of the split staging cost more than the MFMA saves -> exact-f32 MFMA
-    if (mode == MODE_F32_SPLIT && !ak && !bk && !getenv("HSG_GEMM3_TILE")) mode = MODE_F32_MFMA;
+    // both operands M/N-contiguous (the weight gradients dW = dY^T X): exact-f32 MFMA
+    // unless HSG_GEMM3_DW=1 (dev A/B of the transpose-read split path)
+    if (mode == MODE_F32_SPLIT && !ak && !bk && !getenv("HSG_GEMM3_TILE")) {
+        const char *e = getenv("HSG_GEMM3_DW");
+        if (!e || e[0] != '1') mode = MODE_F32_MFMA;
+    }
     if (mode == MODE_F32_SPLIT) {
         int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
         if (const char *f = getenv("HSG_GEMM3_TILE"))      // dev override
