@@ -619,6 +619,500 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// k_gemm4: the 3-limb split GEMM for two K-contiguous operands with an LDS-DMA
+// pipeline.  The fp32 K tiles (32 floats = 128 B per row) go global -> LDS by
+// global_load_lds_dwordx4 (1 KB = 8 rows per wave-instruction, no VGPRs), S stages
+// deep, one raw barrier per K tile with a counted vmcnt so S-2 tiles stay in flight
+// across it.  The limbs are split at fragment-read time (fp32 fragments by
+// ds_read_b128, split3 in registers beside the MFMAs), so LDS holds 4 B per element
+// instead of three 2-B planes and there is no split-and-store phase between barriers.
+// Chunk q (16 B) of tile row r sits at position q ^ swz(r): every 16-lane group of a
+// fragment read then covers 16 distinct 16-B bank slots (conflict-free); the swizzle
+// is applied on the global SOURCE address since the DMA's LDS image is lane-linear.
+// K-tail chunks (k >= K; K % 4 == 0) read a zeroed 16-B global word; rows past M/N
+// are clamped (their outputs are never stored).
+// ---------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) float g_zero16[4];
+
+__device__ __forceinline__ int swz(int r) { return (r >> 1) & 7; }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int ROWS>
+__device__ __forceinline__ void glds_tile(float *img, const float *__restrict__ g, int ld, int r0, int nr, int k0,
+                                          int K, int wid, int lane) {
+#pragma unroll
+    for (int pc = 0; pc < ROWS / 32; ++pc) {              // ROWS/8 pieces of 8 rows over 4 waves
+        const int piece = pc * 4 + wid;
+        const int r = piece * 8 + (lane >> 3);
+        const int q = (lane & 7) ^ swz(r);
+        const int k = k0 + 4 * q;
+        const int gr = min(r0 + r, nr - 1);
+        const float *src = k < K ? g + (size_t)gr * ld + k : g_zero16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(img + piece * 256), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void frag_split(const float *img, int r, int s16, int h, bf16x8 &l0, bf16x8 &l1,
+                                           bf16x8 &l2) {
+    const int q0 = 4 * s16 + 2 * h, sw = swz(r);
+    const f32x4 x = *reinterpret_cast<const f32x4 *>(&img[r * 32 + 4 * (q0 ^ sw)]);
+    const f32x4 y = *reinterpret_cast<const f32x4 *>(&img[r * 32 + 4 * ((q0 + 1) ^ sw)]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, c;
+        split3(e < 4 ? x[e] : y[e - 4], a, b, c);
+        l0[e] = a; l1[e] = b; l2[e] = c;
+    }
+}
+
+template <int BM, int BN, int S>
+__global__ __launch_bounds__(256, 2) void k_gemm4(GemmArgs p) {
+    constexpr int WM = BM / 2, WN = BN / 2;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    constexpr int STAGE = (BM + BN) * 32;                  // floats per stage
+    constexpr int NLD = (BM + BN) / 32;                    // DMA instructions per wave per K tile
+    __shared__ __attribute__((aligned(16))) float lds[S * STAGE];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+    const int li = lane & 31, h = lane >> 5;
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int tiles_mn = tiles_n * tiles_m;
+    const int kt_total = (p.K + 31) / 32;
+    const int total = tiles_mn * p.splits;
+    const int t = blockIdx.x;
+    const int lt = p.xcd ? xcd_tile(t, total) : t;
+    const int tx = lt % tiles_n, ty = (lt / tiles_n) % tiles_m, tz = lt / tiles_mn;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int kt0 = tz * p.k_tiles_per_split;
+    const int nt = min(kt_total, kt0 + p.k_tiles_per_split) - kt0;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto issue = [&](int i) {
+        float *st = lds + (i % S) * STAGE;
+        const int k0 = (kt0 + i) * 32;
+        glds_tile<BM>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
+        glds_tile<BN>(st + BM * 32, p.B, p.ldb, n0, p.N, k0, p.K, wid, lane);
+    };
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i)
+        if (i < nt) issue(i);
+    for (int i = 0; i < nt; ++i) {
+        // this wave's DMAs of tile i have landed once at most the newer tiles' are pending
+        const int ahead = min(S - 2, nt - 1 - i);
+        if (ahead >= 2) wait_vmcnt<2 * NLD>();
+        else if (ahead == 1) wait_vmcnt<NLD>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                      // every wave's DMAs of tile i landed;
+        asm volatile("" ::: "memory");                     // every wave is done reading tile i-1
+        if (i + S - 1 < nt) issue(i + S - 1);              // into tile i-1's stage
+        const float *sa = lds + (i % S) * STAGE, *sb = sa + BM * 32;
+#pragma unroll
+        for (int s16 = 0; s16 < 2; ++s16) {
+            bf16x8 a[3][TM], b[3][TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) frag_split(sb, wn * WN + j * 32 + li, s16, h, b[0][j], b[1][j], b[2][j]);
+#pragma unroll
+            for (int i2 = 0; i2 < TM; ++i2) frag_split(sa, wm * WM + i2 * 32 + li, s16, h, a[0][i2], a[1][i2], a[2][i2]);
+#pragma unroll
+            for (int i2 = 0; i2 < TM; ++i2)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i2], b[0][j], acc[i2][j], 0, 0, 0);
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i2], b[1][j], acc[i2][j], 0, 0, 0);
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i2], b[2][j], acc[i2][j], 0, 0, 0);
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i2], b[0][j], acc[i2][j], 0, 0, 0);
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i2], b[1][j], acc[i2][j], 0, 0, 0);
+                    acc[i2][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i2], b[0][j], acc[i2][j], 0, 0, 0);
+                }
+        }
+    }
+
+    // epilogue (as k_gemm3): lane holds rows (r&3)+8*(r>>2)+4*h, column li of each 32x32 tile
+    const bool split = p.splits > 1;
+    float csum[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) csum[j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WN + j * 32 + li;
+            if (n >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (m >= p.M) continue;
+                if (split) {
+                    p.ws[((size_t)tz * p.M + m) * p.N + n] = acc[i][j][r];
+                } else {
+                    const float v = epi_apply(acc[i][j][r], m, n, p);
+                    p.C[(size_t)m * p.ldc + n] = v;
+                    csum[j] += v;
+                }
+            }
+        }
+    if (p.colpart && !split) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
+        __syncthreads();                                   // no DMA is pending here
+        float *red = lds;
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + li] = csum[j];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < BN; c += 256) {
+            const int n = n0 + c;
+            if (n < p.N) p.colpart[(size_t)ty * p.N + n] = red[c] + red[BN + c];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_gemm5: C = A B^T with fp32 A (K-contiguous) and a PRE-SPLIT weight B: its three
+// bf16 limb planes [3][Np][Kp] are made once per step by k_wsplit (hsg_wsplit), so
+// only A is split in the GEMM, at fragment-read time.  Block = 128 rows x BN columns,
+// 4 waves stacked along M (each wave splits its own 32 A rows once and multiplies
+// them into all BN columns: 6·BN/32 MFMAs per 8-element split).  Both operands go
+// global -> LDS by global_load_lds_dwordx4, S stages deep (as k_gemm4).  Limb plane
+// tile rows are 64 B; chunk c (16 B) of row r sits at c ^ ((r >> 2) & 3), which
+// makes the ds_read_b128 fragment reads conflict-free.
+// ---------------------------------------------------------------------------------
+struct WSplitJobs {
+    const float *W[4];
+    __bf16 *out[4];
+    int N[4], K[4], ldw[4], trans[4], Np[4], Kp[4];
+    int start[5];
+    int n;
+};
+
+// One thread per (n, 8 consecutive k): three 16-B limb stores.  Job q owns blocks
+// [start[q], start[q+1]); for a transposed weight consecutive threads take consecutive
+// n, so each of the 8 reads W[k][n] is coalesced across the wave.
+__global__ __launch_bounds__(256) void k_wsplit(WSplitJobs j) {
+    int q = 0;
+    while (q + 1 < j.n && (int)blockIdx.x >= j.start[q + 1]) ++q;
+    const int u = ((int)blockIdx.x - j.start[q]) * 256 + threadIdx.x;
+    const int Kp = j.Kp[q], Np = j.Np[q], N = j.N[q], K = j.K[q], ldw = j.ldw[q];
+    const int kc8 = Kp / 8;
+    if (u >= Np * kc8) return;
+    const bool tr = j.trans[q] != 0;
+    const int n = tr ? u % Np : u / kc8, k0 = 8 * (tr ? u / Np : u % kc8);
+    const float *W = j.W[q];
+    bf16x8 x0, x1, x2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = k0 + e;
+        float v = 0.f;
+        if (n < N && k < K) v = tr ? W[(size_t)k * ldw + n] : W[(size_t)n * ldw + k];
+        __bf16 a, b, c;
+        split3(v, a, b, c);
+        x0[e] = a; x1[e] = b; x2[e] = c;
+    }
+    const size_t plane = (size_t)Np * Kp, o = (size_t)n * Kp + k0;
+    *reinterpret_cast<bf16x8 *>(j.out[q] + o) = x0;
+    *reinterpret_cast<bf16x8 *>(j.out[q] + plane + o) = x1;
+    *reinterpret_cast<bf16x8 *>(j.out[q] + 2 * plane + o) = x2;
+}
+
+// Epilogue of one wave's TN 32x32 accumulator tiles (lane: rows row0 + (r&3) + 8(r>>2)
+// + 4h, column col0 + 32j + li), epi_apply's semantics.  The aux operand (relu' mask
+// or addend) is loaded for all of the lane's elements FIRST, unconditionally from
+// clamped indices, so the 16·TN loads are in flight together instead of each one
+// waiting behind its own bounds branch; the stores stay guarded.
+template <int TN>
+__device__ __forceinline__ void epi_store(const f32x16 (&acc)[TN], int row0, int col0, int li, int h,
+                                          const GemmArgs &p, float (&csum)[TN]) {
+    float aux[TN][16];
+    if (p.epi != HSG_EPI_STORE) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int nc = min(col0 + 32 * j + li, p.N - 1);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int mc = min(row0 + (r & 3) + 8 * (r >> 2) + 4 * h, p.M - 1);
+                aux[j][r] = p.aux[(size_t)mc * p.ldaux + nc];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = col0 + 32 * j + li;
+        const float bn = p.bias ? p.bias[min(n, p.N - 1)] : 0.f;
+        csum[j] = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int m = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            float v = acc[j][r];
+            if (p.epi == HSG_EPI_RELU_BWD) {
+                v = aux[j][r] > 0.f ? v : 0.f;
+            } else {
+                v += bn;
+                if (p.epi == HSG_EPI_ADD) v += aux[j][r];
+                if (p.relu) v = fmaxf(v, 0.f);
+            }
+            if (m < p.M && n < p.N) {
+                p.C[(size_t)m * p.ldc + n] = v;
+                csum[j] += v;
+            }
+        }
+    }
+}
+
+template <int BN, int S, int IGLP = -1>
+__global__ __launch_bounds__(256, 2) void k_gemm5(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
+    constexpr int BM = 128, TN = BN / 32;
+    constexpr int A_FL = BM * 32;                          // floats of the A tile
+    constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
+    constexpr int STAGE_FL = A_FL + 3 * B_BF / 2;          // stage size in floats
+    constexpr int BPC = BN / 16;                           // 1-KB pieces per limb plane tile
+    constexpr int NLD = (BM / 8 + 3 * BPC) / 4;            // DMA instructions per wave per K tile
+    static_assert((3 * BPC) % 4 == 0, "B pieces must split evenly over 4 waves");
+    __shared__ __attribute__((aligned(16))) float lds[S * STAGE_FL];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int li = lane & 31, h = lane >> 5;
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int total = tiles_n * tiles_m;
+    const int lt = p.xcd ? xcd_tile(blockIdx.x, total) : (int)blockIdx.x;
+    const int tx = lt % tiles_n, ty = lt / tiles_n;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int nt = Kp / 32;
+
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    auto issue = [&](int i) {
+        float *st = lds + (i % S) * STAGE_FL;
+        const int k0 = i * 32;
+        glds_tile<BM>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
+        __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
+#pragma unroll
+        for (int pc = 0; pc < 3 * BPC / 4; ++pc) {
+            const int piece = pc * 4 + wid;
+            const int limb = piece / BPC, prow = (piece % BPC) * 16;
+            const int r = prow + (lane >> 2);
+            const int c = (lane & 3) ^ ((r >> 2) & 3);
+            const __bf16 *src = planes + ((size_t)(limb * Np + n0 + r) * Kp + k0 + 8 * c);
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                             (__attribute__((address_space(3))) void *)(sb + limb * B_BF + prow * 32),
+                                             16, 0, 0);
+        }
+    };
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i)
+        if (i < nt) issue(i);
+    for (int i = 0; i < nt; ++i) {
+        const int ahead = min(S - 2, nt - 1 - i);
+        if (ahead >= 2) wait_vmcnt<2 * NLD>();
+        else if (ahead == 1) wait_vmcnt<NLD>();
+        else wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (i + S - 1 < nt) issue(i + S - 1);
+        const float *sa = lds + (i % S) * STAGE_FL;
+        const __bf16 *sb = reinterpret_cast<const __bf16 *>(sa + A_FL);
+#pragma unroll
+        for (int s16 = 0; s16 < 2; ++s16) {
+            bf16x8 a0, a1, a2;
+            frag_split(sa, wid * 32 + li, s16, h, a0, a1, a2);
+            bf16x8 b[3][TN];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int r = j * 32 + li, c = 2 * s16 + h;
+                const int off = r * 32 + 8 * (c ^ ((r >> 2) & 3));
+#pragma unroll
+                for (int l = 0; l < 3; ++l) b[l][j] = *reinterpret_cast<const bf16x8 *>(&sb[l * B_BF + off]);
+            }
+            // the TN accumulator chains interleaved product by product
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0][j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1][j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[2][j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0][j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1][j], acc[j], 0, 0, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0][j], acc[j], 0, 0, 0);
+        }
+        if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
+    }
+
+    float csum[TN];
+    epi_store<TN>(acc, m0 + wid * 32, n0, li, h, p, csum);
+    if (p.colpart) {                                        // 64-row partials, as hsg_gemm_row_tiles
+#pragma unroll
+        for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
+        __syncthreads();                                   // no DMA is pending here
+        float *red = lds;
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) red[wid * BN + j * 32 + li] = csum[j];
+        }
+        __syncthreads();
+        const int rows64 = (p.M + 63) / 64;
+        for (int c = threadIdx.x; c < 2 * BN; c += 256) {
+            const int half = c / BN, n = n0 + c % BN, slab = 2 * ty + half;
+            if (n < p.N && slab < rows64)
+                p.colpart[(size_t)slab * p.N + n] = red[(2 * half) * BN + c % BN] + red[(2 * half + 1) * BN + c % BN];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// k_gemm6: k_gemm5's contract (fp32 A, pre-split weight planes) with A never staged
+// through LDS: each wave owns 32 A rows that no other wave reads, so every lane loads
+// its own fragment (row li, 8 consecutive k per 16-k step: 2 x dwordx4) straight
+// into registers, two K tiles ahead, and splits it there.  Only the weight limbs go
+// through LDS (register-staged, double-buffered, one barrier per K tile); all loads
+// are ordinary VGPR loads, so the compiler's counted vmcnt waits stay exact.
+// ---------------------------------------------------------------------------------
+template <int BN>
+__global__ __launch_bounds__(256, 2) void k_gemm6(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
+    constexpr int BM = 128, TN = BN / 32;
+    constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
+    constexpr int B_BUF = 3 * B_BF;                        // bf16 per buffer
+    constexpr int BU = 3 * BN * 4 / 256;                   // 16-B B units per thread per K tile
+    __shared__ __attribute__((aligned(16))) __bf16 sb[2 * B_BUF];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int li = lane & 31, h = lane >> 5;
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int total = tiles_n * tiles_m;
+    const int lt = p.xcd ? xcd_tile(blockIdx.x, total) : (int)blockIdx.x;
+    const int tx = lt % tiles_n, ty = lt / tiles_n;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int nt = Kp / 32;
+    const float *arow = p.A + (size_t)min(m0 + wid * 32 + li, p.M - 1) * p.lda;
+
+    f32x16 acc[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+    // A fragment quads of K tile kt: u = 2*s16 + e -> k = 32 kt + 16 s16 + 8 h + 4 e
+    auto load_a = [&](f32x4 (&r)[4], int kt) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = kt * 32 + 16 * (u >> 1) + 8 * h + 4 * (u & 1);
+            const float *src = k < p.K ? arow + k : g_zero16;
+            r[u] = *reinterpret_cast<const f32x4 *>(src);
+        }
+    };
+    auto load_b = [&](uint4 (&r)[BU], int kt) {
+#pragma unroll
+        for (int v = 0; v < BU; ++v) {
+            const int u = threadIdx.x + 256 * v;
+            const int limb = u / (BN * 4), rr = (u >> 2) % BN, c = u & 3;
+            r[v] = *reinterpret_cast<const uint4 *>(planes + ((size_t)(limb * Np + n0 + rr) * Kp + kt * 32 + 8 * c));
+        }
+    };
+    auto store_b = [&](int buf, const uint4 (&r)[BU]) {
+#pragma unroll
+        for (int v = 0; v < BU; ++v) {
+            const int u = threadIdx.x + 256 * v;
+            const int limb = u / (BN * 4), rr = (u >> 2) % BN, c = u & 3;
+            *reinterpret_cast<uint4 *>(&sb[buf * B_BUF + limb * B_BF + rr * 32 + 8 * (c ^ ((rr >> 2) & 3))]) = r[v];
+        }
+    };
+    auto compute = [&](int buf, const f32x4 (&a)[4]) {
+        const __bf16 *b = sb + buf * B_BUF;
+#pragma unroll
+        for (int s16 = 0; s16 < 2; ++s16) {
+            bf16x8 a0, a1, a2;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                __bf16 x0, x1, x2;
+                split3(a[2 * s16 + (e >> 2)][e & 3], x0, x1, x2);
+                a0[e] = x0; a1[e] = x1; a2[e] = x2;
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int r = j * 32 + li, c = 2 * s16 + h;
+                const int off = r * 32 + 8 * (c ^ ((r >> 2) & 3));
+                const bf16x8 b0 = *reinterpret_cast<const bf16x8 *>(&b[off]);
+                const bf16x8 b1 = *reinterpret_cast<const bf16x8 *>(&b[B_BF + off]);
+                const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(&b[2 * B_BF + off]);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[j], 0, 0, 0);
+            }
+        }
+    };
+
+    f32x4 aA[4], aB[4];
+    uint4 braw[BU];
+    load_a(aA, 0);
+    load_b(braw, 0);
+    store_b(0, braw);
+    if (nt > 1) {
+        load_a(aB, 1);
+        load_b(braw, 1);
+    }
+    __syncthreads();
+    // one K tile per step; the two A register sets alternate (steps unrolled in pairs)
+    auto step = [&](int i, f32x4 (&acur)[4], f32x4 (&anext2)[4]) {
+        compute(i & 1, acur);
+        if (i + 1 < nt) store_b((i + 1) & 1, braw);        // tile i+1's limbs, loaded a step ago
+        if (i + 2 < nt) {
+            load_a(anext2, i + 2);
+            load_b(braw, i + 2);
+        }
+        __syncthreads();
+    };
+    int i = 0;
+    for (; i + 1 < nt; i += 2) {
+        step(i, aA, aA);
+        step(i + 1, aB, aB);
+    }
+    if (i < nt) step(i, aA, aA);
+
+    float csum[TN];
+    epi_store<TN>(acc, m0 + wid * 32, n0, li, h, p, csum);
+    if (p.colpart) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) csum[j] += __shfl_xor(csum[j], 32);
+        float *red = reinterpret_cast<float *>(sb);         // the last step ended in a barrier
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) red[wid * BN + j * 32 + li] = csum[j];
+        }
+        __syncthreads();
+        const int rows64 = (p.M + 63) / 64;
+        for (int c = threadIdx.x; c < 2 * BN; c += 256) {
+            const int half = c / BN, n = n0 + c % BN, slab = 2 * ty + half;
+            if (n < p.N && slab < rows64)
+                p.colpart[(size_t)slab * p.N + n] = red[(2 * half) * BN + c % BN] + red[(2 * half + 1) * BN + c % BN];
+        }
+    }
+}
+
 // Sums the split slabs in split order (deterministic).  The slab loads are issued 8
 // at a time ahead of the adds, so a thread has 8 independent loads in flight instead
 // of one dependent load per split; the addition order is unchanged.
@@ -701,6 +1195,37 @@ int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
     else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int BM, int BN, int S>
+int launch4(GemmArgs p, int splits, hipStream_t st) {
+    const int kt_total = (p.K + 31) / 32;
+    p.k_tiles_per_split = (kt_total + splits - 1) / splits;
+    p.splits = splits;
+    const long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
+    hipLaunchKernelGGL((k_gemm4<BM, BN, S>), dim3((unsigned)g), dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int BN>
+int launch6(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    p.splits = 1;
+    p.k_tiles_per_split = Kp / 32;
+    const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
+    hipLaunchKernelGGL((k_gemm6<BN>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int BN, int S, int IGLP = -1>
+int launch5(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    p.splits = 1;
+    p.k_tiles_per_split = Kp / 32;
+    const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
+    hipLaunchKernelGGL((k_gemm5<BN, S, IGLP>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -791,7 +1316,16 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         const char *e = getenv("HSG_GEMM3_DW");
         if (!e || e[0] != '1') mode = MODE_F32_MFMA;
     }
-    if (mode == MODE_F32_SPLIT) {
+    int g4 = 0;                                             // dev switch: k_gemm4 plans
+    if (const char *f = getenv("HSG_GEMM4")) g4 = atoi(f);
+    if (mode == MODE_F32_SPLIT && ak && bk && (K & 3) == 0 && g4 > 0) {
+        if (colsum_part || g4 == 1) rc = launch4<64, 64, 3>(p, splits, st);
+        else if (g4 == 2) rc = launch4<128, 64, 3>(p, splits, st);
+        else if (g4 == 3) rc = launch4<64, 64, 4>(p, splits, st);
+        else if (g4 == 4) rc = launch4<128, 64, 2>(p, splits, st);
+        else if (g4 == 5) rc = launch4<64, 64, 2>(p, splits, st);
+        else rc = launch4<128, 128, 2>(p, splits, st);
+    } else if (mode == MODE_F32_SPLIT) {
         int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
         if (const char *f = getenv("HSG_GEMM3_TILE"))      // dev override
             if (!colsum_part) t3 = atoi(f);
@@ -865,6 +1399,57 @@ int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig, c
                   int relu, int splits, float *workspace, float *colsum_part, void *stream) {
     return gemm_impl(MODE_BF16, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
+}
+
+void hsg_wsplit_dims(int N, int K, int *Np, int *Kp) {
+    *Np = (N + 127) / 128 * 128;
+    *Kp = (K + 31) / 32 * 32;
+}
+
+int hsg_wsplit(int njobs, const float *const *W, const int *N, const int *K, const int *ldw, const int *trans,
+               void *const *planes, void *stream) {
+    if (njobs < 1 || njobs > 4) return HSG_EINVAL;
+    WSplitJobs j{};
+    j.n = njobs;
+    j.start[0] = 0;
+    for (int q = 0; q < njobs; ++q) {
+        if (!W[q] || !planes[q] || N[q] <= 0 || K[q] <= 0 || (((uintptr_t)planes[q]) & 15)) return HSG_EINVAL;
+        if (ldw[q] < (trans[q] ? N[q] : K[q])) return HSG_EINVAL;
+        j.W[q] = W[q];
+        j.out[q] = reinterpret_cast<__bf16 *>(planes[q]);
+        j.N[q] = N[q]; j.K[q] = K[q]; j.ldw[q] = ldw[q]; j.trans[q] = trans[q] != 0;
+        hsg_wsplit_dims(N[q], K[q], &j.Np[q], &j.Kp[q]);
+        j.start[q + 1] = j.start[q] + (j.Np[q] * (j.Kp[q] / 8) + 255) / 256;     // blocks
+    }
+    hipLaunchKernelGGL(k_wsplit, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                     const float *bias, const float *aux, int ldaux, int epi, int relu, float *colsum_part,
+                     void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
+    if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K) return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
+    if (const char *x = getenv("HSG_GEMM_XCD")) p.xcd = atoi(x);
+    int plan = 7;                                           // BN 64, 2 stages, iglp_opt(0) (tools/gemm5_sweep.py)
+    if (const char *f = getenv("HSG_GEMM5")) plan = atoi(f);
+    const __bf16 *pl = reinterpret_cast<const __bf16 *>(planes);
+    hipStream_t st = (hipStream_t)stream;
+    if (plan == 2) return launch5<128, 2>(p, pl, Np, Kp, st);
+    if (plan == 3) return launch5<64, 3>(p, pl, Np, Kp, st);
+    if (plan == 4) return launch5<128, 3>(p, pl, Np, Kp, st);
+    if (plan == 5) return launch6<64>(p, pl, Np, Kp, st);
+    if (plan == 6) return launch6<128>(p, pl, Np, Kp, st);
+    if (plan == 7) return launch5<64, 2, 0>(p, pl, Np, Kp, st);
+    if (plan == 8) return launch5<64, 2, 1>(p, pl, Np, Kp, st);
+    return launch5<64, 2>(p, pl, Np, Kp, st);
 }
 
 #ifdef HSG_GEMM_CENSUS

@@ -18,6 +18,7 @@ Operand precision, chosen process-wide with :func:`set_gemm_dtype` /
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import os
 
 import torch
@@ -93,6 +94,70 @@ def gemm(A, B, a_t=False, b_t=False, out=None, bias=None, relu=False, relu_mask=
     check(fn(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), ptr(out),
                            _ld(out), ptr(bias), ptr(aux), _ld(aux) if aux is not None else 0, epi,
                            int(relu), int(splits), ptr(ws), ptr(colsum_part), stream_of(A)), fn.__name__)
+    return out
+
+
+class SplitWeight:
+    """A weight operand B [N][K] held as its three bf16 limb planes [3][Np][Kp]
+    (hsg_wsplit), for gemm_psw: made once per step, reused by every GEMM that
+    multiplies by B (the FFN's W1 / W2 in the forward, W1^T / W2^T in the backward)."""
+    __slots__ = ("planes", "N", "K")
+
+    def __init__(self, planes, N, K):
+        self.planes, self.N, self.K = planes, N, K
+
+
+def split_dims(N, K):
+    lib = load()
+    np_, kp = ctypes.c_int(), ctypes.c_int()
+    lib.hsg_wsplit_dims(N, K, ctypes.byref(np_), ctypes.byref(kp))
+    return np_.value, kp.value
+
+
+def split_weights(*specs):
+    """[(W, trans), ...] (1..4) -> [SplitWeight]: B = W^T if trans else W, split in
+    one launch."""
+    lib = load()
+    if not 1 <= len(specs) <= 4:
+        raise ValueError("split_weights: 1..4 weights per launch")
+    out, Ns, Ks, lds, trs, Ws, Ps = [], [], [], [], [], [], []
+    for W, trans in specs:
+        if not W.is_cuda or W.dtype != torch.float32 or W.dim() != 2 or W.stride(1) != 1:
+            raise RuntimeError("split_weights: 2-D row-major fp32 ROCm tensors only")
+        N, K = (W.shape[1], W.shape[0]) if trans else (W.shape[0], W.shape[1])
+        Np, Kp = split_dims(N, K)
+        planes = torch.empty(3 * Np * Kp, dtype=torch.bfloat16, device=W.device)
+        out.append(SplitWeight(planes, N, K))
+        Ns.append(N); Ks.append(K); lds.append(W.stride(0)); trs.append(int(trans))
+        Ws.append(W.data_ptr()); Ps.append(planes.data_ptr())
+    n = len(specs)
+    arr_i = ctypes.c_int * n
+    arr_p = ctypes.c_void_p * n
+    check(lib.hsg_wsplit(n, arr_p(*Ws), arr_i(*Ns), arr_i(*Ks), arr_i(*lds), arr_i(*trs), arr_p(*Ps),
+                         stream_of(specs[0][0])), "hsg_wsplit")
+    return out
+
+
+def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, colsum_part=None):
+    """C = A @ B^T [+ bias] [relu] | * (relu_mask > 0) | + add, with B a SplitWeight
+    (hsg_gemm_f32_psw; fp32-accurate as gemm(..., dtype='f32'))."""
+    lib = load()
+    if not A.is_cuda or A.dtype != torch.float32:
+        raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
+    M, K = A.shape
+    if K != Bs.K:
+        raise ValueError(f"gemm_psw: inner dims {K} != {Bs.K}")
+    N = Bs.N
+    if out is None:
+        out = A.new_empty(M, N)
+    epi, aux = HSG_EPI_STORE, None
+    if relu_mask is not None:
+        epi, aux = HSG_EPI_RELU_BWD, relu_mask
+    elif add is not None:
+        epi, aux = HSG_EPI_ADD, add
+    check(lib.hsg_gemm_f32_psw(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias), ptr(aux),
+                               _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part),
+                               stream_of(A)), "hsg_gemm_f32_psw")
     return out
 
 

@@ -26,7 +26,7 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, row_tiles
+from .dense import gemm, gemm_psw, get_gemm_dtype, row_tiles, split_weights
 
 LN_EPS = 1e-5
 
@@ -43,10 +43,28 @@ def _fused_ok(lib, x, w1, w2):
             and w2.is_contiguous())
 
 
-def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None):
+def ffn_wsplit(x, w1, b1, w2, b2):
+    """The pre-split weight operands (hsg_wsplit: W1, W2 for the forward GEMMs, W2^T,
+    W1^T for dH = dy W2 and dx += dH W1) of an FFN that runs on the GEMM path, or
+    None: the narrow fused FFN, a non-'f32' GEMM mode, shapes hsg_gemm_f32_psw does
+    not take, or HSG_GEMM_PSW=0 (A/B).  Made once per forward of the fused stack and
+    shared by all applications of the layer and their backward."""
+    lib = load()
+    if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
+        return None
+    if get_gemm_dtype() != "f32" or os.environ.get("HSG_GEMM_PSW", "1") == "0":
+        return None
+    d_hid, d = w1.shape
+    if d % 4 or d_hid % 4 or not (w1.is_contiguous() and w2.is_contiguous()):
+        return None
+    return tuple(split_weights((w1, False), (w2, False), (w2, True), (w1, True)))
+
+
+def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wsplit="auto"):
     """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  ``H_out``: a contiguous
     [n, d_hid] buffer for the hidden activations (the fused stack hands in slices of
-    one per-layer buffer).  Returns (out, saved)."""
+    one per-layer buffer).  ``wsplit``: :func:`ffn_wsplit`'s result for these weights
+    ("auto": made here).  Returns (out, saved)."""
     lib = load()
     n, d = x.shape
     out = torch.empty_like(x)
@@ -59,13 +77,19 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None):
         check(lib.hsg_ffn_small_fwd(n, d, w1.shape[0], ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(gamma),
                                     ptr(beta), float(eps), float(p_drop), ptr(seed_t), off, ptr(H), ptr(y),
                                     ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ffn_small_fwd")
-        return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
-    H = gemm(x, w1, b_t=True, bias=b1, relu=True, out=H_out)    # [n, d_hid]
-    y = gemm(H, w2, b_t=True, bias=b2)                     # [n, d]
+        return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, None)
+    if isinstance(wsplit, str):
+        wsplit = ffn_wsplit(x, w1, b1, w2, b2)
+    if wsplit is not None:
+        H = gemm_psw(x, wsplit[0], bias=b1, relu=True, out=H_out)    # [n, d_hid]
+        y = gemm_psw(H, wsplit[1], bias=b2)                      # [n, d]
+    else:
+        H = gemm(x, w1, b_t=True, bias=b1, relu=True, out=H_out)
+        y = gemm(H, w2, b_t=True, bias=b2)
     seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
     check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
                          ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
-    return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off)
+    return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
 
 
 def ffn_bwd(saved, dout, dst, act_grads=None):
@@ -77,7 +101,7 @@ def ffn_bwd(saved, dout, dst, act_grads=None):
     dw2 = dy^T H) are then left to the caller, which runs them once over all
     applications of a layer (pass dw1 = dw2 = None).  Returns dx (a fresh tensor)."""
     lib = load()
-    x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off = saved
+    x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off, wsplit = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
     dout = dout.contiguous()
     n, d = x.shape
@@ -101,9 +125,14 @@ def ffn_bwd(saved, dout, dst, act_grads=None):
                              ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
         rt = row_tiles(n, d_hid, d)
         hpart = x.new_empty(rt, d_hid)
-        dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart,   # [n, d_hid] + db1 partials
-                  out=act_grads[1] if act_grads is not None else None)
-        gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
+        dH_out = act_grads[1] if act_grads is not None else None
+        if wsplit is not None:
+            dH = gemm_psw(dy, wsplit[2], relu_mask=H, colsum_part=hpart, out=dH_out)
+            gemm_psw(dH, wsplit[3], out=dx, add=dx)
+        else:
+            dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart,   # [n, d_hid] + db1 partials
+                      out=dH_out)
+            gemm(dH, w1, out=dx, add=dx)                                  # dx += dH W1
     if dw2 is not None:
         gemm(dy, H, a_t=True, out=dw2, add=dw2 if acc_w2 else None)  # [d, d_hid]
     if dw1 is not None:

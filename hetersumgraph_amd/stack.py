@@ -35,7 +35,7 @@ import os
 import torch
 
 from .dense import gemm
-from .ffn import ffn_bwd, ffn_fwd
+from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import hproj_bwd, hproj_fwd
 from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
                   gat_table_fwd)
@@ -98,11 +98,12 @@ class _Layer:
                             self.gamma, self.beta) if p is not None]
 
 
-def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None):
+def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None, wsplit="auto"):
     """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59.
     ``tables``: the layer's (a1, tau) from :func:`ops.attn_tables`, shared by its
     applications within one forward; ``x_out`` / ``H_out``: this application's slots
-    of the layer's FFN-input and hidden-activation buffers."""
+    of the layer's FFN-input and hidden-activation buffers; ``wsplit``: the layer's
+    pre-split FFN weights (ffn.ffn_wsplit), likewise shared."""
     H, D = lay.H, lay.D
     sigma = None
     if lay.p_attn > 0 and tables is not None:     # source logits from the projection's epilogue
@@ -115,7 +116,7 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
                               out=x_out, sigma=sigma)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
-                          lay.p_ffn, lay.eps, H_out=H_out)
+                          lay.p_ffn, lay.eps, H_out=H_out, wsplit=wsplit)
     return out, (hsaved, neighbor, gsaved, fsaved)
 
 
@@ -181,7 +182,7 @@ class _GatStack(torch.autograd.Function):
         # into one [applications, rows, width] buffer per layer, so the backward runs
         # each FFN weight gradient as ONE GEMM over all applications' rows
         n_app = {id(w2s): n_iter + 1, id(s2w): n_iter}
-        bufs, slot = {}, {id(w2s): 0, id(s2w): 0}
+        bufs, slot, wsplits = {}, {id(w2s): 0, id(s2w): 0}, {}
 
         def run(lay, rel, nb, org, outk):
             key = id(lay)
@@ -189,10 +190,13 @@ class _GatStack(torch.autograd.Function):
                 d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
                 bufs[key] = (states[org].new_empty(n_app[key], rel.n_dst, d),
                              states[org].new_empty(n_app[key], rel.n_dst, d_hid))
+                # the FFN weights split into limb planes once per forward (hsg_wsplit)
+                wsplits[key] = ffn_wsplit(bufs[key][0][0], lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid),
+                                          lay.b2)
             a = slot[key]
             slot[key] += 1
             out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],
-                                    H_out=bufs[key][1][a])
+                                    H_out=bufs[key][1][a], wsplit=wsplits[key])
             states[outk] = out
             apps.append((lay, saved, nb, org, a))
 

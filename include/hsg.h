@@ -168,6 +168,21 @@ int hsg_gemm_f32_mfma(int M, int N, int K, const float *A, int lda, int a_kconti
                       const float *B, int ldb, int b_kcontig, float *C, int ldc,
                       const float *bias, const float *aux, int ldaux, int epi, int relu,
                       int splits, float *workspace, float *colsum_part, void *stream);
+/* Pre-split weights (the FFN's W1, W2 and their transposes, SURVEY §8a step 4:
+ * reference module/PositionwiseFeedForward.py:23-34 w_1/w_2).  hsg_wsplit writes, for
+ * each of njobs (1..4) weights, the three bf16 limb planes of the [N][K] matrix
+ * B = trans ? W^T : W (W row pitch ldw floats) into planes[q] = bf16 [3][Np][Kp]
+ * (hsg_wsplit_dims: Np = N rounded up to 128, Kp = K rounded up to 32, zero padded),
+ * limbs as hsg_gemm_f32's split.  hsg_gemm_f32_psw is hsg_gemm_f32 for
+ * C = A B^T with a K-contiguous fp32 A (K % 4 == 0) and B given by its planes: the
+ * weight is split once per step instead of once per row tile of every GEMM.  Same
+ * epilogues and colsum_part rows (hsg_gemm_row_tiles) as hsg_gemm_f32, no split-K. */
+void hsg_wsplit_dims(int N, int K, int *Np, int *Kp);
+int hsg_wsplit(int njobs, const float *const *W, const int *N, const int *K, const int *ldw,
+               const int *trans, void *const *planes, void *stream);
+int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *planes,
+                     float *C, int ldc, const float *bias, const float *aux, int ldaux,
+                     int epi, int relu, float *colsum_part, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,

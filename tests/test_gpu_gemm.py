@@ -158,3 +158,66 @@ def test_split_is_fp32_class(M, N, K, a_t, b_t):
         e[dt] = ((C.double() - ref).abs() / unit).max().item()
     print(f"{M}x{N}x{K}: split {e['f32']:.2e}, f32 mfma {e['f32mfma']:.2e}")
     assert e["f32"] <= 1.5 * e["f32mfma"] + 1e-8 and e["f32"] < 2e-6
+
+
+# ---- hsg_wsplit + hsg_gemm_f32_psw: pre-split weight operand ----------------------
+PSW_SHAPES = [(1, 1, 4), (33, 17, 20), (130, 300, 300), (777, 512, 300), (1000, 300, 512), (257, 64, 300),
+              (19200, 512, 300)]
+
+
+@pytest.mark.parametrize("plan", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("M,N,K", PSW_SHAPES)
+@pytest.mark.parametrize("trans", [False, True])
+def test_psw_layouts(M, N, K, trans, plan, monkeypatch):
+    """Every tile plan, row/column/K tails, both weight orientations: fp32-class error
+    against fp64 (the same bound as hsg_gemm_f32's test_layouts)."""
+    from hetersumgraph_amd.dense import gemm_psw, split_weights
+    monkeypatch.setenv("HSG_GEMM5", plan)
+    torch.manual_seed(M + N + K)
+    A = mk(M, K)
+    W = mk(K, N) if trans else mk(N, K)
+    (S,) = split_weights((W, trans))
+    C = gemm_psw(A, S)
+    R = A.double() @ (W.double() if trans else W.double().t())
+    err = (C.double() - R).abs().max().item()
+    assert err <= 1e-5 * max(1.0, K ** 0.5) * 4, err
+
+
+def test_psw_epilogues_and_colsums():
+    from hetersumgraph_amd.dense import gemm, gemm_psw, row_tiles, split_weights
+    torch.manual_seed(1)
+    X = torch.randn(777, 300, device="cuda")
+    W1 = torch.randn(512, 300, device="cuda")
+    W2 = torch.randn(300, 512, device="cuda")
+    b = torch.randn(512, device="cuda")
+    s1, s2t, s1t = split_weights((W1, False), (W2, True), (W1, True))
+    H = gemm_psw(X, s1, bias=b, relu=True)
+    Hr = torch.relu(X.double() @ W1.double().t() + b.double())
+    assert (H.double() - Hr).abs().max().item() < 1e-4
+    G = torch.randn(777, 300, device="cuda")
+    hpart = torch.zeros(row_tiles(777, 512, 300) * 512, device="cuda")
+    dH = gemm_psw(G, s2t, relu_mask=H, colsum_part=hpart)
+    dHr = (G.double() @ W2.double()) * (Hr > 0)
+    assert (dH.double() - dHr).abs().max().item() < 1e-4
+    # 64-row column partials, as hsg_gemm_f32 writes them
+    hpart_ref = torch.zeros_like(hpart)
+    gemm(G, W2, relu_mask=H, splits=1, colsum_part=hpart_ref)
+    assert torch.allclose(hpart.view(-1, 512).sum(0), hpart_ref.view(-1, 512).sum(0), rtol=1e-5, atol=1e-3)
+    for t in range(row_tiles(777, 512, 300)):
+        blk = dH[64 * t:64 * (t + 1)].double().sum(0)
+        assert torch.allclose(hpart.view(-1, 512)[t].double(), blk, rtol=1e-6, atol=1e-3)
+    acc = torch.randn(777, 300, device="cuda")
+    acc0 = acc.clone()
+    gemm_psw(dH, s1t, out=acc, add=acc)
+    accr = acc0.double() + dH.double() @ W1.double()
+    assert (acc.double() - accr).abs().max().item() < 2e-3
+
+
+def test_psw_rejects_bad_operands():
+    from hetersumgraph_amd._lib import HSG_EINVAL, load
+    lib = load()
+    A = torch.randn(64, 30, device="cuda")            # K % 4 != 0
+    planes = torch.empty(3 * 128 * 32, dtype=torch.bfloat16, device="cuda")
+    C = torch.empty(64, 64, device="cuda")
+    assert lib.hsg_gemm_f32_psw(64, 64, 30, A.data_ptr(), 30, planes.data_ptr(), C.data_ptr(), 64, None, None,
+                                0, 0, 0, None, None) == HSG_EINVAL

@@ -1,0 +1,55 @@
+"""Dev tool: the S2W FFN GEMMs (forward x.W1^T, h.W2^T; backward dy.W2, dH.W1) on
+hsg_gemm_f32 (k_gemm3) vs hsg_gemm_f32_psw (k_gemm5, pre-split weight) under each
+HSG_GEMM5 plan, plus the hsg_wsplit launch of the four weight views: time (HIP
+events, 20 back-to-back launches) and max error vs fp64 scaled by max |ref|."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights  # noqa: E402
+
+PLANS = {"1": "BN64 S2", "2": "BN128 S2", "3": "BN64 S3", "4": "BN128 S3", "5": "reg BN64", "6": "reg BN128", "7": "BN64 iglp0", "8": "BN64 iglp1"}
+
+
+def timed(f, reps=20):
+    for _ in range(3):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+n, d, dh = int(os.environ.get("ROWS", 19200)), 300, 512
+W1 = torch.randn(dh, d, device="cuda") * 0.05
+W2 = torch.randn(d, dh, device="cuda") * 0.05
+x = torch.randn(n, d, device="cuda")
+H = torch.randn(n, dh, device="cuda")
+dy = torch.randn(n, d, device="cuda")
+us = timed(lambda: split_weights((W1, False), (W2, False), (W2, True), (W1, True)))
+print(f"hsg_wsplit x4: {us:.1f} us", flush=True)
+s1, s2, s2t, s1t = split_weights((W1, False), (W2, False), (W2, True), (W1, True))
+cases = [("ffn1 x.W1^T", x, W1, True, s1), ("ffn2 h.W2^T", H, W2, True, s2),
+         ("dH = dy.W2", dy, W2, False, s2t), ("dx = dH.W1", H, W1, False, s1t)]
+for name, A, W, b_t, S in cases:
+    ref = A.double() @ (W.double().t() if b_t else W.double())
+    M, N = ref.shape
+    K = A.shape[1]
+    out = torch.empty(M, N, device="cuda")
+    us = timed(lambda: gemm(A, W, b_t=b_t, out=out, dtype="f32"))
+    err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"{name:14s} {M}x{N}x{K}  gemm3 {us:6.1f} us {2 * M * N * K / us / 1e6:6.1f} TF err {err:.1e}",
+          flush=True)
+    for g5, tag in PLANS.items():
+        os.environ["HSG_GEMM5"] = g5
+        out.zero_()
+        us = timed(lambda: gemm_psw(A, S, out=out))
+        err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
+        print(f"      {tag:9s} {us:6.1f} us {2 * M * N * K / us / 1e6:6.1f} TF err {err:.1e}", flush=True)
+    os.environ.pop("HSG_GEMM5", None)

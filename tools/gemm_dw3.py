@@ -1,6 +1,7 @@
 """Dev tool: the step's weight-gradient GEMMs (dW = dY^T X, both operands
 M/N-contiguous) on the exact-f32 MFMA kernel vs the 3-limb split kernel with
-transpose-read staging (HSG_GEMM3_DW=1), per split count; HIP-event timed (20
+transpose-read staging under each tile plan (HSG_GEMM3_TILE; VAR 3 = one-limb
+probe of the same pipeline), per split count; HIP-event timed (20
 back-to-back launches) with the max relative error against a float64 product."""
 import os
 import sys
@@ -33,11 +34,20 @@ for name, M, N, K in SHAPES:
     ref = A.double().t() @ B.double()
     out = torch.empty(M, N, device="cuda")
     row = [f"{name:18s}"]
-    for dw3, dt in (("0", "f32mfma"), ("1", "f32")):
-        os.environ["HSG_GEMM3_DW"] = dw3
-        for sp in (0, 8, 16, 32, 64):
+    variants = [("mfma", {}, "f32mfma")] + [(f"x3t{t}{'v' + v if v else ''}", {"HSG_GEMM3_TILE": t, "HSG_GEMM3_VAR": v},
+                                             "f32") for t in ("0", "1", "2", "3") for v in ("", "3")]
+    for tag, env, dt in variants:
+        for k, v in env.items():
+            if v:
+                os.environ[k] = v
+            else:
+                os.environ.pop(k, None)
+        for sp in (0, 16, 32, 64):
             us = timed(lambda: gemm(A, B, a_t=True, out=out, splits=sp, dtype=dt))
             err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
-            row.append(f"{dt}/s{sp}:{us:.0f}us,{err:.1e}")
-    os.environ.pop("HSG_GEMM3_DW", None)
-    print(" ".join(row), flush=True)
+            row.append(f"{tag}/s{sp}:{us:.0f}us,{err:.0e}")
+        for k in env:
+            os.environ.pop(k, None)
+    print(f"{name:18s}", flush=True)
+    for i in range(1, len(row), 4):
+        print("   " + " ".join(row[i:i + 4]), flush=True)
