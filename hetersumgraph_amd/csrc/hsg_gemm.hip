@@ -499,7 +499,7 @@ struct Stage3 {
 // are issued while tile kt is multiplied, two tiles of MFMA work to hide their
 // latency).  Two barriers per K tile.  NL = 1 is a bf16-operand probe of the same
 // pipeline (dev only).  The epilogue (and split-K / column partials) is k_gemm's.
-template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL>
+template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL, int IGLP = -1>
 __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
     constexpr int WM = BM / 2, WN = BN / 2;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -573,6 +573,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
                 }
         }
+        if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
     }
     }
 
@@ -1183,7 +1184,7 @@ int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int BM, int BN, int BK = 32, int PF = 1, int NL = 3>
+template <int BM, int BN, int BK = 32, int PF = 1, int NL = 3, int IGLP = -1>
 int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     const int kt_total = (p.K + BK - 1) / BK;
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
@@ -1191,10 +1192,10 @@ int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
     if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
-    if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL>), grid, dim3(256), 0, st, p);
-    else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
-    else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL>), grid, dim3(256), 0, st, p);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1310,11 +1311,15 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
     if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
         if (!colsum_part) best = atoi(f);
     int rc;
-    // both operands M/N-contiguous (the weight gradients dW = dY^T X): exact-f32 MFMA
-    // unless HSG_GEMM3_DW=1 (dev A/B of the transpose-read split path)
+    // both operands M/N-contiguous (the weight gradients dW = dY^T X): the split path
+    // with transpose-read staging, 64x64 tiles and the iglp_opt(0) interleave
+    // (tools/gemm_dw3.py: 108-114 us against 129-142 us for the exact-f32 MFMA on the
+    // cfg2 S2W shapes); HSG_GEMM3_DW=0 selects the exact-f32 MFMA (A/B)
+    bool dw3 = false;
     if (mode == MODE_F32_SPLIT && !ak && !bk && !getenv("HSG_GEMM3_TILE")) {
         const char *e = getenv("HSG_GEMM3_DW");
-        if (!e || e[0] != '1') mode = MODE_F32_MFMA;
+        if (e && e[0] == '0') mode = MODE_F32_MFMA;
+        else dw3 = true;
     }
     int g4 = 0;                                             // dev switch: k_gemm4 plans
     if (const char *f = getenv("HSG_GEMM4")) g4 = atoi(f);
@@ -1329,7 +1334,8 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
         if (const char *f = getenv("HSG_GEMM3_TILE"))      // dev override
             if (!colsum_part) t3 = atoi(f);
-        int var = 0;                                        // dev variants (tools/gemm3_sweep.py)
+        int var = dw3 ? 5 : 0;                              // dev variants (tools/gemm3_sweep.py)
+        if (dw3) t3 = 0;
         if (const char *f = getenv("HSG_GEMM3_VAR")) var = atoi(f);
         if (var == 1) {                                     // 2-deep register prefetch
             if (t3 == 1) rc = launch3<128, 64, 32, 2>(p, ak, bk, splits, st);
@@ -1343,6 +1349,10 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         } else if (var == 4) {                              // one limb, 2-deep prefetch
             if (t3 == 1) rc = launch3<128, 64, 32, 2, 1>(p, ak, bk, splits, st);
             else rc = launch3<64, 64, 32, 2, 1>(p, ak, bk, splits, st);
+        } else if (var == 5) {                              // iglp_opt(0) interleave
+            if (t3 == 1) rc = launch3<128, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
+            else if (t3 == 3) rc = launch3<128, 128, 32, 1, 3, 0>(p, ak, bk, splits, st);
+            else rc = launch3<64, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
         } else if (t3 == 3) rc = launch3<128, 128>(p, ak, bk, splits, st);
         else if (t3 == 1) rc = launch3<128, 64>(p, ak, bk, splits, st);
         else if (t3 == 2) rc = launch3<64, 128>(p, ak, bk, splits, st);

@@ -35,7 +35,7 @@ for name, M, N, K in SHAPES:
     out = torch.empty(M, N, device="cuda")
     row = [f"{name:18s}"]
     variants = [("mfma", {}, "f32mfma")] + [(f"x3t{t}{'v' + v if v else ''}", {"HSG_GEMM3_TILE": t, "HSG_GEMM3_VAR": v},
-                                             "f32") for t in ("0", "1", "2", "3") for v in ("", "3")]
+                                             "f32") for t in ("0", "1", "3") for v in ("", "5", "3")]
     for tag, env, dt in variants:
         for k, v in env.items():
             if v:
