@@ -958,7 +958,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm5(GemmArgs p, const __bf16 *__re
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0][j], acc[j], 0, 0, 0);
         }
-        if constexpr (IGLP >= 0) __builtin_amdgcn_iglp_opt(IGLP);
+        if constexpr (IGLP == 0 || IGLP == 1) __builtin_amdgcn_iglp_opt(IGLP);
     }
 
     float csum[TN];

@@ -70,49 +70,77 @@ __device__ __forceinline__ u32x4v bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // xorshift64 stream (shifts and xors only: 32-bit integer multiplies run at a
 // quarter of the VALU rate on CDNA, and one hash per word instead of per row
 // removes most of them).
-__global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p, const int64_t *seedp,
-                                                  uint32_t offset, uint32_t *__restrict__ bits) {
-    const int NWI = (n + 31) / 32;
-    const int HP = (H + 1) / 2;
-    const int LDC = mask_ldc(in);
+__device__ __forceinline__ uint32_t drop_key(const int64_t *seedp, uint32_t offset) {
     const uint64_t key64 = hsg_mix64((uint64_t)seedp[0] * 0x9E3779B97F4A7C15ull +
                                      (uint64_t)offset * 0xD1B54A32D192ED03ull);
-    const uint32_t key = (uint32_t)key64 ^ (uint32_t)(key64 >> 32);
-    const uint32_t thr = thr16(p);
-    const long total = (long)HP * NWI * LDC;
-    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-        const int c = (int)(t % LDC);
-        const long r = t / LDC;
-        const int iw = (int)(r % NWI);
-        const int kp = (int)(r / NWI);
-        uint32_t b0 = 0, b1 = 0;
-        if (c < in) {
-            const uint32_t w = (uint32_t)(((long)kp * NWI + iw) * in + c);
-            uint64_t x = ((uint64_t)lowbias32(key ^ (w * 0x9E3779B1u)) << 32) |
-                         lowbias32(key + 0x7F4A7C15u + w * 0x85EBCA6Bu);
-            x |= 1ull;                                     // xorshift state must be non-zero
-            const int jmax = min(32, n - iw * 32);
+    return (uint32_t)key64 ^ (uint32_t)(key64 >> 32);
+}
+
+// thread unit t of one mask: (head pair kp, 32-row word iw, column c), c fastest
+__device__ __forceinline__ void dropmask_unit(int n, int in, int H, uint32_t thr, uint32_t key, long t,
+                                              uint32_t *__restrict__ bits) {
+    const int NWI = (n + 31) / 32;
+    const int LDC = mask_ldc(in);
+    const int c = (int)(t % LDC);
+    const long r = t / LDC;
+    const int iw = (int)(r % NWI);
+    const int kp = (int)(r / NWI);
+    uint32_t b0 = 0, b1 = 0;
+    if (c < in) {
+        const uint32_t w = (uint32_t)(((long)kp * NWI + iw) * in + c);
+        uint64_t x = ((uint64_t)lowbias32(key ^ (w * 0x9E3779B1u)) << 32) |
+                     lowbias32(key + 0x7F4A7C15u + w * 0x85EBCA6Bu);
+        x |= 1ull;                                     // xorshift state must be non-zero
+        const int jmax = min(32, n - iw * 32);
 #pragma unroll
-            for (int j0 = 0; j0 < 32; j0 += 2) {
-                x ^= x << 13;
-                x ^= x >> 7;
-                x ^= x << 17;
-                // 4 x 16 bits: rows j0, j0+1 for heads 2kp, 2kp+1
-                const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-                if (j0 < jmax) {
-                    b0 |= (uint32_t)((lo & 0xFFFFu) >= thr) << j0;
-                    b1 |= (uint32_t)((lo >> 16) >= thr) << j0;
-                }
-                if (j0 + 1 < jmax) {
-                    b0 |= (uint32_t)((hi & 0xFFFFu) >= thr) << (j0 + 1);
-                    b1 |= (uint32_t)((hi >> 16) >= thr) << (j0 + 1);
-                }
+        for (int j0 = 0; j0 < 32; j0 += 2) {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            // 4 x 16 bits: rows j0, j0+1 for heads 2kp, 2kp+1
+            const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+            if (j0 < jmax) {
+                b0 |= (uint32_t)((lo & 0xFFFFu) >= thr) << j0;
+                b1 |= (uint32_t)((lo >> 16) >= thr) << j0;
+            }
+            if (j0 + 1 < jmax) {
+                b0 |= (uint32_t)((hi & 0xFFFFu) >= thr) << (j0 + 1);
+                b1 |= (uint32_t)((hi >> 16) >= thr) << (j0 + 1);
             }
         }
-        const int k0 = 2 * kp;
-        bits[((long)k0 * NWI + iw) * LDC + c] = b0;
-        if (k0 + 1 < H) bits[((long)(k0 + 1) * NWI + iw) * LDC + c] = b1;
     }
+    const int k0 = 2 * kp;
+    bits[((long)k0 * NWI + iw) * LDC + c] = b0;
+    if (k0 + 1 < H) bits[((long)(k0 + 1) * NWI + iw) * LDC + c] = b1;
+}
+
+__global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p, const int64_t *seedp,
+                                                  uint32_t offset, uint32_t *__restrict__ bits) {
+    const uint32_t key = drop_key(seedp, offset), thr = thr16(p);
+    const long total = (long)((H + 1) / 2) * ((n + 31) / 32) * mask_ldc(in);
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x)
+        dropmask_unit(n, in, H, thr, key, t, bits);
+}
+
+// Several masks (e.g. every head projection of one fused-stack forward) in one
+// launch: job q owns blocks [start[q], start[q+1]), the same units and bits as
+// hsg_dropmask(n[q], in[q], H[q], p[q], seed, offset[q], bits[q]).
+struct DropJobs {
+    int n[8], in[8], H[8];
+    float p[8];
+    uint32_t offset[8];
+    uint32_t *bits[8];
+    int start[9];
+    int njobs;
+};
+
+__global__ __launch_bounds__(256) void k_dropmask_multi(DropJobs j, const int64_t *seedp) {
+    int q = 0;
+    while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
+    const long t = (long)((int)blockIdx.x - j.start[q]) * 256 + threadIdx.x;
+    const long total = (long)((j.H[q] + 1) / 2) * ((j.n[q] + 31) / 32) * mask_ldc(j.in[q]);
+    if (t >= total) return;
+    dropmask_unit(j.n[q], j.in[q], j.H[q], thr16(j.p[q]), drop_key(seedp, j.offset[q]), t, j.bits[q]);
 }
 
 // ---------------------------------------------------------------- forward ----
@@ -132,7 +160,7 @@ __global__ __launch_bounds__(256) void k_dropmask(int n, int in, int H, float p,
 // 16-lane butterfly over the slot's columns, then the wave's slots of one head are
 // added in slot order.  Needs every head's slots inside one wave's slot group
 // (SG % SPH == 0, checked by the host).
-template <int SG, bool VEC>
+template <int SG, bool VEC, int PF = 1>
 __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, const float *__restrict__ X,
                                                    int ldx, const float *__restrict__ W,
                                                    const uint32_t *__restrict__ bits, float scale,
@@ -176,40 +204,37 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
     f32x4v acc[SG];
 #pragma unroll
     for (int q = 0; q < SG; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
-    int c = 4 * lk;
-    f32x4v xv = load4(rX, xbase, c);
-    f32x4v wv[SG];
-    u32x4v mv[SG];
-#pragma unroll
-    for (int q = 0; q < SG; ++q) {
-        wv[q] = load4(rW, wbase[q], c);
-        mv[q] = loadm(mbase[q], c);
-    }
-    for (int c0 = 0; c0 < in; c0 += 16) {
-        const int cn = c + 16;
-        const f32x4v xn = load4(rX, xbase, cn);
-        f32x4v wn[SG];
-        u32x4v mn[SG];
+    // PF-deep register ring of 16-column chunks: chunk t+PF is requested as soon as
+    // chunk t's MFMAs are issued, so PF chunks of X / W / mask are in flight per wave
+    f32x4v xv[PF], wv[PF][SG];
+    u32x4v mv[PF][SG];
+    auto fetch = [&](int u, int cc) {
+        xv[u] = load4(rX, xbase, cc);
 #pragma unroll
         for (int q = 0; q < SG; ++q) {
-            wn[q] = load4(rW, wbase[q], cn);
-            mn[q] = loadm(mbase[q], cn);
+            wv[u][q] = load4(rW, wbase[q], cc);
+            mv[u][q] = loadm(mbase[q], cc);
         }
+    };
 #pragma unroll
-        for (int q = 0; q < SG; ++q) {               // slots past NS carry zero W
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].x >> ibit) & 1u) ? xv[0] : 0.f, wv[q][0], acc[q],
-                                                          0, 0, 0);
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].y >> ibit) & 1u) ? xv[1] : 0.f, wv[q][1], acc[q],
-                                                          0, 0, 0);
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].z >> ibit) & 1u) ? xv[2] : 0.f, wv[q][2], acc[q],
-                                                          0, 0, 0);
-            acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[q].w >> ibit) & 1u) ? xv[3] : 0.f, wv[q][3], acc[q],
-                                                          0, 0, 0);
+    for (int u = 0; u < PF; ++u) fetch(u, 4 * lk + 16 * u);
+    for (int c0 = 0; c0 < in; c0 += 16 * PF) {
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            if (c0 + 16 * u >= in) break;              // wave-uniform
+#pragma unroll
+            for (int q = 0; q < SG; ++q) {             // slots past NS carry zero W
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[u][q].x >> ibit) & 1u) ? xv[u][0] : 0.f,
+                                                              wv[u][q][0], acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[u][q].y >> ibit) & 1u) ? xv[u][1] : 0.f,
+                                                              wv[u][q][1], acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[u][q].z >> ibit) & 1u) ? xv[u][2] : 0.f,
+                                                              wv[u][q][2], acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[u][q].w >> ibit) & 1u) ? xv[u][3] : 0.f,
+                                                              wv[u][q][3], acc[q], 0, 0, 0);
+            }
+            fetch(u, c0 + 16 * (u + PF) + 4 * lk);     // past `in`: OOB offsets read 0
         }
-        xv = xn;
-#pragma unroll
-        for (int q = 0; q < SG; ++q) { wv[q] = wn[q]; mv[q] = mn[q]; }
-        c = cn;
     }
     // D layout: col = lane & 15 (slot output j), row = (lane >> 4) * 4 + r
 #pragma unroll
@@ -557,6 +582,24 @@ int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t of
     return status();
 }
 
+int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
+                       const uint32_t *offset, uint32_t *const *bits, void *stream) {
+    if (njobs < 1 || njobs > 8 || !seed) return HSG_EINVAL;
+    DropJobs j{};
+    j.njobs = njobs;
+    j.start[0] = 0;
+    for (int q = 0; q < njobs; ++q) {
+        if (n[q] < 0 || in[q] < 1 || H[q] < 1 || p[q] < 0.f || p[q] >= 1.f || !bits[q]) return HSG_EINVAL;
+        if ((long)n[q] * in[q] * ((H[q] + 1) / 2) >= (1L << 32)) return HSG_EINVAL;
+        j.n[q] = n[q]; j.in[q] = in[q]; j.H[q] = H[q]; j.p[q] = p[q]; j.offset[q] = offset[q]; j.bits[q] = bits[q];
+        const long total = (long)((H[q] + 1) / 2) * ((n[q] + 31) / 32) * mask_ldc(in[q]);
+        j.start[q + 1] = j.start[q] + (int)((total + 255) / 256);
+    }
+    if (j.start[njobs] == 0) return 0;
+    hipLaunchKernelGGL(k_dropmask_multi, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j, seed);
+    return status();
+}
+
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W, const uint32_t *bits,
                   float p, float *Z, int ldz, void *stream) {
     return hsg_hproj_fwd_logits(n, in, H, D, X, ldx, W, bits, p, Z, ldz, nullptr, nullptr, stream);
@@ -583,11 +626,19 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
         const int v = atoi(e);
         sg = (v == 1 && sph == 1) ? 1 : (v == 2 && sph <= 2) ? 2 : 4;
     }
+    int pf = 1;                                                                       // register ring depth (2, 4: no gain, tools/ab.py)
+    if (const char *e = getenv("HSG_HPROJ_PF")) pf = atoi(e);                         // dev A/B (1, 2, 4)
 #define HSG_HF(SG_)                                                                                              \
     {                                                                                                            \
         const long tasks = (long)((n + 15) / 16) * ((ns + SG_ - 1) / SG_);                                       \
         const dim3 grid((unsigned)((tasks + 3) / 4));                                                            \
-        if (vec)                                                                                                 \
+        if (vec && pf == 4)                                                                                      \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 4>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, \
+                               X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
+        else if (vec && pf == 2)                                                                                 \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 2>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, \
+                               X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
+        else if (vec)                                                                                            \
             hipLaunchKernelGGL((k_hproj_fwd<SG_, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, \
                                ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
         else                                                                                                     \

@@ -43,6 +43,12 @@ def _fused_ok(lib, x, w1, w2):
             and w2.is_contiguous())
 
 
+def _draw(x, p_drop, rng):
+    if p_drop <= 0:
+        return None, 0
+    return rng if rng is not None else hsg_rng.get(x.device).take()
+
+
 def ffn_wsplit(x, w1, b1, w2, b2):
     """The pre-split weight operands (hsg_wsplit: W1, W2 for the forward GEMMs, W2^T,
     W1^T for dH = dy W2 and dx += dH W1) of an FFN that runs on the GEMM path, or
@@ -60,11 +66,12 @@ def ffn_wsplit(x, w1, b1, w2, b2):
     return tuple(split_weights((w1, False), (w2, False), (w2, True), (w1, True)))
 
 
-def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wsplit="auto"):
+def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wsplit="auto", rng=None):
     """x [n, d] contiguous, w1 [d_hid, d], w2 [d, d_hid].  ``H_out``: a contiguous
     [n, d_hid] buffer for the hidden activations (the fused stack hands in slices of
     one per-layer buffer).  ``wsplit``: :func:`ffn_wsplit`'s result for these weights
-    ("auto": made here).  Returns (out, saved)."""
+    ("auto": made here).  ``rng``: the dropout's (seed, offset), already drawn by
+    the caller (default: drawn here).  Returns (out, saved)."""
     lib = load()
     n, d = x.shape
     out = torch.empty_like(x)
@@ -73,7 +80,7 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
         H = H_out if H_out is not None else x.new_empty(n, w1.shape[0])
         y = torch.empty_like(x)
-        seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
+        seed_t, off = _draw(x, p_drop, rng)
         check(lib.hsg_ffn_small_fwd(n, d, w1.shape[0], ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(gamma),
                                     ptr(beta), float(eps), float(p_drop), ptr(seed_t), off, ptr(H), ptr(y),
                                     ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ffn_small_fwd")
@@ -86,7 +93,7 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     else:
         H = gemm(x, w1, b_t=True, bias=b1, relu=True, out=H_out)
         y = gemm(H, w2, b_t=True, bias=b2)
-    seed_t, off = (hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0))
+    seed_t, off = _draw(x, p_drop, rng)
     check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
                          ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
     return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)

@@ -15,20 +15,52 @@ from __future__ import annotations
 import torch
 
 from . import rng as hsg_rng
+import ctypes
+
 from ._lib import check, load, ptr, stream_of
 
 
-def hproj_fwd(X, W, H, D, p, a1=None):
+def dropmasks(jobs, device, stream_of_t):
+    """Keep-mask bits of several head projections in ONE launch
+    (hsg_dropmask_multi): ``jobs`` = [(n, d_in, H, p, seed_t, offset)] with one
+    shared seed tensor; returns the bit tensors, each as hsg_dropmask would draw it."""
+    lib = load()
+    if not jobs:
+        return []
+    if len({id(j[4]) for j in jobs}) != 1:
+        raise ValueError("dropmasks: one seed tensor per batch")
+    out = []
+    k = len(jobs)
+    ns, ins, hs = (ctypes.c_int * k)(), (ctypes.c_int * k)(), (ctypes.c_int * k)()
+    ps, offs, bp = (ctypes.c_float * k)(), (ctypes.c_uint32 * k)(), (ctypes.c_void_p * k)()
+    for q, (n, d_in, H, p, _, off) in enumerate(jobs):
+        b = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=device)
+        out.append(b)
+        ns[q], ins[q], hs[q], ps[q], offs[q], bp[q] = n, d_in, H, float(p), off, b.data_ptr()
+    for q0 in range(0, k, 8):
+        q1 = min(k, q0 + 8)
+        sl = slice(q0, q1)
+        m = q1 - q0
+        check(lib.hsg_dropmask_multi(m, (ctypes.c_int * m)(*ns[sl]), (ctypes.c_int * m)(*ins[sl]),
+                                     (ctypes.c_int * m)(*hs[sl]), (ctypes.c_float * m)(*ps[sl]),
+                                     ptr(jobs[0][4]), (ctypes.c_uint32 * m)(*offs[sl]),
+                                     (ctypes.c_void_p * m)(*bp[sl]), stream_of_t), "hsg_dropmask_multi")
+    return out
+
+
+def hproj_fwd(X, W, H, D, p, a1=None, bits=None):
     """Z [n, H*D] and the state its backward needs.  X, W contiguous fp32.  With
     ``a1`` [H, D] (the attention's source part), also the source logits
     sigma [n, H] from the same launch: returns (Z, saved, sigma); sigma is None when
-    the fused form does not cover (H, D) (the caller computes it separately)."""
+    the fused form does not cover (H, D) (the caller computes it separately).
+    ``bits``: keep-masks already drawn for this call (:func:`dropmasks`)."""
     lib = load()
     n, d_in = X.shape
     st = stream_of(X)
-    seed_t, off = hsg_rng.get(X.device).take()
-    bits = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=X.device)
-    check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
+    if bits is None:
+        seed_t, off = hsg_rng.get(X.device).take()
+        bits = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=X.device)
+        check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
     Z = X.new_empty(n, H * D)
     saved = (X, W, bits, H, D, float(p))
     if a1 is not None:

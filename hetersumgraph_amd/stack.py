@@ -34,9 +34,11 @@ import os
 
 import torch
 
+from . import rng as hsg_rng
+from ._lib import stream_of
 from .dense import gemm
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
-from .hproj import hproj_bwd, hproj_fwd
+from .hproj import dropmasks, hproj_bwd, hproj_fwd
 from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
                   gat_table_fwd)
 
@@ -98,25 +100,27 @@ class _Layer:
                             self.gamma, self.beta) if p is not None]
 
 
-def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None, wsplit="auto"):
+def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None, wsplit="auto", draws=(None, None)):
     """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59.
     ``tables``: the layer's (a1, tau) from :func:`ops.attn_tables`, shared by its
     applications within one forward; ``x_out`` / ``H_out``: this application's slots
     of the layer's FFN-input and hidden-activation buffers; ``wsplit``: the layer's
-    pre-split FFN weights (ffn.ffn_wsplit), likewise shared."""
+    pre-split FFN weights (ffn.ffn_wsplit), likewise shared; ``draws`` = (head
+    projection keep-mask bits, FFN dropout (seed, offset)) drawn up front by the
+    caller, or None each (drawn here)."""
     H, D = lay.H, lay.D
     sigma = None
     if lay.p_attn > 0 and tables is not None:     # source logits from the projection's epilogue
-        Z, hsaved, sigma = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, a1=tables[0])
+        Z, hsaved, sigma = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, a1=tables[0], bits=draws[0])
     elif lay.p_attn > 0:
-        Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn)
+        Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, bits=draws[0])
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
                               out=x_out, sigma=sigma)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
-                          lay.p_ffn, lay.eps, H_out=H_out, wsplit=wsplit)
+                          lay.p_ffn, lay.eps, H_out=H_out, wsplit=wsplit, rng=draws[1])
     return out, (hsaved, neighbor, gsaved, fsaved)
 
 
@@ -184,6 +188,24 @@ class _GatStack(torch.autograd.Function):
         n_app = {id(w2s): n_iter + 1, id(s2w): n_iter}
         bufs, slot, wsplits = {}, {id(w2s): 0, id(s2w): 0}, {}
 
+        # every dropout draw of the forward, in the order the layer-by-layer path takes
+        # them (per application: head projection, then FFN), so both paths see the
+        # same masks; the head-projection keep-masks are then made in ONE launch
+        seq = [(w2s, rw)] + [(s2w, rs), (w2s, rw)] * n_iter
+        gen = hsg_rng.get(w0.device)
+        draws = []
+        for lay, _ in seq:
+            hm = gen.take() if lay.p_attn > 0 else None
+            fr = gen.take() if lay.p_ffn > 0 else None
+            draws.append([hm, fr])
+        jobs = [(rel.n_src, lay.W.shape[1], lay.H, lay.p_attn, d[0][0], d[0][1])
+                for (lay, rel), d in zip(seq, draws) if d[0] is not None]
+        masks = iter(dropmasks(jobs, w0.device, stream_of(w0)))
+        for d in draws:
+            if d[0] is not None:
+                d[0] = next(masks)
+        napp = [0]
+
         def run(lay, rel, nb, org, outk):
             key = id(lay)
             if key not in bufs:
@@ -196,7 +218,8 @@ class _GatStack(torch.autograd.Function):
             a = slot[key]
             slot[key] += 1
             out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],
-                                    H_out=bufs[key][1][a], wsplit=wsplits[key])
+                                    H_out=bufs[key][1][a], wsplit=wsplits[key], draws=draws[napp[0]])
+            napp[0] += 1
             states[outk] = out
             apps.append((lay, saved, nb, org, a))
 

@@ -260,6 +260,11 @@ int hsg_dropmask_words(int n, int in, int H);
 float hsg_dropmask_scale(float p);
 int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t offset, uint32_t *bits,
                  void *stream);
+/* njobs (1..8) masks in one launch, job q identical to
+ * hsg_dropmask(n[q], in[q], H[q], p[q], seed, offset[q], bits[q]): the fused stack draws
+ * the masks of all its head projections up front. */
+int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, const float *p,
+                       const int64_t *seed, const uint32_t *offset, uint32_t *const *bits, void *stream);
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                   const uint32_t *bits, float p, float *Z, int ldz, void *stream);
 /* hsg_hproj_fwd plus the attention's source logits sigma[i][k] = <Z[i, kD:(k+1)D], a1[k]>

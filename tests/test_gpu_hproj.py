@@ -89,3 +89,20 @@ def test_fused_source_logits_match_split_kernel(n, d_in, H, D):
     torch.cuda.synchronize()
     tol = 1e-5 * max(1.0, ref.abs().max().item())
     assert (sigma - ref).abs().max().item() <= tol
+
+
+def test_batched_dropmask_equals_single_launches():
+    """hsg_dropmask_multi (the fused stack's one launch for all its head projections)
+    draws bit-for-bit the masks of one hsg_dropmask launch per job."""
+    from hetersumgraph_amd._lib import load, ptr, stream_of
+    from hetersumgraph_amd.hproj import dropmasks
+    lib = load()
+    seed = torch.tensor([12345], dtype=torch.int64, device="cuda")
+    jobs = [(19200, 300, 8, 0.1, seed, 3), (1120, 64, 6, 0.1, seed, 5), (777, 33, 3, 0.4, seed, 9),
+            (1, 1, 1, 0.5, seed, 11), (40, 300, 8, 0.0, seed, 12)]
+    got = dropmasks(jobs, torch.device("cuda"), None)
+    for (n, d_in, H, p, s, off), g in zip(jobs, got):
+        ref = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device="cuda")
+        assert lib.hsg_dropmask(n, d_in, H, float(p), ptr(s), off, ptr(ref), None) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(g, ref), (n, d_in, H, p, off)
