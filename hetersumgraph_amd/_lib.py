@@ -28,7 +28,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
-           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi")
+           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -96,6 +96,8 @@ _SIGS = {
     "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_wsplit_dims": [_I, _I, _P, _P],
     "hsg_dropmask_multi": [_I, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gemm_f32_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
+    "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_wsplit": [_I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
 }

@@ -1289,7 +1289,7 @@ enum { MODE_F32_MFMA = 0, MODE_BF16 = 1, MODE_F32_SPLIT = 2 };
 
 int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
               int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
-              int relu, int splits, float *workspace, float *colsum_part, void *stream) {
+              int relu, int splits, float *workspace, float *colsum_part, void *stream, bool slabs_only = false) {
     if (M < 0 || N < 0 || K < 0 || !C) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
@@ -1374,7 +1374,7 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
     else if (best == 10) rc = launch_tiles<64, 128, 1>(p, ak, bk, splits, st);
     else if (best == 11) rc = launch_tiles<64, 128, 2>(p, ak, bk, splits, st);
     else rc = launch_tiles<128, 128, 1, 64>(p, ak, bk, splits, st);
-    if (rc || splits == 1) return rc;
+    if (rc || splits == 1 || slabs_only) return rc;
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
@@ -1395,6 +1395,91 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
         if (e[0] == 'm') mode = MODE_F32_MFMA;
     return gemm_impl(mode, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
+}
+
+int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                       int b_kcontig, int splits, float *workspace, void *stream) {
+    const int kt_total = (K + kBK - 1) / kBK;
+    if (splits < 2 || splits > kt_total || !workspace) return HSG_EINVAL;
+    float dummy_c;
+    return gemm_impl(MODE_F32_SPLIT, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, &dummy_c, N, nullptr, nullptr, 0,
+                     HSG_EPI_STORE, 0, splits, workspace, nullptr, stream, true);
+}
+
+// ---------------------------------------------------------------------------------
+// Deferred column sums: many outputs in one launch.  Job q: for c < cols[q],
+//   out[q][c] = (accumulate[q] ? out[q][c] : 0) + scale[q] * sum_s sum_r part_s[r*pitch + coff + c]
+// over its segments s (in order) and their rows r (8 row groups per column, group
+// sums added in order): deterministic.  Block = 32 columns x 8 row groups; job q owns
+// blocks [start[q], start[q+1]).
+// ---------------------------------------------------------------------------------
+constexpr int kRedJobs = 24, kRedSegs = 4;
+struct RedJobs {
+    float *out[kRedJobs];
+    const float *seg[kRedJobs][kRedSegs];
+    int rows[kRedJobs][kRedSegs];
+    int nseg[kRedJobs], cols[kRedJobs], pitch[kRedJobs], coff[kRedJobs], acc[kRedJobs];
+    float scale[kRedJobs];
+    int start[kRedJobs + 1];
+    int njobs;
+};
+
+__global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
+    __shared__ float red[8][33];
+    int q = 0;
+    while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
+    const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int c = ((int)blockIdx.x - j.start[q]) * 32 + cl;
+    const int pitch = j.pitch[q], coff = j.coff[q];
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c < j.cols[q]) {
+        for (int sg = 0; sg < j.nseg[q]; ++sg) {
+            const float *P = j.seg[q][sg] + coff + c;
+            const int rows = j.rows[q][sg];
+            int r = g;
+            for (; r + 24 < rows; r += 32) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) s[u] += P[(size_t)(r + 8 * u) * pitch];
+            }
+            for (; r < rows; r += 8) s[0] += P[(size_t)r * pitch];
+        }
+    }
+    red[g][cl] = (s[0] + s[1]) + (s[2] + s[3]);
+    __syncthreads();
+    if (g == 0 && c < j.cols[q]) {
+        float a = 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) a += red[u][cl];
+        float *o = j.out[q] + c;
+        *o = j.acc[q] ? *o + j.scale[q] * a : j.scale[q] * a;
+    }
+}
+
+int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *pitch, const int *coff,
+                    const float *scale, const int *accumulate, const int *nseg, const float *const *seg,
+                    const int *seg_rows, void *stream) {
+    if (njobs < 1 || njobs > kRedJobs) return HSG_EINVAL;
+    RedJobs j{};
+    j.njobs = njobs;
+    j.start[0] = 0;
+    int si = 0;
+    for (int q = 0; q < njobs; ++q) {
+        if (!out[q] || cols[q] < 0 || nseg[q] < 1 || nseg[q] > kRedSegs || coff[q] < 0 || pitch[q] < coff[q] + cols[q])
+            return HSG_EINVAL;
+        j.out[q] = out[q];
+        j.cols[q] = cols[q]; j.pitch[q] = pitch[q]; j.coff[q] = coff[q];
+        j.scale[q] = scale[q]; j.acc[q] = accumulate[q] != 0; j.nseg[q] = nseg[q];
+        for (int sg = 0; sg < nseg[q]; ++sg, ++si) {
+            if (seg_rows[si] < 0 || (seg_rows[si] > 0 && !seg[si])) return HSG_EINVAL;
+            j.seg[q][sg] = seg[si];
+            j.rows[q][sg] = seg_rows[si];
+        }
+        j.start[q + 1] = j.start[q] + (cols[q] + 31) / 32;
+    }
+    if (j.start[njobs] == 0) return 0;
+    hipLaunchKernelGGL(k_slab_reduce, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
 }
 
 int hsg_gemm_f32_mfma(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,

@@ -690,7 +690,7 @@ int hsg_hproj_dw_chunks(int n, int in, int H, int D) {
 
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
                  const uint32_t *bits, float p, float *part, float *dW, int accumulate, void *stream) {
-    if (n < 0 || in < 1 || H < 1 || D < 1 || !part || !dW || ldx < in || ldz < H * D ||
+    if (n < 0 || in < 1 || H < 1 || D < 1 || !part || ldx < in || ldz < H * D ||
         !fits_buffers(n, in, H, D, ldx > ldz ? ldx : ldz))
         return HSG_EINVAL;
     hipStream_t st = (hipStream_t)stream;
@@ -702,6 +702,7 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         int rc = status();
         if (rc) return rc;
     }
+    if (!dW) return n > 0 ? 0 : HSG_EINVAL;            // partial slabs only (hsg_slab_reduce sums them)
     int blocks = (int)((total + 255) / 256);
     if (blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(k_sum_parts, dim3(blocks), dim3(256), 0, st, total, n > 0 ? g.chunks : 0, drop_scale(p),

@@ -161,6 +161,26 @@ def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, c
     return out
 
 
+def gemm_slabs(A, B, a_t=False, b_t=False):
+    """The split-K partial products of op(A) @ op(B) (hsg_gemm_f32_slabs, 'f32' mode):
+    (workspace [splits*M*N], splits), summed later by hsg_slab_reduce -- or None when
+    the automatic plan does not split this shape or the GEMM mode is not 'f32'."""
+    lib = load()
+    if _GEMM_DTYPE != "f32" or not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
+        return None
+    M, K = (A.shape[1], A.shape[0]) if a_t else (A.shape[0], A.shape[1])
+    K2, N = (B.shape[1], B.shape[0]) if b_t else (B.shape[0], B.shape[1])
+    if K != K2:
+        raise ValueError(f"gemm_slabs: inner dims {K} != {K2}")
+    splits = auto_splits(M, N, K)
+    if splits < 2:
+        return None
+    ws = A.new_empty(lib.hsg_gemm_workspace_floats(M, N, K, splits))
+    check(lib.hsg_gemm_f32_slabs(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), splits, ptr(ws),
+                                 stream_of(A)), "hsg_gemm_f32_slabs")
+    return ws, splits
+
+
 def auto_splits(M, N, K):
     """hsg_gemm_f32's splits == 0 plan (so the workspace can be sized)."""
     return load().hsg_gemm_auto_splits(M, N, K)

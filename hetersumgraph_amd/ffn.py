@@ -99,14 +99,17 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
 
 
-def ffn_bwd(saved, dout, dst, act_grads=None):
+def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
     """Backward of :func:`ffn_fwd`.  ``dst`` = (dw1, acc_w1, dw2, acc_w2, db1, db2,
     dgamma, dbeta, acc_b): gradient buffers shaped [d_hid, d], [d, d_hid], [d_hid],
     [d], [d], [d] (None when not needed), each written or -- with its accumulate
     flag -- added into.  ``act_grads`` = (dy [n, d], dH [n, d_hid]) contiguous buffers
     that receive the two activation gradients; the weight gradients (dw1 = dH^T x,
     dw2 = dy^T H) are then left to the caller, which runs them once over all
-    applications of a layer (pass dw1 = dw2 = None).  Returns dx (a fresh tensor)."""
+    applications of a layer (pass dw1 = dw2 = None).  ``batch`` (a
+    reduce.SlabBatch) with ``key``: the bias / LayerNorm column sums are recorded
+    there (one job per output across every call with the same key) instead of run
+    here.  Returns dx (a fresh tensor)."""
     lib = load()
     x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off, wsplit = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
@@ -145,6 +148,13 @@ def ffn_bwd(saved, dout, dst, act_grads=None):
     if dw1 is not None:
         gemm(dH, x, a_t=True, out=dw1, add=dw1 if acc_w1 else None)  # [d_hid, d]
     outs = [db1, dg, dbt, db2]
+    if batch is not None:
+        if db1 is not None:
+            batch.add((key, "b1"), db1, d_hid, d_hid, 0, 1.0, acc, hpart, rt)
+        for o, name, off in ((dg, "g", 0), (dbt, "bt", d), (db2, "b2", 2 * d)):
+            if o is not None:
+                batch.add((key, name), o, d, 3 * d, off, 1.0, acc, part, nb)
+        return dx
     if any(o is not None for o in outs):
         db1, dg, dbt, db2 = [o if o is not None else x.new_empty(n_)
                              for o, n_ in zip(outs, (d_hid, d, d, d))]   # scratch for unneeded ones

@@ -77,9 +77,11 @@ def hproj_fwd(X, W, H, D, p, a1=None, bits=None):
     return Z, saved
 
 
-def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False):
+def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False, batch=None, key=None):
     """dX (into ``dX`` -- written or, with dX_acc, added) and dW (same, into ``dW``).
-    Either destination may be None (that gradient is skipped)."""
+    Either destination may be None (that gradient is skipped).  ``batch`` (a
+    reduce.SlabBatch) with ``key``: dW's partial slabs are recorded there and summed
+    with every other call of the same key in the batch's one launch."""
     lib = load()
     X, W, bits, H, D, p = saved
     dZ = dZ.contiguous()
@@ -89,9 +91,16 @@ def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False):
         check(lib.hsg_hproj_dx(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(bits), p, ptr(dX), d_in, int(dX_acc), st),
               "hsg_hproj_dx")
     if dW is not None:
-        part = X.new_empty(lib.hsg_hproj_dw_chunks(n, d_in, H, D) * H * D * d_in)
-        check(lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), p, ptr(part), ptr(dW),
-                               int(dW_acc), st), "hsg_hproj_dw")
+        chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+        part = X.new_empty(chunks * H * D * d_in)
+        if batch is not None and n > 0:
+            check(lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), p, ptr(part), None,
+                                   0, st), "hsg_hproj_dw")
+            batch.add((key, "W"), dW.view(-1), H * D * d_in, H * D * d_in, 0, lib.hsg_dropmask_scale(p), dW_acc,
+                      part, chunks)
+        else:
+            check(lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), p, ptr(part), ptr(dW),
+                                   int(dW_acc), st), "hsg_hproj_dw")
     return dX
 
 

@@ -36,9 +36,10 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import stream_of
-from .dense import gemm
+from .dense import gemm, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd
+from .reduce import SlabBatch
 from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
                   gat_table_fwd)
 
@@ -139,14 +140,16 @@ def _attn_dst(grads, lay, T):
     return dattn, dwf, dbf, dT, a_h, a_T
 
 
-def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None):
+def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None, batch=None):
     """Backward of one application.  Parameter gradients go to ``grads``; the
     neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
     not None.  ``stage`` = (workspace, accumulate): the attention-parameter partials
     only go into the layer's stage workspace (finished once per layer by the caller).
     ``act_grads`` = (dy, dH) slots: the FFN's activation gradients go there and its
     weight gradients are left to the caller (one GEMM per weight over all
-    applications).  Returns the origin's gradient (the FFN's residual-branch dx)."""
+    applications).  ``batch``: a reduce.SlabBatch collecting the column sums of the
+    FFN bias / LayerNorm and head-projection dW partials (summed once per backward).
+    Returns the origin's gradient (the FFN's residual-branch dx)."""
     hsaved, neighbor, gsaved, fsaved = saved
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     if act_grads is None:
@@ -157,7 +160,7 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     (db1, db2, dg, dbt), a_b = grads.group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
                                 dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b),
-                 act_grads=act_grads)
+                 act_grads=act_grads, batch=batch, key=id(lay))
     need_dz = nb_grad is not None or lay.W.requires_grad
     if stage is not None:
         dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage)
@@ -166,7 +169,7 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     if need_dz:
         dW, a_W = grads.dst(lay.W)
         if hsaved is not None:
-            hproj_bwd(hsaved, dZ, dX=nb_grad, dX_acc=nb_acc, dW=dW, dW_acc=a_W)
+            hproj_bwd(hsaved, dZ, dX=nb_grad, dX_acc=nb_acc, dW=dW, dW_acc=a_W, batch=batch, key=id(lay))
         else:                                   # eval-mode projection Z = neighbor W^T
             if nb_grad is not None:
                 gemm(dZ, lay.W, out=nb_grad, add=nb_grad if nb_acc else None)
@@ -250,6 +253,7 @@ class _GatStack(torch.autograd.Function):
         # stage workspace; the parameter transform runs once per layer at the end
         stages, gbufs = {}, {}
         pgrads = _Grads()
+        batch = SlabBatch()
         for lay, saved, nb, org, a in reversed(ctx.apps):
             dout = grads.pop((org[0], org[1] + 1))
             nb_grad, nb_acc = None, False
@@ -268,7 +272,8 @@ class _GatStack(torch.autograd.Function):
                 X, Hh = ctx.bufs[id(lay)]
                 gbufs[id(lay)] = (lay, torch.empty_like(X), torch.empty_like(Hh))
             _, DY, DH = gbufs[id(lay)]
-            dx = _apply_bwd(pgrads, lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]))
+            dx = _apply_bwd(pgrads, lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]),
+                            batch=batch)
             if org in skip:
                 continue
             if org in grads:
@@ -284,14 +289,17 @@ class _GatStack(torch.autograd.Function):
         for lay, DY, DH in gbufs.values():
             X, Hh = ctx.bufs[id(lay)]
             d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
-            dw2, a_w2 = pgrads.dst(lay.w2)
-            if dw2 is not None:
-                gemm(DY.view(-1, d), Hh.view(-1, d_hid), a_t=True, out=dw2.view(d, d_hid),
-                     add=dw2.view(d, d_hid) if a_w2 else None)
-            dw1, a_w1 = pgrads.dst(lay.w1)
-            if dw1 is not None:
-                gemm(DH.view(-1, d_hid), X.view(-1, d), a_t=True, out=dw1.view(d_hid, d),
-                     add=dw1.view(d_hid, d) if a_w1 else None)
+            for p, A, B, (m, n) in ((lay.w2, DY.view(-1, d), Hh.view(-1, d_hid), (d, d_hid)),
+                                    (lay.w1, DH.view(-1, d_hid), X.view(-1, d), (d_hid, d))):
+                dw, a_w = pgrads.dst(p)
+                if dw is None:
+                    continue
+                sl = gemm_slabs(A, B, a_t=True)             # split-K slabs, summed in the batch
+                if sl is not None:
+                    batch.add((id(lay), id(p)), dw.view(-1), m * n, m * n, 0, 1.0, a_w, sl[0], sl[1])
+                else:
+                    gemm(A, B, a_t=True, out=dw.view(m, n), add=dw.view(m, n) if a_w else None)
+        batch.flush()
         ctx.apps = ctx.bufs = None
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None

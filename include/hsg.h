@@ -188,6 +188,21 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
  * bf16).  Products of bf16 values are exact in fp32, so the result equals
  * an fp32 GEMM of the rounded operands up to fp32 summation order. */
+/* hsg_gemm_f32's split-K pass alone: workspace[splits][M][N] receives the K-slice
+ * products, summed by hsg_slab_reduce (splits >= 2). */
+int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig,
+                       const float *B, int ldb, int b_kcontig, int splits, float *workspace,
+                       void *stream);
+/* Deferred column sums of partial slabs, njobs (1..24) outputs in one deterministic
+ * launch: out[q][c] = (accumulate[q] ? out[q][c] : 0) + scale[q] *
+ * sum over job q's nseg[q] (1..4) segments s (in order) and their rows r of
+ * seg_s[r*pitch[q] + coff[q] + c], c < cols[q].  seg / seg_rows list the segments of
+ * all jobs back to back.  The fused stack's backward sums every layer's
+ * head-projection dW slabs, FFN bias / LayerNorm partials and split-K weight
+ * gradients here, once per step, instead of one reduce launch per application. */
+int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *pitch, const int *coff,
+                    const float *scale, const int *accumulate, const int *nseg, const float *const *seg,
+                    const int *seg_rows, void *stream);
 int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig,
                   const float *B, int ldb, int b_kcontig, float *C, int ldc,
                   const float *bias, const float *aux, int ldaux, int epi, int relu,
@@ -278,6 +293,8 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
                  const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);
+/* dW == NULL: only the partial slabs part[chunk][H*D][in] (unscaled), to be summed
+ * with scale hsg_dropmask_scale(p) by hsg_slab_reduce. */
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
                  const uint32_t *bits, float p, float *part, float *dW, int accumulate, void *stream);
 

@@ -221,3 +221,48 @@ def test_psw_rejects_bad_operands():
     C = torch.empty(64, 64, device="cuda")
     assert lib.hsg_gemm_f32_psw(64, 64, 30, A.data_ptr(), 30, planes.data_ptr(), C.data_ptr(), 64, None, None,
                                 0, 0, 0, None, None) == HSG_EINVAL
+
+
+# ---- hsg_gemm_f32_slabs + hsg_slab_reduce (the stack's deferred reductions) ------
+def test_slab_batch_sums_segments_in_one_launch():
+    from hetersumgraph_amd.reduce import SlabBatch
+    torch.manual_seed(3)
+    b = SlabBatch()
+    outs, refs = [], []
+    # job 1: three segments (applications), pitch/offset into a [rows][3][d] slab
+    d = 70
+    parts = [torch.randn(r, 3, d, device="cuda") for r in (5, 17, 1)]
+    for off in range(3):
+        o = torch.full((d,), 7.0, device="cuda")
+        for prt in parts:
+            b.add(("ln", off), o, d, 3 * d, off * d, 1.0, False, prt, prt.shape[0])
+        outs.append(o)
+        refs.append(sum(prt[:, off].double().sum(0) for prt in parts))
+    # job 2: scaled, accumulating, more than 4 segments (chained launches)
+    o2 = torch.randn(1000, device="cuda")
+    base = o2.double().clone()
+    segs = [torch.randn(r, 1000, device="cuda") for r in (3, 9, 1, 4, 2, 8)]
+    for sg in segs:
+        b.add("w", o2, 1000, 1000, 0, 0.5, True, sg, sg.shape[0])
+    b.flush()
+    torch.cuda.synchronize()
+    for o, r in zip(outs, refs):
+        assert torch.allclose(o.double(), r, rtol=1e-5, atol=1e-4)
+    r2 = base + 0.5 * sum(sg.double().sum(0) for sg in segs)
+    assert torch.allclose(o2.double(), r2, rtol=1e-5, atol=1e-4)
+
+
+def test_gemm_slabs_reduce_to_the_product():
+    from hetersumgraph_amd.dense import gemm_slabs
+    from hetersumgraph_amd.reduce import SlabBatch
+    torch.manual_seed(4)
+    A = torch.randn(9000, 300, device="cuda")
+    B = torch.randn(9000, 512, device="cuda")
+    ws, splits = gemm_slabs(A, B, a_t=True)
+    assert splits > 1
+    out = torch.empty(300, 512, device="cuda")
+    b = SlabBatch()
+    b.add("dw", out.view(-1), 300 * 512, 300 * 512, 0, 1.0, False, ws, splits)
+    b.flush()
+    R = A.double().t() @ B.double()
+    assert (out.double() - R).abs().max().item() < 2e-3
