@@ -97,7 +97,7 @@ _SIGS = {
     "hsg_wsplit_dims": [_I, _I, _P, _P],
     "hsg_dropmask_multi": [_I, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
-    "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_wsplit": [_I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
 }

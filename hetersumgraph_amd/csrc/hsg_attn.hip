@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
                                                          const float *__restrict__ bf,
                                                          const float *__restrict__ T, float *__restrict__ dattn,
                                                          float *__restrict__ dwf, float *__restrict__ dbf,
-                                                         float *__restrict__ dT, int accumulate) {
+                                                         float *__restrict__ dT, int accumulate, int srows) {
     __shared__ float wlds[kWfLds];
     __shared__ float a3s[kDMax];
     __shared__ float dv[kFMax];
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
     for (int i = tid; i < NTH; i += nt) {
         float s = 0.f;
 #pragma unroll 16
-        for (int r = 0; r < kStage; ++r) s += dtau_st[r * NTH + i];
+        for (int r = 0; r < srows; ++r) s += dtau_st[r * NTH + i];
         dtau[i] = s;
     }
     __syncthreads();
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
         }
         float g = 0.f;                             // d a1: stage rows in order
 #pragma unroll 16
-        for (int r = 0; r < kStage; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
+        for (int r = 0; r < srows; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
         if (accumulate & 1) {
             dattn[k * D3 + d] += g;
             dattn[k * D3 + 2 * D + d] += s;
@@ -256,8 +256,9 @@ int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const fl
     if (!dims_ok(H, D, F) || !workspace || !attn || !wf || !T || !dattn || !dwf || !dT) return HSG_EINVAL;
     const float *s0 = workspace, *s1 = workspace + (size_t)kStage * kNT * H;
     hipLaunchKernelGGL(k_attn_params_bwd, dim3(H + 1), dim3(256), 0, (hipStream_t)stream, H, D, F, s0, s1, attn, wf,
-                       bf, T, dattn, dwf, dbf, dT, accumulate);
+                       bf, T, dattn, dwf, dbf, dT, accumulate, kStage);
     return status();
 }
+
 
 }  // extern "C"

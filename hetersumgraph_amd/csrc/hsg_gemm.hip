@@ -1407,18 +1407,20 @@ int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcont
 }
 
 // ---------------------------------------------------------------------------------
-// Deferred column sums: many outputs in one launch.  Job q: for c < cols[q],
-//   out[q][c] = (accumulate[q] ? out[q][c] : 0) + scale[q] * sum_s sum_r part_s[r*pitch + coff + c]
-// over its segments s (in order) and their rows r (8 row groups per column, group
-// sums added in order): deterministic.  Block = 32 columns x 8 row groups; job q owns
-// blocks [start[q], start[q+1]).
+// Deferred column sums: many outputs in one launch.  Job q: for c < cols[q] and
+// output row b < out_rows[q],
+//   out[q][b][c] = (accumulate[q] ? out : 0) + scale[q] * sum_s sum_{r in range_b(s)} part_s[r*pitch + coff + c]
+// over its segments s (in order); range_b(s) is the b-th of out_rows[q] equal row
+// ranges of segment s (out_rows > 1: a staged partial for tall, narrow slabs).
+// 8 row groups per column, group sums added in order: deterministic.  Block = 32
+// columns x 8 row groups of one output row; job q owns blocks [start[q], start[q+1]).
 // ---------------------------------------------------------------------------------
 constexpr int kRedJobs = 24, kRedSegs = 4;
 struct RedJobs {
     float *out[kRedJobs];
     const float *seg[kRedJobs][kRedSegs];
     int rows[kRedJobs][kRedSegs];
-    int nseg[kRedJobs], cols[kRedJobs], pitch[kRedJobs], coff[kRedJobs], acc[kRedJobs];
+    int nseg[kRedJobs], cols[kRedJobs], pitch[kRedJobs], coff[kRedJobs], acc[kRedJobs], orows[kRedJobs];
     float scale[kRedJobs];
     int start[kRedJobs + 1];
     int njobs;
@@ -1429,19 +1431,22 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
     int q = 0;
     while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
     const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const int c = ((int)blockIdx.x - j.start[q]) * 32 + cl;
-    const int pitch = j.pitch[q], coff = j.coff[q];
+    const int nbc = (j.cols[q] + 31) / 32, blk = (int)blockIdx.x - j.start[q];
+    const int ob = blk / nbc;                              // output row (row range of every segment)
+    const int c = (blk - ob * nbc) * 32 + cl;
+    const int pitch = j.pitch[q], coff = j.coff[q], orows = j.orows[q];
     float s[4] = {0.f, 0.f, 0.f, 0.f};
     if (c < j.cols[q]) {
         for (int sg = 0; sg < j.nseg[q]; ++sg) {
             const float *P = j.seg[q][sg] + coff + c;
-            const int rows = j.rows[q][sg];
-            int r = g;
-            for (; r + 24 < rows; r += 32) {
+            const int rows = j.rows[q][sg], per = (rows + orows - 1) / orows;
+            const int r1 = min(rows, (ob + 1) * per);
+            int r = ob * per + g;
+            for (; r + 24 < r1; r += 32) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) s[u] += P[(size_t)(r + 8 * u) * pitch];
             }
-            for (; r < rows; r += 8) s[0] += P[(size_t)r * pitch];
+            for (; r < r1; r += 8) s[0] += P[(size_t)r * pitch];
         }
     }
     red[g][cl] = (s[0] + s[1]) + (s[2] + s[3]);
@@ -1450,22 +1455,24 @@ __global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
         float a = 0.f;
 #pragma unroll
         for (int u = 0; u < 8; ++u) a += red[u][cl];
-        float *o = j.out[q] + c;
+        float *o = j.out[q] + (size_t)ob * j.cols[q] + c;
         *o = j.acc[q] ? *o + j.scale[q] * a : j.scale[q] * a;
     }
 }
 
-int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *pitch, const int *coff,
-                    const float *scale, const int *accumulate, const int *nseg, const float *const *seg,
-                    const int *seg_rows, void *stream) {
+int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *out_rows, const int *pitch,
+                    const int *coff, const float *scale, const int *accumulate, const int *nseg,
+                    const float *const *seg, const int *seg_rows, void *stream) {
     if (njobs < 1 || njobs > kRedJobs) return HSG_EINVAL;
     RedJobs j{};
     j.njobs = njobs;
     j.start[0] = 0;
     int si = 0;
     for (int q = 0; q < njobs; ++q) {
-        if (!out[q] || cols[q] < 0 || nseg[q] < 1 || nseg[q] > kRedSegs || coff[q] < 0 || pitch[q] < coff[q] + cols[q])
+        if (!out[q] || cols[q] < 0 || nseg[q] < 1 || nseg[q] > kRedSegs || coff[q] < 0 ||
+            pitch[q] < coff[q] + cols[q] || out_rows[q] < 1)
             return HSG_EINVAL;
+        j.orows[q] = out_rows[q];
         j.out[q] = out[q];
         j.cols[q] = cols[q]; j.pitch[q] = pitch[q]; j.coff[q] = coff[q];
         j.scale[q] = scale[q]; j.acc[q] = accumulate[q] != 0; j.nseg[q] = nseg[q];
@@ -1474,7 +1481,7 @@ int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *pi
             j.seg[q][sg] = seg[si];
             j.rows[q][sg] = seg_rows[si];
         }
-        j.start[q + 1] = j.start[q] + (cols[q] + 31) / 32;
+        j.start[q + 1] = j.start[q] + (cols[q] + 31) / 32 * out_rows[q];
     }
     if (j.start[njobs] == 0) return 0;
     hipLaunchKernelGGL(k_slab_reduce, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);

@@ -177,7 +177,13 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
                               ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
           "hsg_gat_bwd_src")
     _clock_stop(tok, Z)
-    if stage is not None:
+    if stage is not None and len(stage) == 3:       # (batch, key, workspace): staged with every application
+        batch, key, ws = stage
+        nt = (N_BOX + 1) * H
+        rows = ws.numel() // (nt + H * D)                # the workspace's stage rows
+        batch.add((key, "dtau"), ws[:rows * nt], nt, nt, 0, 1.0, False, dtp, nbd, out_rows=rows)
+        batch.add((key, "da1"), ws[rows * nt:], H * D, H * D, 0, 1.0, False, da1p, nbs, out_rows=rows)
+    elif stage is not None:
         ws, acc = stage
         check(lib.hsg_attn_params_stage(H, D, nbd, ptr(dtp), nbs, ptr(da1p), ptr(ws), int(bool(acc)), st),
               "hsg_attn_params_stage")

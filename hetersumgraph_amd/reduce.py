@@ -19,21 +19,23 @@ _MAX_JOBS, _MAX_SEGS = 24, 4
 
 class SlabBatch:
     def __init__(self):
-        self.jobs = {}          # key -> [out, cols, pitch, coff, scale, acc, [(part, rows)]]
+        self.jobs = {}          # key -> [out, cols, pitch, coff, scale, acc, [(part, rows)], out_rows]
         self.order = []
 
-    def add(self, key, out, cols, pitch, coff, scale, acc, part, rows):
-        """Output ``out`` (flat fp32, cols floats) += scale * column sums of
-        part[rows][pitch] at column offset coff.  A repeated ``key`` adds ``part``
-        as one more segment of the same job (out / acc of the first call stand)."""
+    def add(self, key, out, cols, pitch, coff, scale, acc, part, rows, out_rows=1):
+        """Output ``out`` (flat fp32, cols floats; [out_rows][cols] with out_rows > 1,
+        row b summing the b-th of out_rows equal row ranges of every segment) +=
+        scale * column sums of part[rows][pitch] at column offset coff.  A repeated
+        ``key`` adds ``part`` as one more segment of the same job (out / acc of the
+        first call stand)."""
         if rows <= 0:
             return
         j = self.jobs.get(key)
         if j is None:
-            self.jobs[key] = [out, cols, pitch, coff, float(scale), bool(acc), [(part, rows)]]
+            self.jobs[key] = [out, cols, pitch, coff, float(scale), bool(acc), [(part, rows)], int(out_rows)]
             self.order.append(key)
         else:
-            if j[1] != cols or j[2] != pitch or j[3] != coff or j[4] != float(scale):
+            if j[1] != cols or j[2] != pitch or j[3] != coff or j[4] != float(scale) or j[7] != out_rows:
                 raise ValueError(f"SlabBatch: inconsistent segment for {key}")
             j[6].append((part, rows))
 
@@ -43,9 +45,9 @@ class SlabBatch:
         lib = load()
         flat = []
         for key in self.order:
-            out, cols, pitch, coff, scale, acc, segs = self.jobs[key]
+            out, cols, pitch, coff, scale, acc, segs, orows = self.jobs[key]
             for i in range(0, len(segs), _MAX_SEGS):
-                flat.append((out, cols, pitch, coff, scale, acc if i == 0 else True, segs[i:i + _MAX_SEGS]))
+                flat.append((out, cols, pitch, coff, scale, acc if i == 0 else True, segs[i:i + _MAX_SEGS], orows))
         # a job that accumulates onto an output written by an earlier job of the same
         # launch would race: such chains go to separate launches
         while flat:
@@ -68,7 +70,7 @@ class SlabBatch:
         P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
         check(lib.hsg_slab_reduce(
             k, (P * k)(*[f[0].data_ptr() for f in batch]), (I * k)(*[f[1] for f in batch]),
-            (I * k)(*[f[2] for f in batch]), (I * k)(*[f[3] for f in batch]), (F * k)(*[f[4] for f in batch]),
+            (I * k)(*[f[7] for f in batch]), (I * k)(*[f[2] for f in batch]), (I * k)(*[f[3] for f in batch]), (F * k)(*[f[4] for f in batch]),
             (I * k)(*[int(f[5]) for f in batch]), (I * k)(*[len(f[6]) for f in batch]),
             (P * len(segs))(*[s[0].data_ptr() for s in segs]), (I * len(segs))(*[s[1] for s in segs]),
             stream_of(batch[0][0])), "hsg_slab_reduce")

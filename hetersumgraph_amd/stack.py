@@ -263,11 +263,9 @@ class _GatStack(torch.autograd.Function):
                 else:
                     nb_grad = saved[1].new_empty(ctx.shapes[nb])
                     grads[nb] = nb_grad
-            if id(lay) not in stages:
+            if id(lay) not in stages:                  # the layer's staged attention partials
                 stages[id(lay)] = (lay, attn_params_workspace(saved[2][0], lay.H, lay.D))
-                stage = (stages[id(lay)][1], False)
-            else:
-                stage = (stages[id(lay)][1], True)
+            stage = (batch, id(lay), stages[id(lay)][1])
             if id(lay) not in gbufs:
                 X, Hh = ctx.bufs[id(lay)]
                 gbufs[id(lay)] = (lay, torch.empty_like(X), torch.empty_like(Hh))
@@ -280,10 +278,6 @@ class _GatStack(torch.autograd.Function):
                 grads[org].add_(dx)
             else:
                 grads[org] = dx
-        for lay, ws in stages.values():
-            dst = _attn_dst(pgrads, lay, T)
-            if dst is not None:
-                attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
         # FFN weight gradients, one GEMM per weight over every application's rows:
         # dW2 = dY^T H, dW1 = dH^T X with [applications * rows] as the reduction
         for lay, DY, DH in gbufs.values():
@@ -300,6 +294,10 @@ class _GatStack(torch.autograd.Function):
                 else:
                     gemm(A, B, a_t=True, out=dw.view(m, n), add=dw.view(m, n) if a_w else None)
         batch.flush()
+        for lay, ws in stages.values():
+            dst = _attn_dst(pgrads, lay, T)
+            if dst is not None:
+                attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
         ctx.apps = ctx.bufs = None
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None

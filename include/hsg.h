@@ -194,15 +194,17 @@ int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcont
                        const float *B, int ldb, int b_kcontig, int splits, float *workspace,
                        void *stream);
 /* Deferred column sums of partial slabs, njobs (1..24) outputs in one deterministic
- * launch: out[q][c] = (accumulate[q] ? out[q][c] : 0) + scale[q] *
- * sum over job q's nseg[q] (1..4) segments s (in order) and their rows r of
- * seg_s[r*pitch[q] + coff[q] + c], c < cols[q].  seg / seg_rows list the segments of
- * all jobs back to back.  The fused stack's backward sums every layer's
- * head-projection dW slabs, FFN bias / LayerNorm partials and split-K weight
- * gradients here, once per step, instead of one reduce launch per application. */
-int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *pitch, const int *coff,
-                    const float *scale, const int *accumulate, const int *nseg, const float *const *seg,
-                    const int *seg_rows, void *stream);
+ * launch: out[q][b][c] = (accumulate[q] ? out[q][b][c] : 0) + scale[q] * sum over
+ * job q's nseg[q] (1..4) segments s (in order) of the rows r in the b-th of
+ * out_rows[q] equal row ranges of s of seg_s[r*pitch[q] + coff[q] + c], c < cols[q]
+ * (out_rows 1: plain column sums; > 1: a staged partial [out_rows][cols], e.g. the
+ * hsg_attn_params_stage workspace).  seg / seg_rows list the segments of all jobs
+ * back to back.  The fused stack's backward sums every layer's head-projection dW
+ * slabs, FFN bias / LayerNorm partials, attention-parameter partials and split-K
+ * weight gradients here, once per step, instead of one launch per application. */
+int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *out_rows, const int *pitch,
+                    const int *coff, const float *scale, const int *accumulate, const int *nseg,
+                    const float *const *seg, const int *seg_rows, void *stream);
 int hsg_gemm_bf16(int M, int N, int K, const float *A, int lda, int a_kcontig,
                   const float *B, int ldb, int b_kcontig, float *C, int ldc,
                   const float *bias, const float *aux, int ldaux, int epi, int relu,

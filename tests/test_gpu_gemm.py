@@ -266,3 +266,23 @@ def test_gemm_slabs_reduce_to_the_product():
     b.flush()
     R = A.double().t() @ B.double()
     assert (out.double() - R).abs().max().item() < 2e-3
+
+
+def test_slab_batch_staged_rows():
+    """out_rows > 1: row b of the output sums the b-th of out_rows equal row ranges of
+    every segment (the attention-parameter stage layout)."""
+    from hetersumgraph_amd.reduce import SlabBatch
+    torch.manual_seed(6)
+    segs = [torch.randn(r, 88, device="cuda") for r in (4096, 301, 7)]
+    R = 64
+    out = torch.empty(R * 88, device="cuda")
+    b = SlabBatch()
+    for sg in segs:
+        b.add("stage", out, 88, 88, 0, 1.0, False, sg, sg.shape[0], out_rows=R)
+    b.flush()
+    ref = torch.zeros(R, 88, dtype=torch.float64, device="cuda")
+    for sg in segs:
+        per = (sg.shape[0] + R - 1) // R
+        for r in range(R):
+            ref[r] += sg[r * per:(r + 1) * per].double().sum(0)
+    assert torch.allclose(out.view(R, 88).double(), ref, rtol=1e-5, atol=1e-4)
