@@ -266,24 +266,33 @@ def pmc_traffic():
 
 def time_dense_kernel(stack, n_rows, reps):
     """Average duration of the S2W FFN first GEMM (x W1^T + b1, ReLU;
-    [n_w, 300] x [300, 512]) on the stack's own weights, back-to-back launches
-    between HIP events on the launching stream.  Returns (ms, flops per launch)."""
-    from hetersumgraph_amd.dense import gemm
+    [n_w, 300] x [300, 512]) on the stack's own weights, on the path the step runs
+    (hsg_gemm_f32_psw on the pre-split W1 in 'f32' mode, else hsg_gemm_*),
+    back-to-back launches between HIP events on the launching stream.  Returns
+    (ms, flops per launch, entry point name)."""
+    from hetersumgraph_amd.dense import gemm, gemm_psw
+    from hetersumgraph_amd.ffn import ffn_wsplit
     ffn = stack.sent2word.ffn
     w1, b1 = ffn.w_1.weight.detach().squeeze(-1).contiguous(), ffn.w_1.bias.detach()
+    w2, b2 = ffn.w_2.weight.detach().squeeze(-1).contiguous(), ffn.w_2.bias.detach()
     x = torch.randn(n_rows, w1.shape[1], device=w1.device)
     out = x.new_empty(n_rows, w1.shape[0])
+    ws = ffn_wsplit(x, w1, b1, w2, b2)
+    if ws is not None:
+        run, name = (lambda: gemm_psw(x, ws[0], bias=b1, relu=True, out=out)), "hsg_gemm_f32_psw"
+    else:
+        run, name = (lambda: gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)), "hsg_gemm_*"
     st = torch.cuda.current_stream()
     for _ in range(5):
-        gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
+        run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record(st)
     for _ in range(reps):
-        gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)
+        run()
     e1.record(st)
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps, 2.0 * n_rows * w1.shape[0] * w1.shape[1]
+    return e0.elapsed_time(e1) / reps, 2.0 * n_rows * w1.shape[0] * w1.shape[1], name
 
 
 # ------------------------------------------------------------- CPU baseline --
@@ -482,7 +491,7 @@ def main():
     traffic, traffic_src, traffic_rec = pmc_traffic() if args.config == "cfg2" else (None, None, None)
     items = step_work(rel_w, rel_s, args.n_iter, args.dtype)
     floor_s, edge_floor_s, dense_floor_s, gflop = full_stack_floor(items)
-    d_ms, d_flops = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
+    d_ms, d_flops, d_name = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
     d_tf = d_flops / (d_ms * 1e-3) / 1e12
 
     out = {
@@ -525,7 +534,7 @@ def main():
                        "frac": floor_s / (ms_per_step * 1e-3),
                        "formula": "sum_k max(B_k/8 TB/s, F_k/peak_k) / t_step over the step's edge, head-"
                                   "projection and FFN work (bench.step_work)"},
-        "roofline_dense": {"kernel": "hsg_gemm_f32 (S2W FFN x W1^T + b1, ReLU; "
+        "roofline_dense": {"kernel": f"{d_name} (S2W FFN x W1^T + b1, ReLU; "
                                      f"{rel_s.n_dst}x300 @ 300x512)", "bound": "mfma",
                            "achieved": d_tf, "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                            "frac": d_tf / FP32_MFMA_PEAK_TFLOPS, "flops_per_launch": d_flops,
