@@ -407,11 +407,12 @@ __device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &
 //        thread covers (k, 4 consecutive rows) -> NL x ds_write_b64, and fragments
 //        come back k-contiguous through the hardware transpose read
 //        ds_read_b64_tr_b16 (two per fragment) -- no in-register transpose.
-template <bool KC, int ROWS, int BK, int NL>
+template <bool KC, int ROWS, int BK, int NL, int NT = 256>
 struct Stage3 {
     static constexpr int LD = KC ? Ldh<BK>::v : ROWS + 8;     // bf16 per image row
     static constexpr int IMG = KC ? ROWS * LD : BK * LD;      // bf16 per limb plane
-    static constexpr int NU = ROWS * BK / 1024;               // float4 units per thread
+    static constexpr int NU = ROWS * BK / (4 * NT);           // float4 units per thread
+    static_assert(NU * 4 * NT == ROWS * BK, "tile must split evenly over the block");
     f32x4 v[NU];
 
     __device__ __forceinline__ static f32x4 ld4(const float *__restrict__ g, int ld, int gr, int gc, int lim_r,
@@ -433,7 +434,7 @@ struct Stage3 {
     __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int r0, int nr, int k0, int nk) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const int idx = threadIdx.x + 256 * i;
+            const int idx = threadIdx.x + NT * i;
             if constexpr (KC) {
                 const int row = idx / (BK / 4), col = (idx % (BK / 4)) * 4;
                 v[i] = ld4(g, ld, r0 + row, k0 + col, nr, nk);
@@ -447,7 +448,7 @@ struct Stage3 {
     __device__ __forceinline__ void store(__bf16 (*s)[IMG]) const {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const int idx = threadIdx.x + 256 * i;
+            const int idx = threadIdx.x + NT * i;
             const int o = KC ? (idx / (BK / 4)) * LD + (idx % (BK / 4)) * 4
                              : (idx / (ROWS / 4)) * LD + (idx % (ROWS / 4)) * 4;
             bf16x4 x0, x1, x2;
@@ -494,26 +495,29 @@ struct Stage3 {
     }
 };
 
-// Block = 256 threads (2x2 waves), tile BM x BN x BK, one LDS buffer of limb planes;
+// Block = NT threads (2 x NT/128 waves), tile BM x BN x BK, one LDS buffer of limb planes;
 // the next PF K tiles are prefetched into registers (PF = 2: the loads of tile kt+2
 // are issued while tile kt is multiplied, two tiles of MFMA work to hide their
 // latency).  Two barriers per K tile.  NL = 1 is a bf16-operand probe of the same
 // pipeline (dev only).  The epilogue (and split-K / column partials) is k_gemm's.
-template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL, int IGLP = -1>
-__global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
-    constexpr int WM = BM / 2, WN = BN / 2;
+template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL, int IGLP = -1, int NT = 256>
+__global__ __launch_bounds__(NT, NT == 256 ? 2 : 1) void k_gemm3(GemmArgs p) {
+    constexpr int WGN = NT / 128;                          // waves along N (2 along M)
+    constexpr int WM = BM / 2, WN = BN / WGN;
     constexpr int TM = WM / 32, TN = WN / 32;
-    __shared__ __attribute__((aligned(16))) __bf16 sA[NL][Stage3<AK, BM, BK, NL>::IMG];
-    __shared__ __attribute__((aligned(16))) __bf16 sB[NL][Stage3<BKC, BN, BK, NL>::IMG];
+    using SA = Stage3<AK, BM, BK, NL, NT>;
+    using SB = Stage3<BKC, BN, BK, NL, NT>;
+    __shared__ __attribute__((aligned(16))) __bf16 sA[NL][SA::IMG];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[NL][SB::IMG];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WGN, wn = wid % WGN;
     const int li = lane & 31, h = lane >> 5;
     const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
     const int tiles_mn = tiles_n * tiles_m;
     const int kt_total = (p.K + BK - 1) / BK;
     const int total = tiles_mn * p.splits;
-    Stage3<AK, BM, BK, NL> ra[PF];
-    Stage3<BKC, BN, BK, NL> rb[PF];
+    SA ra[PF];
+    SB rb[PF];
     for (int t = blockIdx.x; t < total; t += gridDim.x) {
     const int lt = p.xcd ? xcd_tile(t, total) : t;
     const int tx = lt % tiles_n, ty = (lt / tiles_n) % tiles_m, tz = lt / tiles_mn;
@@ -554,9 +558,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
 #pragma unroll
             for (int l = 0; l < NL; ++l) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) a[l][i] = Stage3<AK, BM, BK, NL>::frag(sA[l], wm * WM + i * 32, s16, lane);
+                for (int i = 0; i < TM; ++i) a[l][i] = SA::frag(sA[l], wm * WM + i * 32, s16, lane);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) b[l][j] = Stage3<BKC, BN, BK, NL>::frag(sB[l], wn * WN + j * 32, s16, lane);
+                for (int j = 0; j < TN; ++j) b[l][j] = SB::frag(sB[l], wn * WN + j * 32, s16, lane);
             }
             // smallest limb products first, a0*b0 last
 #pragma unroll
@@ -611,7 +615,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm3(GemmArgs p) {
             for (int j = 0; j < TN; ++j) red[wm * BN + wn * WN + j * 32 + li] = csum[j];
         }
         __syncthreads();
-        for (int c = threadIdx.x; c < BN; c += 256) {
+        for (int c = threadIdx.x; c < BN; c += NT) {
             const int n = n0 + c;
             if (n < p.N) p.colpart[(size_t)ty * p.N + n] = red[c] + red[BN + c];
         }
@@ -1184,7 +1188,7 @@ int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int BM, int BN, int BK = 32, int PF = 1, int NL = 3, int IGLP = -1>
+template <int BM, int BN, int BK = 32, int PF = 1, int NL = 3, int IGLP = -1, int NT = 256>
 int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     const int kt_total = (p.K + BK - 1) / BK;
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
@@ -1192,10 +1196,10 @@ int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
     if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
-    if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
-    else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
-    else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL, IGLP>), grid, dim3(256), 0, st, p);
+    if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
+    else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
+    else if (!ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, false, true, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL((k_gemm3<BM, BN, false, false, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1353,6 +1357,10 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
             if (t3 == 1) rc = launch3<128, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
             else if (t3 == 3) rc = launch3<128, 128, 32, 1, 3, 0>(p, ak, bk, splits, st);
             else rc = launch3<64, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
+        } else if (var == 6) {                              // 8 waves (2 x 4), iglp_opt(0)
+            if (t3 == 1) rc = launch3<64, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
+            else if (t3 == 3) rc = launch3<128, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
+            else rc = launch3<64, 128, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
         } else if (t3 == 3) rc = launch3<128, 128>(p, ak, bk, splits, st);
         else if (t3 == 1) rc = launch3<128, 64>(p, ak, bk, splits, st);
         else if (t3 == 2) rc = launch3<64, 128>(p, ak, bk, splits, st);

@@ -217,11 +217,16 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
         }
     };
 #pragma unroll
-    for (int u = 0; u < PF; ++u) fetch(u, 4 * lk + 16 * u);
-    for (int c0 = 0; c0 < in; c0 += 16 * PF) {
+    for (int u = 0; u < PF; ++u) {
+        fetch(u, 4 * lk + 16 * u);
+        if constexpr (PF > 1) __builtin_amdgcn_sched_barrier(0);   // issue order = slot order
+    }
+    // whole rings only (chunks past `in` read zeros): a break inside the ring makes the
+    // compiler wait vmcnt(0) at the loop head and the ring collapses to depth 1
+    const int in_pad = (in + 16 * PF - 1) / (16 * PF) * (16 * PF);
+    for (int c0 = 0; c0 < in_pad; c0 += 16 * PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
-            if (c0 + 16 * u >= in) break;              // wave-uniform
 #pragma unroll
             for (int q = 0; q < SG; ++q) {             // slots past NS carry zero W
                 acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(((mv[u][q].x >> ibit) & 1u) ? xv[u][0] : 0.f,
@@ -234,6 +239,9 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
                                                               wv[u][q][3], acc[q], 0, 0, 0);
             }
             fetch(u, c0 + 16 * (u + PF) + 4 * lk);     // past `in`: OOB offsets read 0
+            // keep the next slot's mask / operand work out of this step: hoisted, it
+            // makes the loop head wait for every load of the ring (vmcnt(0))
+            if constexpr (PF > 1) __builtin_amdgcn_sched_barrier(0);
         }
     }
     // D layout: col = lane & 15 (slot output j), row = (lane >> 4) * 4 + r

@@ -35,14 +35,14 @@ for name, M, N, K in SHAPES:
     out = torch.empty(M, N, device="cuda")
     row = [f"{name:18s}"]
     variants = [("mfma", {}, "f32mfma")] + [(f"x3t{t}{'v' + v if v else ''}", {"HSG_GEMM3_TILE": t, "HSG_GEMM3_VAR": v},
-                                             "f32") for t in ("0", "1", "3") for v in ("", "5", "3")]
+                                             "f32") for t in ("0", "1", "3") for v in ("5", "6")]
     for tag, env, dt in variants:
         for k, v in env.items():
             if v:
                 os.environ[k] = v
             else:
                 os.environ.pop(k, None)
-        for sp in (0, 16, 32, 64):
+        for sp in (0, 8, 16, 32):
             us = timed(lambda: gemm(A, B, a_t=True, out=out, splits=sp, dtype=dt))
             err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
             row.append(f"{tag}/s{sp}:{us:.0f}us,{err:.0e}")
