@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights  # noqa: E402
 
-PLANS = {"1": "BN64 S2", "7": "BN64 iglp0", "9": "BN64 sgb2", "10": "BN64 sgb4", "11": "BN128 iglp0"}
+PLANS = {"1": "BN64 S2", "2": "BN128 S2", "7": "BN64 iglp0", "5": "reg BN64"}
 
 
 def timed(f, reps=20):
