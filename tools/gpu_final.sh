@@ -1,7 +1,8 @@
 # Round evidence in one GPU call: the full -m gpu suite, smoke(), the in-step PMC
 # traffic passes of the roofline kernel, per-kernel counters of the edge / head
 # projection / FFN kernels, the kernel-trace profile of bench.py and of replayed
-# steps, and the default bench line.
+# steps, the per-shape FFN GEMM table, the head-projection counter passes, and the
+# default bench line.
 # usage (repo root, via gpurun): bash tools/gpu_final.sh <tag>;  results in gpurun_out/<tag>/
 set -e
 OUT=gpurun_out/${1:-final}
@@ -19,6 +20,9 @@ python tools/pmc_kernels.py $OUT/pmc_sq1 > $OUT/pmc_kernels.txt
 python tools/pmc_kernels.py $OUT/pmc_sq2 >> $OUT/pmc_kernels.txt
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/step -o step -- python tools/step_profile.py run > $OUT/step_run.log 2>&1
 python tools/step_profile.py parse $(ls $OUT/step/*/step_kernel_trace.csv $OUT/step/step_kernel_trace.csv 2>/dev/null | head -1) > $OUT/step_kernels.txt
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/shapes -o shapes -- python tools/gemm_shapes.py run > $OUT/shapes_run.log 2>&1
+python tools/gemm_shapes.py parse $(ls $OUT/shapes/*/shapes_kernel_trace.csv $OUT/shapes/shapes_kernel_trace.csv 2>/dev/null | head -1) > $OUT/gemm_shapes.md
+bash tools/pmc_hproj.sh $OUT/hproj
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python bench.py --no-cpu-baseline --no-e2e > $OUT/bench_prof.json 2> $OUT/bench_prof.err
 timeout -k 10 400 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err
 echo done
