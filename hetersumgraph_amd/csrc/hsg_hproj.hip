@@ -391,29 +391,35 @@ __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, c
 
 // ------------------------------------------------------------------ dW ----
 // v_mfma_f32_16x16x4_f32, reduction over rows.  Block = 64 input columns (wave w:
-// columns 16w..16w+15) x 8 slots (slot = 16 outputs of one head) x one chunk of
+// columns 16w..16w+15) x SL slots (slot = 16 outputs of one head) x one chunk of
 // rows.  Per 32-row step, staged in LDS:
 //   Xs[32][80]       X[r, c0 .. c0+63]
-//   Zs[32][8*16+16]  dZ of the 8 slots, zero-padded to 16 per slot
-//   Ms[8][64]        the slots' mask words for these 32 rows
+//   Zs[32][SL*16+16] dZ of the SL slots, zero-padded to 16 per slot
+//   Ms[SL][64]       the slots' mask words for these 32 rows
 // and MFMA A[c][r] = bit X[r, c], B[r][j] = dZ[r, kD+d0+j].  The next step's
 // global loads are issued before this step's MFMAs.  Each block writes its own
 // partial slab part[chunk][H*D][in]; k_sum_parts adds the chunks in order.
-constexpr int kDwSlots = 8;
 constexpr int kDwXs = 80;                         // row stride: 4 rows hit 4 disjoint bank quarters
-constexpr int kDwZs = kDwSlots * 16 + 16;
 
 struct DwGeom {
     int ctiles, sgroups, chunks, rows;            // rows per chunk (multiple of 32)
 };
 
+// 4 slots per block (twice the blocks of 8, half the accumulators per wave) and a
+// 1,024-block target: cfg2 step 1.502 vs 1.526 ms (tools/ab.py; 1,536 / 2,048 blocks
+// and the 8-slot, 512-block plan are slower)
+int dw_slots() {
+    if (const char *e = getenv("HSG_HPROJ_DWS")) return atoi(e) == 8 ? 8 : 4;        // dev A/B
+    return 4;
+}
+
 DwGeom dw_geom(int n, int in, int H, int D) {
     DwGeom g;
     const int ns = H * ((D + 15) / 16);
     g.ctiles = (in + 63) / 64;
-    g.sgroups = (ns + kDwSlots - 1) / kDwSlots;
+    g.sgroups = (ns + dw_slots() - 1) / dw_slots();
     const int steps = (n + 31) / 32 > 0 ? (n + 31) / 32 : 1;
-    int target = 512;                                   // blocks to aim for
+    int target = dw_slots() == 4 ? 1024 : 512;          // blocks to aim for
     if (const char *e = getenv("HSG_HPROJ_DWB")) target = atoi(e);     // dev sweep
     int want = target / (g.ctiles * g.sgroups);
     if (want < 1) want = 1;
@@ -424,19 +430,21 @@ DwGeom dw_geom(int n, int in, int H, int D) {
     return g;
 }
 
+template <int SL>
 __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, int rows_per_chunk,
                                                   const float *__restrict__ dZ, int ldz,
                                                   const float *__restrict__ X, int ldx,
                                                   const uint32_t *__restrict__ bits, float *__restrict__ part) {
     __shared__ __attribute__((aligned(16))) float Xs[32][kDwXs];
-    __shared__ __attribute__((aligned(16))) float Zs[32][kDwZs];
-    __shared__ uint32_t Ms[kDwSlots][64];
+    constexpr int ZC = SL * 16, NZ = 32 * ZC / 256, NM = SL * 64 / 256;   // slot columns, per-thread loads
+    __shared__ __attribute__((aligned(16))) float Zs[32][ZC + 16];
+    __shared__ uint32_t Ms[SL][64];
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int SPH = (D + 15) / 16, NS = H * SPH;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
     const int c0 = blockIdx.x * 64;
-    const int s0 = blockIdx.y * kDwSlots;
+    const int s0 = blockIdx.y * SL;
     const int rb = blockIdx.z * rows_per_chunk;
     const int rend = min(rb + rows_per_chunk, n);
     // per-thread staging: X 2 x 4 columns, dZ 16 values, 2 mask words.  The
@@ -445,22 +453,22 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
     const auto rX = rsrc(X, (long)n * ldx * 4);
     const auto rZ = rsrc(dZ, (long)n * ldz * 4);
     const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
-    float xr[8], zr[16];
-    uint32_t mr[2];
-    int xcol[2], zcol[16];
-    uint32_t moff[2];
+    float xr[8], zr[NZ];
+    uint32_t mr[NM];
+    int xcol[2], zcol[NZ];
+    uint32_t moff[NM];
 #pragma unroll
     for (int u = 0; u < 2; ++u) xcol[u] = c0 + ((tid + 256 * u) & 15) * 4;   // 32 rows x 16 column quads
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int a = (tid + 256 * u) & 127;          // 32 rows x 128 slot columns
+    for (int u = 0; u < NZ; ++u) {
+        const int a = (tid + 256 * u) % ZC;           // 32 rows x ZC slot columns
         const int v = s0 + (a >> 4);
         const int k = min(v, NS - 1) / SPH, d = (min(v, NS - 1) - k * SPH) * 16 + (a & 15);
         zcol[u] = (v < NS && d < D) ? k * D + d : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int e = tid + 256 * u;                  // 8 slots x 64 columns
+    for (int u = 0; u < NM; ++u) {
+        const int e = tid + 256 * u;                  // SL slots x 64 columns
         const int v = s0 + (e >> 6), gc = c0 + (e & 63);
         moff[u] = (v < NS && gc < LDC) ? (uint32_t)((v / SPH) * NWI * LDC + gc) * 4 : kOOB;
     }
@@ -474,13 +482,13 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
                 xr[u * 4 + v] = bld(rX, (rok && xcol[u] + v < in) ? (uint32_t)(gi * ldx + xcol[u] + v) * 4 : kOOB);
         }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int gi = r0 + ((tid + 256 * u) >> 7);
+        for (int u = 0; u < NZ; ++u) {
+            const int gi = r0 + (tid + 256 * u) / ZC;
             zr[u] = bld(rZ, (gi < rend && zcol[u] >= 0) ? (uint32_t)(gi * ldz + zcol[u]) * 4 : kOOB);
         }
         const uint32_t roff = (uint32_t)(r0 / 32) * LDC * 4;
 #pragma unroll
-        for (int u = 0; u < 2; ++u) mr[u] = bldu(rM, moff[u] != kOOB ? moff[u] + roff : kOOB);
+        for (int u = 0; u < NM; ++u) mr[u] = bldu(rM, moff[u] != kOOB ? moff[u] + roff : kOOB);
     };
     auto stash = [&]() {
 #pragma unroll
@@ -490,19 +498,19 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
             *reinterpret_cast<f32x4v *>(&Xs[rr][cq]) = f32x4v{xr[u * 4], xr[u * 4 + 1], xr[u * 4 + 2], xr[u * 4 + 3]};
         }
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < NZ; ++u) {
             const int e = tid + 256 * u;
-            Zs[e >> 7][e & 127] = zr[u];
+            Zs[e / ZC][e % ZC] = zr[u];
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < NM; ++u) {
             const int e = tid + 256 * u;
             Ms[e >> 6][e & 63] = mr[u];
         }
     };
-    f32x4v acc[kDwSlots];
+    f32x4v acc[SL];
 #pragma unroll
-    for (int q = 0; q < kDwSlots; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < SL; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const int col = wv * 16 + li;
     if (rb < rend) fetch(rb);
     for (int r0 = rb; r0 < rend; r0 += 32) {
@@ -517,7 +525,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
             // slots past NS were staged as zeros: no branch around the MFMAs (a
             // conditional MFMA makes the compiler shuffle accumulators)
 #pragma unroll
-            for (int q = 0; q < kDwSlots; ++q) {
+            for (int q = 0; q < SL; ++q) {
                 const float a = ((Ms[q][col] >> rr) & 1u) ? xv : 0.f;
                 acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Zs[rr][q * 16 + li], acc[q], 0, 0, 0);
             }
@@ -526,7 +534,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
     // D: col = lane & 15 -> slot output j, row = (lane >> 4) * 4 + r -> input column
     const long base = (long)blockIdx.z * H * D * in;
 #pragma unroll
-    for (int q = 0; q < kDwSlots; ++q) {
+    for (int q = 0; q < SL; ++q) {
         const int v = s0 + q;
         if (v >= NS) continue;
         const int k = v / SPH, j = (v - k * SPH) * 16 + li;
@@ -705,7 +713,11 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const DwGeom g = dw_geom(n, in, H, D);
     const long total = (long)H * D * in;
     if (n > 0) {
-        hipLaunchKernelGGL(k_hproj_dw, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D, g.rows,
+        if (dw_slots() == 4)
+            hipLaunchKernelGGL(k_hproj_dw<4>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D,
+                               g.rows, dZ, ldz, X, ldx, bits, part);
+        else
+        hipLaunchKernelGGL(k_hproj_dw<8>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D, g.rows,
                            dZ, ldz, X, ldx, bits, part);
         int rc = status();
         if (rc) return rc;
