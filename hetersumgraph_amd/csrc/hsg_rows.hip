@@ -13,6 +13,7 @@
 // mask tensor is stored.  One wave per row; lane owns columns lane + 64*i.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/hsg.h"
 #include "hsg_rng.h"
@@ -62,6 +63,70 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
         for (int i = 0; i < NPL; ++i) {
             const int c = lane + 64 * i;
             if (c < d) out[(size_t)r * d + c] = (s[i] - mu) * rs * gamma[c] + beta[c];
+        }
+        if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+    }
+}
+
+// Vector form (d % 4 == 0, 16-byte aligned rows): lane owns the column quads
+// 4*lane + 256*i, i < NV, and each wave takes RPW rows whose loads are issued
+// together (float4 loads: a quarter of the load instructions of k_ln_fwd).
+typedef float f32x4r __attribute__((ext_vector_type(4)));
+template <int NV, int RPW>
+__global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__restrict__ y,
+                                                 const float *__restrict__ x, const float *__restrict__ gamma,
+                                                 const float *__restrict__ beta, float eps, float p_drop,
+                                                 const int64_t *__restrict__ seedp, uint32_t offset,
+                                                 float *__restrict__ out, float *__restrict__ mean,
+                                                 float *__restrict__ rstd) {
+    const int lane = threadIdx.x & 63;
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    if (row0 >= n) return;
+    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    f32x4r s[RPW][NV];
+    float acc[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int r = min(row0 + q, n - 1);
+        acc[q] = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = 4 * lane + 256 * i;
+            s[q][i] = f32x4r{0.f, 0.f, 0.f, 0.f};
+            if (c < d) {
+                const size_t o = (size_t)r * d + c;
+                f32x4r v = *reinterpret_cast<const f32x4r *>(y + o);
+                if (p_drop > 0.f) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = hsg_keep(seed, offset, o + e, thr) ? v[e] * scale : 0.f;
+                }
+                s[q][i] = v + *reinterpret_cast<const f32x4r *>(x + o);
+                acc[q] += (s[q][i][0] + s[q][i][1]) + (s[q][i][2] + s[q][i][3]);
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+        const int r = row0 + q;
+        const float mu = wsum(acc[q]) / d;
+        float var = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            if (4 * lane + 256 * i < d)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { const float t = s[q][i][e] - mu; var = fmaf(t, t, var); }
+        const float rs = rsqrtf(wsum(var) / d + eps);
+        if (r >= n) continue;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const int c = 4 * lane + 256 * i;
+            if (c < d) {
+                const f32x4r g = *reinterpret_cast<const f32x4r *>(gamma + c);
+                const f32x4r b = *reinterpret_cast<const f32x4r *>(beta + c);
+                *reinterpret_cast<f32x4r *>(out + (size_t)r * d + c) = (s[q][i] - mu) * rs * g + b;
+            }
         }
         if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
     }
@@ -229,6 +294,25 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
     const int npl = (d + 63) / 64;
     dim3 grid(grid_rows(n, 8192)), block(256);
     hipStream_t st = (hipStream_t)stream;
+    int vec = d % 4 == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)out & 15) == 0 &&
+              ((uintptr_t)gamma & 15) == 0 && ((uintptr_t)beta & 15) == 0;
+    int rpw = 2;
+    if (const char *e = getenv("HSG_LN_FWD")) {                   // dev A/B: 0 = scalar, 1/2/4 rows per wave
+        rpw = atoi(e);
+        vec = vec && rpw > 0;
+    }
+    if (vec) {
+        const int nv = (d + 255) / 256;
+        const dim3 g4((unsigned)((n + 4 * rpw - 1) / (4 * rpw)));
+#define HSG_LNF4(NV_, R_)                                                                                  \
+    if (nv == NV_ && rpw == R_) {                                                                          \
+        hipLaunchKernelGGL((k_ln_fwd4<NV_, R_>), g4, block, 0, st, n, d, y, x, gamma, beta, eps, p_drop, seed, \
+                           offset, out, mean, rstd);                                                       \
+        return status();                                                                                   \
+    }
+        HSG_LNF4(1, 1) HSG_LNF4(1, 2) HSG_LNF4(1, 4) HSG_LNF4(2, 1) HSG_LNF4(2, 2) HSG_LNF4(2, 4)
+#undef HSG_LNF4
+    }
 #define HSG_LNF(K)                                                                                       \
     case K:                                                                                              \
         hipLaunchKernelGGL(k_ln_fwd<K>, grid, block, 0, st, n, d, y, x, gamma, beta, eps, p_drop, seed, \
