@@ -172,9 +172,14 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     K2, N = (B.shape[1], B.shape[0]) if b_t else (B.shape[0], B.shape[1])
     if K != K2:
         raise ValueError(f"gemm_slabs: inner dims {K} != {K2}")
-    splits = auto_splits(M, N, K)
-    if splits < 2:
+    if auto_splits(M, N, K) < 2:
         return None
+    # 64 K slices: the slabs are summed in the stack's one deferred reduction anyway,
+    # and the smaller slices keep each slice's operand rows L2-resident (cfg2 step
+    # -17..-21 us against the 32 of hsg_gemm_f32's own plan; 24 / 48 / 96 / 128 are
+    # slower, tools/ab.py)
+    splits = int(os.environ.get("HSG_DW_SPLITS", "64"))          # dev A/B
+    splits = max(2, min(splits, (K + 31) // 32))
     ws = A.new_empty(lib.hsg_gemm_workspace_floats(M, N, K, splits))
     check(lib.hsg_gemm_f32_slabs(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), splits, ptr(ws),
                                  stream_of(A)), "hsg_gemm_f32_slabs")
