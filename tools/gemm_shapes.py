@@ -6,9 +6,9 @@ path the step runs, from a rocprofv3 kernel trace:
   python tools/gemm_shapes.py parse DIR/.../shapes_kernel_trace.csv > profiles/<round>/gemm_shapes.md
 
 run: each shape REPS times back to back (forward/backward FFN GEMMs on hsg_gemm_f32_psw
-with pre-split weights; the weight gradients on hsg_gemm_f32's split-K path, whose
-slab sum the step does in its one hsg_slab_reduce launch -- here k_splitk_reduce),
-with a 64 MiB buffer write between shapes as a separator."""
+with pre-split weights; the weight gradients as the step's 64-slice split-K slabs,
+hsg_gemm_f32_slabs, whose sum the step does in its one hsg_slab_reduce launch), with
+a 64 MiB buffer write between shapes as a separator."""
 import csv
 import os
 import sys
@@ -24,7 +24,7 @@ PEAK = 157.3
 
 def run():
     import torch
-    from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights
+    from hetersumgraph_amd.dense import gemm_psw, gemm_slabs, split_weights
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     W1 = 0.05 * torch.randn(512, 300, device=dev, generator=g)
@@ -44,8 +44,8 @@ def run():
              lambda: gemm_psw(H, s2, bias=b2, out=o300),
              lambda: gemm_psw(dy, s2t, relu_mask=H, out=o512),
              lambda: gemm_psw(dH, s1t, out=dx, add=dx),
-             lambda: gemm(DY, HH, a_t=True),
-             lambda: gemm(DH, XX, a_t=True)]
+             lambda: gemm_slabs(DY, HH, a_t=True),
+             lambda: gemm_slabs(DH, XX, a_t=True)]
     for f in calls:
         sep.fill_(1.0)
         for _ in range(REPS):
