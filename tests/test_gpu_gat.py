@@ -26,10 +26,11 @@ def max_err(a, b):
     return (a - b).abs().max().item() if a.numel() else 0.0
 
 
-def assert_grad_close(got, ref, rtol=2e-4, max_bad_rows=0):
+def assert_grad_close(got, ref, rtol=2e-4, max_bad_rows=0, worst=1e-2):
     """|got - ref| <= rtol * max|ref| except in at most ``max_bad_rows`` rows
     (fp32 vs fp64 ReLU-gate flips at near-zero pre-activations, see
-    tests/test_oracle_golden.py)."""
+    tests/test_oracle_golden.py), and even those rows within ``worst`` * max|ref|:
+    a gate flip moves a row by one ReLU-masked term, an indexing bug by O(1)."""
     got = torch.as_tensor(np.asarray(got.detach().cpu() if torch.is_tensor(got) else got), dtype=torch.float64)
     ref = torch.as_tensor(np.asarray(ref.detach().cpu() if torch.is_tensor(ref) else ref), dtype=torch.float64)
     scale = max(ref.abs().max().item(), 1e-6)
@@ -39,6 +40,7 @@ def assert_grad_close(got, ref, rtol=2e-4, max_bad_rows=0):
     bad_rows = (err.reshape(err.shape[0], -1).max(1).values > rtol * scale).sum().item()
     assert bad_rows <= max_bad_rows, (
         f"{bad_rows} rows off (max err {err.max().item():.3e}, scale {scale:.3e})")
+    assert err.max().item() <= worst * scale, f"worst row err {err.max().item():.3e} > {worst} x {scale:.3e}"
 
 
 def run_gat(z, seed, dense_tfidf=False, device="cuda"):
