@@ -28,7 +28,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
-           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce")
+           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
+           "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -78,6 +79,9 @@ _SIGS = {
     "hsg_hproj_fwd": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P],
     "hsg_hproj_fwd_logits_supported": [_I, _I],
     "hsg_hproj_fwd_logits": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P],
+    "hsg_hproj_wt": [_I, _I, _I, _P, _P, _P],
+    "hsg_hproj_fwd_t8_supported": [_I, _I, _I],
+    "hsg_hproj_fwd_t8": [_I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P],
     "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _I, _P],

@@ -42,6 +42,11 @@ def _flags():
             "-I", os.path.join(ROOT, "include")]
 
 
+# per-file extra flags: the narrow-head projection wants plain v_fmac_f32 (SGPR weight
+# operand) rather than SLP-packed v_pk_fma_f32, which issues slower on gfx950
+FILE_FLAGS = {"hsg_hproj.hip": ["-fno-slp-vectorize"]}
+
+
 def _obj(src):
     return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
 
@@ -52,7 +57,7 @@ def _compile(src, force, verbose):
         t = os.path.getmtime(obj)
         if os.path.getmtime(src) <= t and all(os.path.getmtime(h) <= t for h in HEADERS):
             return obj
-    cmd = [hipcc()] + _flags() + ["-c", src, "-o", obj + ".tmp"]
+    cmd = [hipcc()] + _flags() + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -288,6 +288,168 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
     }
 }
 
+// ----------------------------------------------------- forward, narrow heads ----
+// VALU form for D = 8 (the W2S projection, 8 heads x 8): the 16x16x4 MFMA pads a
+// head's 8 outputs to 16 columns, so its floor is twice the f32 FLOP floor.  One
+// wave = 64 rows (one per lane) x one head x one K part.  The head's weights come
+// transposed, Wt[k][c][d] (hsg_hproj_wt, once per forward), so W[kD+d, c..c+3] is 32
+// contiguous wave-uniform floats (two s_load_dwordx16 per quad of columns) and each
+// fmaf takes its weight as the SGPR operand.  The keep bit is one v_bfe_i32 + v_and
+// on the X value.  The block (HB heads x KS K parts of one 64-row tile) stages X
+// and the keep words through LDS, 32 columns per part per step (coalesced loads;
+// lanes walking their own rows straight from memory thrash L1: 64 lines per load),
+// the next step's loads in flight during this one.  K parts are added in part order
+// through LDS (deterministic).  Blocks of one row tile sit on one XCD (block b runs
+// on XCD b % 8), so their X rows are L2 hits.
+// cfg2 W2S shape, rocprofv3: 22.7 us in-step against 32 us for the MFMA kernel
+// (the staging alone, no FMA work: 5.2 us).
+__global__ __launch_bounds__(256) void k_hproj_wt(int H, int D, int in, const float *__restrict__ W,
+                                                  float *__restrict__ Wt) {
+    const long total = (long)H * D * in;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int d = (int)(e % D);
+        const long r = e / D;
+        const int c = (int)(r % in), k = (int)(r / in);
+        Wt[e] = W[((long)k * D + d) * in + c];
+    }
+}
+
+template <int HB, int KS>
+__global__ __launch_bounds__(64 * HB * KS) void k_hproj_fwd_v8(int n, int in, int H, const float *__restrict__ X,
+                                                              int ldx, const float *__restrict__ Wt,
+                                                              const uint32_t *__restrict__ bits, float scale,
+                                                              float *__restrict__ Z, int ldz,
+                                                              const float *__restrict__ a1,
+                                                              float *__restrict__ sigma) {
+    constexpr int D = 8, T = 64 * HB * KS, NS = KS * 512 / T, RS = 36;
+    static_assert(NS >= 1 && KS * 512 % T == 0, "staging split");
+    __shared__ __attribute__((aligned(16))) float sX[KS][64][RS];     // 64 rows x 32 columns per part
+    __shared__ __attribute__((aligned(16))) float s_part[KS > 1 ? (KS - 1) * HB : 1][64 * D];
+    __shared__ __attribute__((aligned(16))) uint32_t sM[HB][KS][2][32];       // keep words of the step
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int nrt = (n + 63) / 64, bpr = (H + HB - 1) / HB;
+    // XCD-aware block -> (row tile, head group)
+    const int b = blockIdx.x, xcd = b & 7, idx = b >> 3;
+    const int rt = (idx / bpr) * 8 + xcd, hg = idx % bpr;
+    if (rt >= nrt) return;                                       // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kp = wv % KS, hb = wv / KS;
+    const int k = hg * HB + hb;
+    const bool kok = k < H;                                      // wave-uniform
+    const int r0 = rt * 64, i = r0 + lane;
+    const int sh = i & 31;
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const int nq = in / 4, pq0 = kp * nq / KS, pq1 = (kp + 1) * nq / KS;
+    const int steps = ((nq + KS - 1) / KS + 7) / 8;
+    // staging: thread unit e = (part p, row r, quad u) loads X[r0 + r][4 (p nq/KS + 8t + u) ..]
+    uint32_t goff[NS];
+    float *ldst[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int e = tid + T * s, p = e / 512, f = e % 512, r = f / 8, u = f % 8;
+        goff[s] = r0 + r < n ? (uint32_t)((r0 + r) * ldx + 4 * (p * nq / KS + u)) * 4 : kOOB;
+        ldst[s] = &sX[p][r][4 * u];
+    }
+    f32x4v sr[NS];
+    auto stage_load = [&](int t) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const u32x4v v = bld4(rX, goff[s] + t * 128);        // past the row / buffer: unused / 0
+            sr[s] = f32x4v{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+        }
+    };
+    // keep words: thread tid stages word (head hg*HB + mh, row group r0/32 + mg, column
+    // 4 pq0(mp) + 32 t + mw) of every step: one word per thread
+    const int mw = tid & 31, mg = (tid >> 5) & 1, mp = (tid >> 6) % KS, mh = tid / (64 * KS);
+    const int mk = hg * HB + mh;
+    const uint32_t moff = mk < H ? (uint32_t)(((mk * NWI + r0 / 32 + mg) * LDC + 4 * (mp * nq / KS) + mw) * 4) : kOOB;
+    uint32_t mr = 0;
+    auto mask_load = [&](int t) { mr = bldu(rM, moff != kOOB ? moff + t * 128 : kOOB); };
+    // this head's W^T [in][8] (wave-uniform: 32 floats per quad, two s_load_dwordx16)
+    const f32x16 *wt = reinterpret_cast<const f32x16 *>(Wt + (size_t)min(k, H - 1) * in * D);
+    // two accumulator sets (even / odd quads): 16 independent fmaf chains.  Plain
+    // v_fmac_f32 with the weight as the SGPR operand (this file is built with
+    // -fno-slp-vectorize: a packed v_pk_fma_f32 issues slower than two v_fma_f32)
+    float acc2[2][D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc2[0][d] = acc2[1][d] = 0.f;
+    auto quad = [&](f32x16 w0, f32x16 w1, f32x4v x, u32x4v m, float (&a)[D]) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int keep = __builtin_amdgcn_sbfe((int)m[j], sh, 1);         // 0 or -1
+            const float xm = __int_as_float(__float_as_int(x[j]) & keep);
+#pragma unroll
+            for (int d = 0; d < D; ++d) a[d] = fmaf(xm, j < 2 ? w0[(j & 1) * 8 + d] : w1[(j & 1) * 8 + d], a[d]);
+        }
+    };
+    // one step: the staged chunk t -> LDS, chunk t+1 requested, then the 8 quads of
+    // this wave's part: X rows (row = lane) read from LDS up front, W two quads at a
+    // time (one scalar-load wait per pair), mask words loaded one step ahead
+    auto run_step = [&](int t) {
+        __syncthreads();                                         // previous step's LDS reads done
+#pragma unroll
+        for (int s = 0; s < NS; ++s) *reinterpret_cast<f32x4v *>(ldst[s]) = sr[s];
+        sM[mh][mp][mg][mw] = mr;
+        __syncthreads();
+        if (t + 1 < steps) {
+            stage_load(t + 1);
+            mask_load(t + 1);
+        }
+        if (kok) {
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                const int q = pq0 + 8 * t + u;
+                if (q >= pq1) break;
+                const f32x4v x0 = *reinterpret_cast<const f32x4v *>(&sX[kp][lane][4 * u]);
+                const f32x4v x1 = *reinterpret_cast<const f32x4v *>(&sX[kp][lane][4 * u + 4]);
+                const u32x4v m0 = *reinterpret_cast<const u32x4v *>(&sM[hb][kp][lane >> 5][4 * u]);
+                const u32x4v m1 = *reinterpret_cast<const u32x4v *>(&sM[hb][kp][lane >> 5][4 * u + 4]);
+                const f32x16 w0 = wt[2 * q], w1 = wt[2 * q + 1];
+                if (q + 1 < pq1) {
+                    const f32x16 w2 = wt[2 * q + 2], w3 = wt[2 * q + 3];
+                    quad(w0, w1, x0, m0, acc2[0]);
+                    quad(w2, w3, x1, m1, acc2[1]);
+                } else {
+                    quad(w0, w1, x0, m0, acc2[0]);
+                }
+            }
+        }
+    };
+    stage_load(0);
+    mask_load(0);
+    for (int t = 0; t < steps; ++t) run_step(t);
+    float acc[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[d] = acc2[0][d] + acc2[1][d];
+    if constexpr (KS > 1) {
+        if (kp > 0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) s_part[(kp - 1) * HB + hb][d * 64 + lane] = acc[d];
+        }
+        __syncthreads();
+        if (kp > 0) return;
+#pragma unroll
+        for (int p = 1; p < KS; ++p)
+#pragma unroll
+            for (int d = 0; d < D; ++d) acc[d] += s_part[(p - 1) * HB + hb][d * 64 + lane];
+    }
+    if (!kok || i >= n) return;
+    float z[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) z[d] = acc[d] * scale;
+    float *zr = Z + (size_t)i * ldz + k * D;
+    *reinterpret_cast<f32x4v *>(zr) = f32x4v{z[0], z[1], z[2], z[3]};
+    *reinterpret_cast<f32x4v *>(zr + 4) = f32x4v{z[4], z[5], z[6], z[7]};
+    if (a1) {
+        float sg = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) sg = fmaf(z[d], a1[k * D + d], sg);
+        sigma[(size_t)i * H + k] = sg;
+    }
+}
+
 // ------------------------------------------------------------------ dX ----
 // v_mfma_f32_16x16x4_f32, no LDS.  One wave = 16 rows x (16*CT) input columns.
 // Per head k the K = D product  t = dZ[i0.., kD..kD+D) W[kD.., c..]  runs on MFMA
@@ -385,6 +547,139 @@ __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, c
                 const long o = (long)gi * ldx + gc;
                 dX[o] = accumulate ? dX[o] + tot[t][r] * scale : tot[t][r] * scale;
             }
+        }
+    }
+}
+
+// dX, every operand of the wave requested up front (one memory round trip instead
+// of a load -> MFMA chain per head and step): for narrow heads (H <= HH = 8, D <= 8:
+// the W2S shape) that is H*DS dZ values, H*DS*CT W values and H*CT keep words per
+// lane.  Same products, head order and accumulation as k_hproj_dx<CT, 1> (bitwise
+// equal results).
+template <int CT, int HH, int DS>
+__global__ __launch_bounds__(256) void k_hproj_dx_pre(int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                      int ldz, const float *__restrict__ W,
+                                                      const uint32_t *__restrict__ bits, float scale,
+                                                      float *__restrict__ dX, int ldx, int accumulate) {
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int nct = (in + 16 * CT - 1) / (16 * CT);
+    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int rt = task / nct, ctile = task - rt * nct;
+    const int i0 = rt * 16;
+    if (i0 >= n) return;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int cbase = ctile * 16 * CT;
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rW = rsrc(W, (long)H * D * in * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const int zi = i0 + li;
+    const uint32_t zbase = zi < n ? (uint32_t)zi * ldz * 4 : kOOB;
+    int cb[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) cb[t] = cbase + 16 * t + li;
+    float av[HH][DS], bv[HH][DS][CT];
+    uint32_t mw[HH][CT];
+#pragma unroll
+    for (int k = 0; k < HH; ++k) {
+#pragma unroll
+        for (int s = 0; s < DS; ++s) {
+            const int d = 4 * s + lk;
+            const bool ok = d < D && k < H;
+            const int hd = k * D + d;
+            av[k][s] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
+#pragma unroll
+            for (int t = 0; t < CT; ++t)
+                bv[k][s][t] = bld(rW, (ok && cb[t] < in) ? (uint32_t)(hd * in + cb[t]) * 4 : kOOB);
+        }
+        const uint32_t mrow = (uint32_t)((k * NWI + i0 / 32) * LDC) * 4;
+#pragma unroll
+        for (int t = 0; t < CT; ++t) mw[k][t] = bldu(rM, (k < H && cb[t] < in) ? mrow + cb[t] * 4 : kOOB);
+    }
+    const int sh = (i0 & 31) + 4 * lk;
+    f32x4v tot[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) tot[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < HH; ++k) {
+        f32x4v acc[CT];
+#pragma unroll
+        for (int t = 0; t < CT; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DS; ++s)
+#pragma unroll
+            for (int t = 0; t < CT; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][s], bv[k][s][t], acc[t], 0, 0, 0);
+        if (k < H) {
+#pragma unroll
+            for (int t = 0; t < CT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tot[t][r] += ((mw[k][t] >> (sh + r)) & 1u) ? acc[t][r] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+        const int gc = cbase + 16 * t + li;
+        if (gc >= in) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int gi = i0 + 4 * lk + r;
+            if (gi < n) {
+                const long o = (long)gi * ldx + gc;
+                dX[o] = accumulate ? dX[o] + tot[t][r] * scale : tot[t][r] * scale;
+            }
+        }
+    }
+}
+
+// dX with one wave per head (wide heads, e.g. S2W: H = 6, D = 50, few rows): block =
+// H waves on one 16-row x 16-column tile.  Wave k requests its head's DS dZ values,
+// DS W values and keep word up front, runs the DS-step MFMA chain, and leaves the
+// masked product in LDS; the block then adds the heads in head order (the order of
+// k_hproj_dx: bitwise equal results).  DSM = largest DS the instance holds.
+template <int DSM>
+__global__ __launch_bounds__(1024) void k_hproj_dx_hw(int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                      int ldz, const float *__restrict__ W,
+                                                      const uint32_t *__restrict__ bits, float scale,
+                                                      float *__restrict__ dX, int ldx, int accumulate) {
+    __shared__ float sP[16][4][64];                   // [head][r][lane]
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int nct = (in + 15) / 16;
+    const int rt = blockIdx.x / nct, ctile = blockIdx.x - rt * nct;
+    const int i0 = rt * 16;
+    const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int DS = (D + 3) / 4;
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rW = rsrc(W, (long)H * D * in * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const int zi = i0 + li, c = ctile * 16 + li;
+    const uint32_t zbase = zi < n ? (uint32_t)zi * ldz * 4 : kOOB;
+    float av[DSM], bv[DSM];
+#pragma unroll
+    for (int s = 0; s < DSM; ++s) {
+        const int d = 4 * s + lk;
+        const bool ok = s < DS && d < D;
+        const int hd = k * D + d;
+        av[s] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
+        bv[s] = bld(rW, (ok && c < in) ? (uint32_t)(hd * in + c) * 4 : kOOB);
+    }
+    const uint32_t mw = bldu(rM, c < in ? (uint32_t)(((k * NWI + i0 / 32) * LDC) + c) * 4 : kOOB);
+    f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < DSM; ++s)
+        if (s < DS) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+    const int sh = (i0 & 31) + 4 * lk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sP[k][r][lane] = ((mw >> (sh + r)) & 1u) ? acc[r] : 0.f;
+    __syncthreads();
+    for (int o = threadIdx.x; o < 256; o += blockDim.x) {         // 16 x 16 outputs
+        const int r = o >> 6, ln = o & 63;
+        float tot = 0.f;
+        for (int h = 0; h < H; ++h) tot += sP[h][r][ln];
+        const int gi = i0 + 4 * (ln >> 4) + r, gc = ctile * 16 + (ln & 15);
+        if (gi < n && gc < in) {
+            const long ofs = (long)gi * ldx + gc;
+            dX[ofs] = accumulate ? dX[ofs] + tot * scale : tot * scale;
         }
     }
 }
@@ -666,6 +961,47 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
     return status();
 }
 
+int hsg_hproj_wt(int H, int D, int in, const float *W, float *Wt, void *stream) {
+    if (H < 1 || D < 1 || in < 1 || !W || !Wt) return HSG_EINVAL;
+    const long total = (long)H * D * in;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_hproj_wt, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, D, in, W, Wt);
+    return status();
+}
+
+int hsg_hproj_fwd_t8_supported(int in, int H, int D) {
+    return D == 8 && H >= 1 && in >= 4 && in % 4 == 0 ? 1 : 0;
+}
+
+int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float *Wt, const uint32_t *bits, float p,
+                     float *Z, int ldz, const float *a1, float *sigma, void *stream) {
+    if (n < 0 || !hsg_hproj_fwd_t8_supported(in, H, 8) || ldx < in || ldx % 4 != 0 || ldz < H * 8 ||
+        ldz % 4 != 0 || !X || !Wt || !bits || !Z || !aligned16(X) || !aligned16(Z) || !fits_buffers(n, in, H, 8, ldx))
+        return HSG_EINVAL;
+    if ((a1 == nullptr) != (sigma == nullptr)) return HSG_EINVAL;
+    if (n == 0) return 0;
+    // block = HB heads x KS K parts (HSG_HPROJ_FWD_PLAN = HB*10 + KS for A/B)
+    int plan = 22;
+    if (const char *e = getenv("HSG_HPROJ_FWD_PLAN")) plan = atoi(e);
+    hipStream_t st = (hipStream_t)stream;
+    const float s = drop_scale(p);
+    const int nrt = (n + 63) / 64;
+#define HSG_T8(HB_, KS_)                                                                                          \
+    if (plan == HB_ * 10 + KS_) {                                                                                 \
+        const int bpr = (H + HB_ - 1) / HB_;                                                                      \
+        hipLaunchKernelGGL((k_hproj_fwd_v8<HB_, KS_>), dim3((unsigned)((nrt + 7) / 8 * 8 * bpr)),                 \
+                           dim3(64 * HB_ * KS_), 0, st, n, in, H, X, ldx, Wt, bits, s, Z, ldz, a1, sigma);       \
+        return status();                                                                                          \
+    }
+    HSG_T8(4, 2) HSG_T8(8, 1) HSG_T8(4, 1) HSG_T8(2, 4) HSG_T8(1, 4)
+#undef HSG_T8
+    const int bpr = (H + 1) / 2;
+    hipLaunchKernelGGL((k_hproj_fwd_v8<2, 2>), dim3((unsigned)((nrt + 7) / 8 * 8 * bpr)), dim3(256), 0, st, n, in, H,
+                       X, ldx, Wt, bits, s, Z, ldz, a1, sigma);
+    return status();
+}
+
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W, const uint32_t *bits,
                  float p, float *dX, int ldx, int accumulate, void *stream) {
     if (n < 0 || in < 1 || H < 1 || D < 1 || ldz < H * D || !fits_buffers(n, in, H, D, ldz)) return HSG_EINVAL;
@@ -687,6 +1023,30 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     }
         HSG_DXV(4, 1) HSG_DXV(4, 4) HSG_DXV(2, 2)
 #undef HSG_DXV
+    }
+    // dev A/B (HSG_HPROJ_DXPRE): 0 = the chained kernels only, 1 = one wave per head
+    // when the grid is small (default), 2 = one wave per head always, 3 = 1 + the
+    // up-front-operand kernel for narrow heads
+    const char *pe = getenv("HSG_HPROJ_DXPRE");
+    const int mode = pe ? atoi(pe) : 1;
+    if (mode == 3 && wide >= 2048 && H <= 8 && D <= 8) {
+        // narrow heads: every operand up front (W2S: 35.7 us, slower than the 30.1 us
+        // of the chained kernel at 146 VGPRs)
+        hipLaunchKernelGGL((k_hproj_dx_pre<4, 8, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D,
+                           dZ, ldz, W, bits, s, dX, ldx, accumulate);
+        return status();
+    }
+    if (mode != 0 && (wide < 2048 || mode == 2) && H <= 16 && D <= 64) {
+        // few rows, wide heads: one wave per head (S2W: 6.4 us against 17.7 us for the
+        // chained kernel, cold cache)
+        const unsigned blocks = (unsigned)(rtiles * ((in + 15) / 16));
+        if (D <= 32)
+            hipLaunchKernelGGL((k_hproj_dx_hw<8>), dim3(blocks), dim3(64 * H), 0, st, n, in, H, D, dZ, ldz, W, bits, s,
+                               dX, ldx, accumulate);
+        else
+            hipLaunchKernelGGL((k_hproj_dx_hw<16>), dim3(blocks), dim3(64 * H), 0, st, n, in, H, D, dZ, ldz, W, bits,
+                               s, dX, ldx, accumulate);
+        return status();
     }
     if (wide >= 2048) {                  // HF = 1: 26.9 us vs 28.0 (HF = 2) on the W2S shape
         hipLaunchKernelGGL((k_hproj_dx<4, 1>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D, dZ,

@@ -12,6 +12,8 @@ fused stack (:mod:`hetersumgraph_amd.stack`).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import rng as hsg_rng
@@ -48,12 +50,28 @@ def dropmasks(jobs, device, stream_of_t):
     return out
 
 
-def hproj_fwd(X, W, H, D, p, a1=None, bits=None):
+def narrow_heads(d_in, H, D):
+    """Whether the VALU projection (hsg_hproj_fwd_t8, D = 8) takes (d_in, H, D);
+    HSG_HPROJ_FWDV=0 keeps the MFMA kernel (dev A/B)."""
+    return os.environ.get("HSG_HPROJ_FWDV", "1") != "0" and bool(load().hsg_hproj_fwd_t8_supported(d_in, H, D))
+
+
+def transposed_weight(W, H, D):
+    """Wt[k][c][d] = W[kD+d][c] for hsg_hproj_fwd_t8 (hsg_hproj_wt)."""
+    lib = load()
+    d_in = W.shape[1]
+    Wt = W.new_empty(H * d_in * D)
+    check(lib.hsg_hproj_wt(H, D, d_in, ptr(W), ptr(Wt), stream_of(W)), "hsg_hproj_wt")
+    return Wt
+
+
+def hproj_fwd(X, W, H, D, p, a1=None, bits=None, wt=None):
     """Z [n, H*D] and the state its backward needs.  X, W contiguous fp32.  With
     ``a1`` [H, D] (the attention's source part), also the source logits
     sigma [n, H] from the same launch: returns (Z, saved, sigma); sigma is None when
     the fused form does not cover (H, D) (the caller computes it separately).
-    ``bits``: keep-masks already drawn for this call (:func:`dropmasks`)."""
+    ``bits``: keep-masks already drawn for this call (:func:`dropmasks`); ``wt``:
+    :func:`transposed_weight` of W when the caller shares it between calls."""
     lib = load()
     n, d_in = X.shape
     st = stream_of(X)
@@ -63,6 +81,14 @@ def hproj_fwd(X, W, H, D, p, a1=None, bits=None):
         check(lib.hsg_dropmask(n, d_in, H, float(p), ptr(seed_t), off, ptr(bits), st), "hsg_dropmask")
     Z = X.new_empty(n, H * D)
     saved = (X, W, bits, H, D, float(p))
+    if narrow_heads(d_in, H, D) and X.data_ptr() % 16 == 0:
+        if wt is None:
+            wt = transposed_weight(W, H, D)
+        sigma = X.new_empty(n, H) if a1 is not None else None
+        check(lib.hsg_hproj_fwd_t8(n, d_in, H, ptr(X), d_in, ptr(wt), ptr(bits), float(p), ptr(Z), H * D,
+                                   ptr(a1.contiguous()) if a1 is not None else None,
+                                   ptr(sigma) if sigma is not None else None, st), "hsg_hproj_fwd_t8")
+        return (Z, saved, sigma) if a1 is not None else (Z, saved)
     if a1 is not None:
         if not lib.hsg_hproj_fwd_logits_supported(H, D):
             check(lib.hsg_hproj_fwd(n, d_in, H, D, ptr(X), d_in, ptr(W), ptr(bits), float(p), ptr(Z), H * D, st),

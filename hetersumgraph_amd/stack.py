@@ -38,7 +38,7 @@ from . import rng as hsg_rng
 from ._lib import stream_of
 from .dense import gemm, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
-from .hproj import dropmasks, hproj_bwd, hproj_fwd
+from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
 from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
                   gat_table_fwd)
@@ -101,20 +101,22 @@ class _Layer:
                             self.gamma, self.beta) if p is not None]
 
 
-def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None, wsplit="auto", draws=(None, None)):
+def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=None, wsplit="auto", draws=(None, None),
+               wt=None):
     """out = FFN(elu(MultiHeadLayer(neighbor)) + origin) -- module/GAT.py:45-59.
     ``tables``: the layer's (a1, tau) from :func:`ops.attn_tables`, shared by its
     applications within one forward; ``x_out`` / ``H_out``: this application's slots
     of the layer's FFN-input and hidden-activation buffers; ``wsplit``: the layer's
     pre-split FFN weights (ffn.ffn_wsplit), likewise shared; ``draws`` = (head
     projection keep-mask bits, FFN dropout (seed, offset)) drawn up front by the
-    caller, or None each (drawn here)."""
+    caller, or None each (drawn here); ``wt``: the layer's transposed head weights for
+    the narrow-head projection (hproj.transposed_weight), shared likewise."""
     H, D = lay.H, lay.D
     sigma = None
     if lay.p_attn > 0 and tables is not None:     # source logits from the projection's epilogue
-        Z, hsaved, sigma = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, a1=tables[0], bits=draws[0])
+        Z, hsaved, sigma = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, a1=tables[0], bits=draws[0], wt=wt)
     elif lay.p_attn > 0:
-        Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, bits=draws[0])
+        Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, bits=draws[0], wt=wt)
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
@@ -221,13 +223,18 @@ class _GatStack(torch.autograd.Function):
             a = slot[key]
             slot[key] += 1
             out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],
-                                    H_out=bufs[key][1][a], wsplit=wsplits[key], draws=draws[napp[0]])
+                                    H_out=bufs[key][1][a], wsplit=wsplits[key], draws=draws[napp[0]],
+                                    wt=wts[key])
             napp[0] += 1
             states[outk] = out
             apps.append((lay, saved, nb, org, a))
 
         # the attention tables depend on the parameters only: once per layer
         tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
+        # likewise the transposed head weights of a narrow-head (VALU) projection
+        wts = {id(lay): (transposed_weight(lay.W, lay.H, lay.D)
+                         if lay.p_attn > 0 and narrow_heads(lay.W.shape[1], lay.H, lay.D) else None)
+               for lay in (w2s, s2w)}
         run(w2s, rw, ("w", 0), ("s", 0), ("s", 1))
         for i in range(n_iter):
             run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))

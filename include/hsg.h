@@ -292,6 +292,15 @@ int hsg_hproj_fwd_logits_supported(int H, int D);
 int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                          const uint32_t *bits, float p, float *Z, int ldz, const float *a1, float *sigma,
                          void *stream);
+/* Narrow heads (D = 8: the W2S projection, GATStackLayer.py:56 with 8 heads x 8) on
+ * the f32 VALU: hsg_hproj_fwd_logits with the weight given transposed per head,
+ * Wt[k][c][d] = W[kD+d][c] (hsg_hproj_wt, once per forward; H*in*8 floats).  Same
+ * Z, sigma and keep bits.  hsg_hproj_fwd_t8_supported(in, H, D): D == 8, in % 4 == 0;
+ * X and Z 16-byte aligned with ldx, ldz multiples of 4. */
+int hsg_hproj_wt(int H, int D, int in, const float *W, float *Wt, void *stream);
+int hsg_hproj_fwd_t8_supported(int in, int H, int D);
+int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float *Wt, const uint32_t *bits,
+                     float p, float *Z, int ldz, const float *a1, float *sigma, void *stream);
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
                  const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);
