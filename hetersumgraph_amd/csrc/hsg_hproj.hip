@@ -551,83 +551,86 @@ __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, c
     }
 }
 
-// dX, every operand of the wave requested up front (one memory round trip instead
-// of a load -> MFMA chain per head and step): for narrow heads (H <= HH = 8, D <= 8:
-// the W2S shape) that is H*DS dZ values, H*DS*CT W values and H*CT keep words per
-// lane.  Same products, head order and accumulation as k_hproj_dx<CT, 1> (bitwise
-// equal results).
-template <int CT, int HH, int DS>
-__global__ __launch_bounds__(256) void k_hproj_dx_pre(int n, int in, int H, int D, const float *__restrict__ dZ,
-                                                      int ldz, const float *__restrict__ W,
-                                                      const uint32_t *__restrict__ bits, float scale,
-                                                      float *__restrict__ dX, int ldx, int accumulate) {
+// dX for narrow heads (D = 8, H <= 8: the W2S shape), every operand requested up
+// front in 16-byte pieces.  Wave = 16 rows x 64 columns; the four 16-column MFMA
+// tiles are interleaved (tile t, output column n <-> column cbase + 4n + t), so a lane's
+// W quad W[hd, cbase+4li .. +3], keep-word quad and dX quad serve all four tiles, and
+// the reduction index of head k's two 16x16x4 steps is hd = kD + 2 lk + s, so the
+// lane's dZ pair is one 8-byte load: 8 + 16 + 8 vector loads per wave instead of the
+// chained kernel's 112 dword loads.  Heads are added in head order.
+template <int HH, int HG>
+__global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const float *__restrict__ dZ, int ldz,
+                                                     const float *__restrict__ W,
+                                                     const uint32_t *__restrict__ bits, float scale,
+                                                     float *__restrict__ dX, int ldx, int accumulate) {
+    constexpr int D = 8;
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
-    const int nct = (in + 16 * CT - 1) / (16 * CT);
+    const int nct = (in + 63) / 64;
     const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int rt = task / nct, ctile = task - rt * nct;
     const int i0 = rt * 16;
     if (i0 >= n) return;
     const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-    const int cbase = ctile * 16 * CT;
+    const int c = ctile * 64 + 4 * li;                     // this lane's column quad
+    const bool cok = c < in;                               // in % 4 == 0: whole quads
     const auto rZ = rsrc(dZ, (long)n * ldz * 4);
     const auto rW = rsrc(W, (long)H * D * in * 4);
     const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
     const int zi = i0 + li;
     const uint32_t zbase = zi < n ? (uint32_t)zi * ldz * 4 : kOOB;
-    int cb[CT];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) cb[t] = cbase + 16 * t + li;
-    float av[HH][DS], bv[HH][DS][CT];
-    uint32_t mw[HH][CT];
-#pragma unroll
-    for (int k = 0; k < HH; ++k) {
-#pragma unroll
-        for (int s = 0; s < DS; ++s) {
-            const int d = 4 * s + lk;
-            const bool ok = d < D && k < H;
-            const int hd = k * D + d;
-            av[k][s] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
-#pragma unroll
-            for (int t = 0; t < CT; ++t)
-                bv[k][s][t] = bld(rW, (ok && cb[t] < in) ? (uint32_t)(hd * in + cb[t]) * 4 : kOOB);
-        }
-        const uint32_t mrow = (uint32_t)((k * NWI + i0 / 32) * LDC) * 4;
-#pragma unroll
-        for (int t = 0; t < CT; ++t) mw[k][t] = bldu(rM, (k < H && cb[t] < in) ? mrow + cb[t] * 4 : kOOB);
-    }
     const int sh = (i0 & 31) + 4 * lk;
-    f32x4v tot[CT];
+    f32x4v tot[4];
 #pragma unroll
-    for (int t = 0; t < CT; ++t) tot[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < 4; ++t) tot[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    // heads in groups of HG: a group's operands are requested together, then used
 #pragma unroll
-    for (int k = 0; k < HH; ++k) {
-        f32x4v acc[CT];
+    for (int k0 = 0; k0 < HH; k0 += HG) {
+        f32x2v av[HG];
+        f32x4v bv[HG][2];
+        u32x4v mw[HG];
 #pragma unroll
-        for (int t = 0; t < CT; ++t) acc[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        for (int f = 0; f < HG; ++f) {
+            const int k = k0 + f;
+            const bool ok = k < H;
+            const int hd = k * D + 2 * lk;
+            const u32x4v z = bld4(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);   // (hd, hd+1) used
+            av[f] = f32x2v{__uint_as_float(z.x), __uint_as_float(z.y)};
 #pragma unroll
-        for (int s = 0; s < DS; ++s)
-#pragma unroll
-            for (int t = 0; t < CT; ++t)
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[k][s], bv[k][s][t], acc[t], 0, 0, 0);
-        if (k < H) {
-#pragma unroll
-            for (int t = 0; t < CT; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) tot[t][r] += ((mw[k][t] >> (sh + r)) & 1u) ? acc[t][r] : 0.f;
+            for (int s = 0; s < 2; ++s) {
+                const u32x4v w = bld4(rW, (ok && cok) ? (uint32_t)((hd + s) * in + c) * 4 : kOOB);
+                bv[f][s] = f32x4v{__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w)};
+            }
+            mw[f] = bld4(rM, (ok && cok) ? (uint32_t)(((k * NWI + i0 / 32) * LDC) + c) * 4 : kOOB);
         }
-    }
 #pragma unroll
-    for (int t = 0; t < CT; ++t) {
-        const int gc = cbase + 16 * t + li;
-        if (gc >= in) continue;
+        for (int f = 0; f < HG; ++f) {
+            f32x4v acc[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int gi = i0 + 4 * lk + r;
-            if (gi < n) {
-                const long o = (long)gi * ldx + gc;
-                dX[o] = accumulate ? dX[o] + tot[t][r] * scale : tot[t][r] * scale;
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[f][0], bv[f][0][t], f32x4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[f][1], bv[f][1][t], acc[t], 0, 0, 0);
+            if (k0 + f < H) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) tot[t][r] += ((mw[f][t] >> (sh + r)) & 1u) ? acc[t][r] : 0.f;
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // C layout: col = li (tile t: column c + t), row = 4 lk + r
+    if (!cok) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int gi = i0 + 4 * lk + r;
+        if (gi >= n) continue;
+        f32x4v *o = reinterpret_cast<f32x4v *>(dX + (long)gi * ldx + c);
+        f32x4v v = f32x4v{tot[0][r], tot[1][r], tot[2][r], tot[3][r]} * scale;
+        if (accumulate) v += *o;
+        *o = v;
     }
 }
 
@@ -1024,16 +1027,18 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         HSG_DXV(4, 1) HSG_DXV(4, 4) HSG_DXV(2, 2)
 #undef HSG_DXV
     }
-    // dev A/B (HSG_HPROJ_DXPRE): 0 = the chained kernels only, 1 = one wave per head
-    // when the grid is small (default), 2 = one wave per head always, 3 = 1 + the
-    // up-front-operand kernel for narrow heads
+    // dev A/B (HSG_HPROJ_DXPRE): 0 = the chained kernels only; 1 (default) = one wave
+    // per head when the grid is small, k_hproj_dx_n8 for narrow heads; 2 = one wave per
+    // head for every small-D shape that is not narrow
+    // (an up-front-operand form of k_hproj_dx<4, 1> with dword loads: 35.7 us, slower)
     const char *pe = getenv("HSG_HPROJ_DXPRE");
     const int mode = pe ? atoi(pe) : 1;
-    if (mode == 3 && wide >= 2048 && H <= 8 && D <= 8) {
-        // narrow heads: every operand up front (W2S: 35.7 us, slower than the 30.1 us
-        // of the chained kernel at 146 VGPRs)
-        hipLaunchKernelGGL((k_hproj_dx_pre<4, 8, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, D,
-                           dZ, ldz, W, bits, s, dX, ldx, accumulate);
+    if (mode != 0 && wide >= 2048 && H <= 8 && D == 8 && in % 4 == 0 && ldx % 4 == 0 && ldz % 2 == 0 &&
+        aligned16(dX) && ((uintptr_t)dZ & 7) == 0 && aligned16(W)) {
+        // narrow heads: 16-byte operand pieces, all requested up front (W2S)
+        // two heads' operands at a time (22.4 us cold; 4 / 8 at a time: 23.2 / 23.1 us)
+        hipLaunchKernelGGL((k_hproj_dx_n8<8, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, dZ, ldz,
+                           W, bits, s, dX, ldx, accumulate);
         return status();
     }
     if (mode != 0 && (wide < 2048 || mode == 2) && H <= 16 && D <= 64) {
