@@ -1429,43 +1429,75 @@ struct RedJobs {
     const float *seg[kRedJobs][kRedSegs];
     int rows[kRedJobs][kRedSegs];
     int nseg[kRedJobs], cols[kRedJobs], pitch[kRedJobs], coff[kRedJobs], acc[kRedJobs], orows[kRedJobs];
+    int vec[kRedJobs];                                    // 4: float4 columns (aligned), else 1
     float scale[kRedJobs];
     int start[kRedJobs + 1];
     int njobs;
 };
 
-__global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
-    __shared__ float red[8][33];
-    int q = 0;
-    while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
+// Block = 32 lanes along the columns x 8 row groups.  Thread (g, cl) sums rows
+// r = g (mod 8) of every segment (four interleaved partial sums, rows added to each
+// in row order, up to 16 rows in flight), then the
+// 8 groups are added in group order: a fixed order per column, the same for the
+// scalar (V = 1: 32 columns per block) and the float4 (V = 4: 128 columns per block,
+// 512-B row pieces) form, so both give bitwise equal sums.
+extern "C++" {
+template <int V>
+__device__ __forceinline__ void slab_reduce_job(const RedJobs &j, int q, int blk) {
+    typedef float vec_t __attribute__((ext_vector_type(V)));
+    __shared__ __attribute__((aligned(16))) float red[8][32 * V];
     const int cl = threadIdx.x & 31, g = threadIdx.x >> 5;
-    const int nbc = (j.cols[q] + 31) / 32, blk = (int)blockIdx.x - j.start[q];
+    const int nbc = (j.cols[q] + 32 * V - 1) / (32 * V);
     const int ob = blk / nbc;                              // output row (row range of every segment)
-    const int c = (blk - ob * nbc) * 32 + cl;
+    const int c = (blk - ob * nbc) * 32 * V + V * cl;
     const int pitch = j.pitch[q], coff = j.coff[q], orows = j.orows[q];
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    vec_t s[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s[u] = vec_t(0.f);
     if (c < j.cols[q]) {
         for (int sg = 0; sg < j.nseg[q]; ++sg) {
             const float *P = j.seg[q][sg] + coff + c;
             const int rows = j.rows[q][sg], per = (rows + orows - 1) / orows;
             const int r1 = min(rows, (ob + 1) * per);
             int r = ob * per + g;
-            for (; r + 24 < r1; r += 32) {
+            // 16 rows in flight per thread (long segments: the hproj dW slabs are ~300
+            // rows deep), added into the four partial sums in row order
+            for (; r + 120 < r1; r += 128) {
+                vec_t v[16];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) s[u] += P[(size_t)(r + 8 * u) * pitch];
+                for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)(r + 8 * u) * pitch);
+#pragma unroll
+                for (int u = 0; u < 16; ++u) s[u & 3] += v[u];
             }
-            for (; r < r1; r += 8) s[0] += P[(size_t)r * pitch];
+            for (; r + 24 < r1; r += 32) {
+                vec_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)(r + 8 * u) * pitch);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) s[u] += v[u];
+            }
+            for (; r < r1; r += 8) s[0] += *reinterpret_cast<const vec_t *>(P + (size_t)r * pitch);
         }
     }
-    red[g][cl] = (s[0] + s[1]) + (s[2] + s[3]);
+    const vec_t t = (s[0] + s[1]) + (s[2] + s[3]);
+    *reinterpret_cast<vec_t *>(&red[g][V * cl]) = t;
     __syncthreads();
     if (g == 0 && c < j.cols[q]) {
-        float a = 0.f;
+        vec_t a = vec_t(0.f);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) a += red[u][cl];
-        float *o = j.out[q] + (size_t)ob * j.cols[q] + c;
+        for (int u = 0; u < 8; ++u) a += *reinterpret_cast<const vec_t *>(&red[u][V * cl]);
+        vec_t *o = reinterpret_cast<vec_t *>(j.out[q] + (size_t)ob * j.cols[q] + c);
         *o = j.acc[q] ? *o + j.scale[q] * a : j.scale[q] * a;
     }
+}
+}  // extern "C++"
+
+__global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
+    int q = 0;
+    while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
+    const int blk = (int)blockIdx.x - j.start[q];
+    if (j.vec[q] == 4) slab_reduce_job<4>(j, q, blk);
+    else slab_reduce_job<1>(j, q, blk);
 }
 
 int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *out_rows, const int *pitch,
@@ -1489,7 +1521,12 @@ int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *ou
             j.seg[q][sg] = seg[si];
             j.rows[q][sg] = seg_rows[si];
         }
-        j.start[q + 1] = j.start[q] + (cols[q] + 31) / 32 * out_rows[q];
+        // float4 columns when every segment, the output and the column geometry allow
+        bool v4 = cols[q] % 4 == 0 && pitch[q] % 4 == 0 && coff[q] % 4 == 0 && ((uintptr_t)out[q] & 15) == 0;
+        for (int sg = 0; sg < nseg[q]; ++sg) v4 = v4 && ((uintptr_t)j.seg[q][sg] & 15) == 0;
+        if (const char *e = getenv("HSG_SLAB_VEC")) v4 = v4 && atoi(e) != 1;                // dev A/B
+        j.vec[q] = v4 ? 4 : 1;
+        j.start[q + 1] = j.start[q] + (cols[q] + 32 * j.vec[q] - 1) / (32 * j.vec[q]) * out_rows[q];
     }
     if (j.start[njobs] == 0) return 0;
     hipLaunchKernelGGL(k_slab_reduce, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);

@@ -286,3 +286,34 @@ def test_slab_batch_staged_rows():
         for r in range(R):
             ref[r] += sg[r * per:(r + 1) * per].double().sum(0)
     assert torch.allclose(out.view(R, 88).double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("cols,pitch,coff,out_rows", [(1000, 1000, 0, 1), (300, 904, 300, 1), (88, 88, 0, 64),
+                                                      (70, 210, 70, 1)])
+def test_slab_reduce_float4_columns_bitwise_equal_scalar(cols, pitch, coff, out_rows, monkeypatch):
+    """hsg_slab_reduce reads 16-byte column pieces when the job's geometry is aligned
+    (cols, pitch, offset multiples of 4); the per-column summation order is the scalar
+    form's, so the sums are bitwise equal (HSG_SLAB_VEC=1 forces the scalar form)."""
+    from hetersumgraph_amd.reduce import SlabBatch
+    torch.manual_seed(7)
+    segs = [torch.randn(r, pitch, device="cuda") for r in (4096, 301, 7, 64)]
+
+    def run():
+        out = torch.full((out_rows * cols,), 3.0, device="cuda")
+        b = SlabBatch()
+        for sg in segs:
+            b.add("j", out, cols, pitch, coff, 0.75, True, sg, sg.shape[0], out_rows=out_rows)
+        b.flush()
+        torch.cuda.synchronize()
+        return out
+
+    vec = run()
+    monkeypatch.setenv("HSG_SLAB_VEC", "1")
+    scalar = run()
+    assert torch.equal(vec, scalar)
+    per = [(sg.shape[0] + out_rows - 1) // out_rows for sg in segs]
+    ref = torch.full((out_rows, cols), 3.0, dtype=torch.float64, device="cuda")
+    for sg, pr in zip(segs, per):
+        for r in range(out_rows):
+            ref[r] += 0.75 * sg[r * pr:(r + 1) * pr, coff:coff + cols].double().sum(0)
+    assert torch.allclose(vec.view(out_rows, cols).double(), ref, rtol=1e-5, atol=1e-3)
