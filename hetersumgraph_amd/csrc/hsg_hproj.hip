@@ -69,7 +69,9 @@ __device__ __forceinline__ u32x4v bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // x 2 heads) come from one lowbias32 hash of (key, word index) that seeds a
 // xorshift64 stream (shifts and xors only: 32-bit integer multiplies run at a
 // quarter of the VALU rate on CDNA, and one hash per word instead of per row
-// removes most of them).
+// removes most of them), read bit-sliced: 16 steps give the 16 bit planes of both
+// heads' 32 uniforms, compared against the threshold with two or three logic ops
+// per plane instead of a compare and a shift per row.
 __device__ __forceinline__ uint32_t drop_key(const int64_t *seedp, uint32_t offset) {
     const uint64_t key64 = hsg_mix64((uint64_t)seedp[0] * 0x9E3779B97F4A7C15ull +
                                      (uint64_t)offset * 0xD1B54A32D192ED03ull);
@@ -79,10 +81,11 @@ __device__ __forceinline__ uint32_t drop_key(const int64_t *seedp, uint32_t offs
 // thread unit t of one mask: (head pair kp, 32-row word iw, column c), c fastest
 __device__ __forceinline__ void dropmask_unit(int n, int in, int H, uint32_t thr, uint32_t key, long t,
                                               uint32_t *__restrict__ bits) {
-    const int NWI = (n + 31) / 32;
-    const int LDC = mask_ldc(in);
-    const int c = (int)(t % LDC);
-    const long r = t / LDC;
+    const uint32_t NWI = (uint32_t)(n + 31) / 32;
+    const uint32_t LDC = (uint32_t)mask_ldc(in);
+    const uint32_t tu = (uint32_t)t;                   // < 2^31 (host-checked sizes): 32-bit division
+    const int c = (int)(tu % LDC);
+    const uint32_t r = tu / LDC;
     const int iw = (int)(r % NWI);
     const int kp = (int)(r / NWI);
     uint32_t b0 = 0, b1 = 0;
@@ -92,22 +95,29 @@ __device__ __forceinline__ void dropmask_unit(int n, int in, int H, uint32_t thr
                      lowbias32(key + 0x7F4A7C15u + w * 0x85EBCA6Bu);
         x |= 1ull;                                     // xorshift state must be non-zero
         const int jmax = min(32, n - iw * 32);
+        // bit-sliced compare of the 32 rows' 16-bit uniforms against thr, most significant
+        // bit first: bit j of the b-th word is bit b of row j's uniform (one xorshift64
+        // step gives the b-th word of both heads); keep = u >= thr = gt | eq at the end
+        uint32_t eq0 = 0xFFFFFFFFu, gt0 = 0u, eq1 = 0xFFFFFFFFu, gt1 = 0u;
 #pragma unroll
-        for (int j0 = 0; j0 < 32; j0 += 2) {
+        for (int b = 15; b >= 0; --b) {
             x ^= x << 13;
             x ^= x >> 7;
             x ^= x << 17;
-            // 4 x 16 bits: rows j0, j0+1 for heads 2kp, 2kp+1
-            const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-            if (j0 < jmax) {
-                b0 |= (uint32_t)((lo & 0xFFFFu) >= thr) << j0;
-                b1 |= (uint32_t)((lo >> 16) >= thr) << j0;
-            }
-            if (j0 + 1 < jmax) {
-                b0 |= (uint32_t)((hi & 0xFFFFu) >= thr) << (j0 + 1);
-                b1 |= (uint32_t)((hi >> 16) >= thr) << (j0 + 1);
+            const uint32_t r0 = (uint32_t)x, r1 = (uint32_t)(x >> 32);
+            if ((thr >> b) & 1u) {
+                eq0 &= r0;
+                eq1 &= r1;
+            } else {
+                gt0 |= eq0 & r0;
+                eq0 &= ~r0;
+                gt1 |= eq1 & r1;
+                eq1 &= ~r1;
             }
         }
+        const uint32_t rows = jmax >= 32 ? 0xFFFFFFFFu : ((1u << jmax) - 1u);
+        b0 = (gt0 | eq0) & rows;
+        b1 = (gt1 | eq1) & rows;
     }
     const int k0 = 2 * kp;
     bits[((long)k0 * NWI + iw) * LDC + c] = b0;
@@ -303,14 +313,14 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
 // on XCD b % 8), so their X rows are L2 hits.
 // cfg2 W2S shape, rocprofv3: 22.7 us in-step against 32 us for the MFMA kernel
 // (the staging alone, no FMA work: 5.2 us).
+// Wt[k][c][d] = W[kD+d][c]: block (c-tile of 64, head k); thread (c, d) pairs, reads
+// coalesced along c, 32-bit index arithmetic only.
 __global__ __launch_bounds__(256) void k_hproj_wt(int H, int D, int in, const float *__restrict__ W,
                                                   float *__restrict__ Wt) {
-    const long total = (long)H * D * in;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const int d = (int)(e % D);
-        const long r = e / D;
-        const int c = (int)(r % in), k = (int)(r / in);
-        Wt[e] = W[((long)k * D + d) * in + c];
+    const int k = blockIdx.y, c0 = blockIdx.x * 64;
+    for (int e = threadIdx.x; e < 64 * D; e += 256) {
+        const int d = e >> 6, c = c0 + (e & 63);
+        if (c < in) Wt[((size_t)k * in + c) * D + d] = W[((size_t)k * D + d) * in + c];
     }
 }
 
@@ -966,10 +976,8 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
 
 int hsg_hproj_wt(int H, int D, int in, const float *W, float *Wt, void *stream) {
     if (H < 1 || D < 1 || in < 1 || !W || !Wt) return HSG_EINVAL;
-    const long total = (long)H * D * in;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(k_hproj_wt, dim3(blocks), dim3(256), 0, (hipStream_t)stream, H, D, in, W, Wt);
+    hipLaunchKernelGGL(k_hproj_wt, dim3((unsigned)((in + 63) / 64), (unsigned)H), dim3(256), 0, (hipStream_t)stream, H,
+                       D, in, W, Wt);
     return status();
 }
 
