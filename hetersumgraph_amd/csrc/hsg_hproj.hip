@@ -738,7 +738,11 @@ DwGeom dw_geom(int n, int in, int H, int D) {
     return g;
 }
 
-template <int SL>
+// VEC (SL = 4, D = 8, in % 4 == 0, 16-byte rows): X and the four heads' dZ columns
+// (32 contiguous floats per row) are staged with 16-byte loads -- 4 loads per thread
+// per 32-row step instead of 17 dword loads; the padding columns of the dZ stage are
+// zeroed once.  Same LDS image, same products (bitwise equal).
+template <int SL, bool VEC = false>
 __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, int rows_per_chunk,
                                                   const float *__restrict__ dZ, int ldz,
                                                   const float *__restrict__ X, int ldx,
@@ -761,7 +765,9 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
     const auto rX = rsrc(X, (long)n * ldx * 4);
     const auto rZ = rsrc(dZ, (long)n * ldz * 4);
     const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    static_assert(!VEC || SL == 4, "vector staging: 4 slots of D = 8");
     float xr[8], zr[NZ];
+    f32x4v xq[2], zq;
     uint32_t mr[NM];
     int xcol[2], zcol[NZ];
     uint32_t moff[NM];
@@ -781,6 +787,17 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
         moff[u] = (v < NS && gc < LDC) ? (uint32_t)((v / SPH) * NWI * LDC + gc) * 4 : kOOB;
     }
     auto fetch = [&](int r0) {
+        if constexpr (VEC) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int gi = r0 + ((tid + 256 * u) >> 4);
+                const u32x4v v = bld4(rX, (gi < rend && xcol[u] < in) ? (uint32_t)(gi * ldx + xcol[u]) * 4 : kOOB);
+                xq[u] = f32x4v{__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+            }
+            const int gi = r0 + (tid >> 3), q = tid & 7, v = s0 + (q >> 1);
+            const u32x4v z = bld4(rZ, (gi < rend && v < NS) ? (uint32_t)(gi * ldz + v * 8 + (q & 1) * 4) * 4 : kOOB);
+            zq = f32x4v{__uint_as_float(z.x), __uint_as_float(z.y), __uint_as_float(z.z), __uint_as_float(z.w)};
+        } else {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int gi = r0 + ((tid + 256 * u) >> 4);
@@ -794,11 +811,21 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
             const int gi = r0 + (tid + 256 * u) / ZC;
             zr[u] = bld(rZ, (gi < rend && zcol[u] >= 0) ? (uint32_t)(gi * ldz + zcol[u]) * 4 : kOOB);
         }
+        }
         const uint32_t roff = (uint32_t)(r0 / 32) * LDC * 4;
 #pragma unroll
         for (int u = 0; u < NM; ++u) mr[u] = bldu(rM, moff[u] != kOOB ? moff[u] + roff : kOOB);
     };
     auto stash = [&]() {
+        if constexpr (VEC) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int e = tid + 256 * u;
+                *reinterpret_cast<f32x4v *>(&Xs[e >> 4][(e & 15) * 4]) = xq[u];
+            }
+            const int q = tid & 7;
+            *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][(q >> 1) * 16 + (q & 1) * 4]) = zq;
+        } else {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int e = tid + 256 * u;
@@ -810,12 +837,16 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
             const int e = tid + 256 * u;
             Zs[e / ZC][e % ZC] = zr[u];
         }
+        }
 #pragma unroll
         for (int u = 0; u < NM; ++u) {
             const int e = tid + 256 * u;
             Ms[e >> 6][e & 63] = mr[u];
         }
     };
+    if constexpr (VEC)                                    // dZ stage columns 8..15 of each slot: zero
+        *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][((tid >> 1) & 3) * 16 + 8 + (tid & 1) * 4]) =
+            f32x4v{0.f, 0.f, 0.f, 0.f};
     f32x4v acc[SL];
 #pragma unroll
     for (int q = 0; q < SL; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
@@ -1086,7 +1117,13 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const DwGeom g = dw_geom(n, in, H, D);
     const long total = (long)H * D * in;
     if (n > 0) {
-        if (dw_slots() == 4)
+        const char *ve = getenv("HSG_HPROJ_DWVEC");                   // dev A/B: 0 = dword staging
+        const bool vec = (!ve || atoi(ve) != 0) && dw_slots() == 4 && D == 8 && in % 4 == 0 && ldx % 4 == 0 &&
+                         ldz % 4 == 0 && aligned16(X) && aligned16(dZ);
+        if (vec)
+            hipLaunchKernelGGL((k_hproj_dw<4, true>), dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H,
+                               D, g.rows, dZ, ldz, X, ldx, bits, part);
+        else if (dw_slots() == 4)
             hipLaunchKernelGGL(k_hproj_dw<4>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D,
                                g.rows, dZ, ldz, X, ldx, bits, part);
         else
