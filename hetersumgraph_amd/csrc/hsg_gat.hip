@@ -129,8 +129,8 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
 }
 
 // ---------------------------------------------------------------- forward ----
-template <int NF, int TAU_MODE, int WPN>
-__global__ __launch_bounds__(256) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
+template <int NF, int TAU_MODE, int WPN, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
                                                 const float *__restrict__ tau,
@@ -609,8 +609,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 // features d = l + lph*i; per edge the G.Z dot is a group sum.  The first lph
 // edges' (src, pre) are loaded before the G/h/dOut rows so that chain overlaps
 // them, then broadcast to the head group with a lane shuffle.
-template <int NE, int TAU_MODE>
-__global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
+template <int NE, int TAU_MODE, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
                                                     const float *__restrict__ Z,
                                                     const float *__restrict__ sigma,
@@ -740,8 +740,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst(RelPtrs R, int H, int D, in
 }
 
 // ---------------------------------------------------- backward: src-centric ----
-template <int NF, int TAU_MODE, int WPN>
-__global__ __launch_bounds__(256) void k_gat_bwd_src(RelPtrs R, int H, int D, int lph, float slope,
+template <int NF, int TAU_MODE, int WPN, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int D, int lph, float slope,
                                                     const float *__restrict__ sigma,
                                                     const float *__restrict__ tau,
                                                     const float *__restrict__ mv,
@@ -908,14 +908,14 @@ int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int TAU, int WPN>
+template <int TAU, int WPN, int OCC = 1>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
                  float *out, float *m, float *l) {
-#define HSG_FWD(NF_)                                                                                \
-    case NF_:                                                                                       \
-        hipLaunchKernelGGL((k_gat_fwd<NF_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
-                           sg, tau, org, h, out, m, l);                                             \
+#define HSG_FWD(NF_)                                                                                     \
+    case NF_:                                                                                            \
+        hipLaunchKernelGGL((k_gat_fwd<NF_, TAU, WPN, OCC>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
+                           sg, tau, org, h, out, m, l);                                                  \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
@@ -1022,6 +1022,22 @@ int fwd_rows_dispatch(RowsPlan pl, hipStream_t st, RelPtrs R, int H, int D, floa
 
 bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+// occupancy hints of the feature-split dst pass (6 waves per SIMD: 88 -> 79 VGPRs,
+// no spill) and of the 4-waves-per-node src pass (5: 101 -> 90); HSG_GAT_BWD_OCC=0
+// drops them.  cfg2 S2W backward 61.2 -> 56.1 us per step in one A/B.
+bool bwd_occ() {
+    const char *e = getenv("HSG_GAT_BWD_OCC");
+    return !(e && atoi(e) == 0);
+}
+
+// occupancy hint of the one-destination-per-wave forward: 7 waves per SIMD (73 -> 64
+// VGPRs, no spill; the SGPR count admits 7 blocks per CU); HSG_GAT_FWD_OCC=1 drops it
+int fwd_occ() {
+    int o = 7;
+    if (const char *e = getenv("HSG_GAT_FWD_OCC")) o = atoi(e);
+    return o == 7 || o == 8 ? o : 1;
+}
+
 template <int TAU, int WPN>
 int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int lph, int om, float slope,
                         const float *Z, const float *sg, const float *tau, const float *h, const float *m,
@@ -1036,15 +1052,15 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
     return launch_status();
 }
 
-template <int TAU>
+template <int TAU, int OCC = 1>
 int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, int om,
                      float slope, const float *Z, const float *sg, const float *tau, const float *h,
                      const float *m, const float *l, const float *dout, float *G, float *dpre,
                      float *dtp) {
-#define HSG_BD(NE_)                                                                              \
-    case NE_:                                                                                    \
-        hipLaunchKernelGGL((k_gat_bwd_dst<NE_, TAU>), grid, dim3(256), 0, st, R, H, D, lph, om,   \
-                           slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp);                      \
+#define HSG_BD(NE_)                                                                                   \
+    case NE_:                                                                                         \
+        hipLaunchKernelGGL((k_gat_bwd_dst<NE_, TAU, OCC>), grid, dim3(256), 0, st, R, H, D, lph, om,   \
+                           slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp);                           \
         break;
     switch (ne) {
         HSG_BD(1) HSG_BD(2) HSG_BD(3) HSG_BD(4) HSG_BD(5) HSG_BD(6) HSG_BD(7) HSG_BD(8)
@@ -1063,14 +1079,14 @@ int ne_bucket(int ne) {
     return -1;
 }
 
-template <int TAU, int WPN>
+template <int TAU, int WPN, int OCC = 1>
 int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                      const float *sg, const float *tau, const float *m, const float *l, const float *G,
                      const float *dpre, const float *a1, const float *Z, float *dZ, float *dsig, float *da1p) {
-#define HSG_BS(NF_)                                                                                   \
-    case NF_:                                                                                         \
-        hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
-                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                            \
+#define HSG_BS(NF_)                                                                                        \
+    case NF_:                                                                                              \
+        hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU, WPN, OCC>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
+                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                                 \
         break;
     switch (nf) {
         HSG_BS(1) HSG_BS(2) HSG_BS(3) HSG_BS(4) HSG_BS(5) HSG_BS(6) HSG_BS(7) HSG_BS(8)
@@ -1120,6 +1136,13 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     }
     const dim3 grid(grid_nodes(rel->n_dst, wpn, kFwdGridCap));
     const int lph = lanes_per_head(H);
+    const int occ = wpn == 1 ? fwd_occ() : 1;
+    if (occ > 1) {
+#define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
+        if (tau_mode == HSG_TAU_TABLE) return occ == 8 ? HSG_FO(HSG_TAU_TABLE, 8) : HSG_FO(HSG_TAU_TABLE, 7);
+        return occ == 8 ? HSG_FO(HSG_TAU_PER_EDGE, 8) : HSG_FO(HSG_TAU_PER_EDGE, 7);
+#undef HSG_FO
+    }
 #define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
     if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_F(HSG_TAU_TABLE, 4) : HSG_F(HSG_TAU_TABLE, 1);
     return wpn == 4 ? HSG_F(HSG_TAU_PER_EDGE, 4) : HSG_F(HSG_TAU_PER_EDGE, 1);
@@ -1158,6 +1181,13 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
     // the same grid as above, the d tau slab's row count, with some idle waves)
     const int ne = ne_bucket((D + lph - 1) / lph);
     if (ne < 0) return HSG_EINVAL;
+    if (bwd_occ()) {
+        if (tau_mode == HSG_TAU_TABLE)
+            return bwd_dst_dispatch<HSG_TAU_TABLE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
+                                                      tau, h, m, l, dout, G, dpre, dtau_part);
+        return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
+                                                     sigma, tau, h, m, l, dout, G, dpre, dtau_part);
+    }
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
                                                tau, h, m, l, dout, G, dpre, dtau_part);
@@ -1185,6 +1215,13 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
         return 0;
     }
     const int wpn = src_wpn(rel), lph = lanes_per_head(H);
+    if (wpn == 4 && bwd_occ()) {
+        if (tau_mode == HSG_TAU_TABLE)
+            return bwd_src_dispatch<HSG_TAU_TABLE, 4, 5>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G,
+                                                         dpre, a1, Z, dZ, dsigma, da1_part);
+        return bwd_src_dispatch<HSG_TAU_PER_EDGE, 4, 5>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G,
+                                                        dpre, a1, Z, dZ, dsigma, da1_part);
+    }
 #define HSG_S(TAU, W) bwd_src_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G, dpre, a1, \
                                                Z, dZ, dsigma, da1_part)
     if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_S(HSG_TAU_TABLE, 4) : HSG_S(HSG_TAU_TABLE, 1);
