@@ -1151,7 +1151,9 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
 
 int hsg_gat_bwd_blocks(const hsg_rel *rel) {
     if (!rel) return 0;
-    return grid_nodes(rel->n_dst, dst_wpn(rel), kBwdDstGridCap);
+    int cap = kBwdDstGridCap;
+    if (const char *e = getenv("HSG_GAT_BWD_CAP")) cap = atoi(e) > 0 ? atoi(e) : cap;   // dev sweep
+    return grid_nodes(rel->n_dst, dst_wpn(rel), cap);
 }
 
 int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_mode, float slope,
