@@ -887,7 +887,11 @@ __global__ __launch_bounds__(256) void k_attn_src_logits(int n, int H, int D, in
 int next_pow2(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 int lanes_per_head(int H) { return 64 / next_pow2(H); }
 constexpr int kFwdGridCap = 8192;
-constexpr int kBwdDstGridCap = 1024;   // bounds the dtau partial slab
+constexpr int kFwdPersistentCap = 1792;
+// bounds the dtau partial slab; 1,536 = 256 CUs x the 6 resident blocks of the
+// feature-split dst pass (w = 6): one persistent wave of blocks (cfg2 S2W dst pass
+// 55.6 -> 49.9 us per step against 1,024; 2,048 / 4,800: 52.0 / 50.6)
+constexpr int kBwdDstGridCap = 1536;
 constexpr int kBwdSrcGridCap = 2048;   // bounds the d a1 partial slab
 constexpr int kLongSegment = 16;       // mean segment length from which 4 waves share a node
 
@@ -1134,7 +1138,11 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
             return fwd_rows_dispatch<HSG_TAU_PER_EDGE>(pl, st, R, H, D, slope, Z, sigma, tau, origin, h, out, m, l);
         }
     }
-    const dim3 grid(grid_nodes(rel->n_dst, wpn, kFwdGridCap));
+    // one destination per wave: one persistent wave of blocks (256 CUs x the 7 blocks
+    // the w = 7 kernel keeps resident; cfg2 S2W forward 24.8 -> 22.4 us per step)
+    int fcap = wpn == 1 && fwd_occ() == 7 ? kFwdPersistentCap : kFwdGridCap;
+    if (const char *e = getenv("HSG_GAT_FWD_CAP")) fcap = atoi(e) > 0 ? atoi(e) : fcap;   // dev sweep
+    const dim3 grid(grid_nodes(rel->n_dst, wpn, fcap));
     const int lph = lanes_per_head(H);
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
