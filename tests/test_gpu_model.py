@@ -84,29 +84,44 @@ def test_model_logits_match_reference(name, cls, seed):
 
 
 def test_train_step_runs_and_learns():
-    """One reference-style train step (train.py:114-135): fwd, CE, sum_nodes, bwd,
-    clip, Adam -- in train mode with dropout -- and the loss goes down."""
+    """Reference-style train steps (train.py:114-135): fwd, CE, sum_nodes, bwd, clip,
+    Adam -- in train mode with dropout (seeded) -- and the dropout-free (eval-mode)
+    loss on the same batch goes down.  The train-mode losses themselves carry the
+    dropout noise of one 2-document batch, so they are only checked for finiteness."""
     from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import rng as hsg_rng
     z = load_fixture("model_hsg")
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))
-    model = build_model("HSumGraph", 4).train()
+    model = build_model("HSumGraph", 4)
+    hsg_rng.manual_seed(1234)
+    torch.cuda.manual_seed(1234)
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], lr=5e-4)
-    losses = []
-    for _ in range(5):
+
+    def batch_loss():
         out = model(G)
         snode = G.filter_nodes(lambda n: n.data["dtype"] == 1)
         label = G.ndata["label"][snode].sum(-1)
         G.nodes[snode].data["loss"] = F.cross_entropy(out, label, reduction="none").unsqueeze(-1)
         loss = hg.sum_nodes(G, "loss").mean()
+        G.ndata.pop("loss")          # train.py gets a fresh graph every step
+        return loss
+
+    model.eval()
+    with torch.no_grad():
+        before = batch_loss().item()
+    model.train()
+    for _ in range(5):
+        loss = batch_loss()
         assert torch.isfinite(loss)
         opt.zero_grad()
         loss.backward()
         torch.nn.utils.clip_grad_norm_(model.parameters(), 1.0)
         opt.step()
-        G.ndata.pop("loss")          # train.py gets a fresh graph every step
-        losses.append(loss.item())
-    assert losses[-1] < losses[0]
+    model.eval()
+    with torch.no_grad():
+        after = batch_loss().item()
+    assert after < before, (before, after)
 
 
 @pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
