@@ -399,10 +399,13 @@ def main():
         s.backward(R)                  # d/ds of sum(s * R): the upstream gradient of the stack output
 
     def allreduce():
-        # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL,
-        # in 2 MiB buckets issued back to back asynchronously, then waited
+        # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL.
+        # After a graph replay every gradient is final at once, so there is nothing to
+        # overlap with: ONE flat bucket (7 MB at cfg2) pays one collective latency
+        # instead of one per 2 MiB bucket (the eager train step overlaps its buckets
+        # with the backward instead: parallel.GradientReducer)
         from hetersumgraph_amd.parallel import allreduce_gradients
-        allreduce_gradients(params, scale=frac)
+        allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
 
     def zero():
         # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
