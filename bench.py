@@ -238,7 +238,8 @@ def full_stack_floor(items):
 
 def time_edge_kernels_in_step(step, zero, n_steps):
     """Average duration of every edge-kernel launch INSIDE eager training steps:
-    HIP events on the launching stream around each hsg_gat_fwd and each
+    HIP events recorded by the kernels' own dispatch packets on the launching stream
+    (hipExtLaunchKernel via hsg_kclock_arm) for each hsg_gat_fwd and each
     (hsg_gat_bwd_dst + hsg_gat_bwd_src) pair (hetersumgraph_amd._lib.KernelClock),
     so each launch runs with the caches its real predecessors in the step leave.
     Returns tag -> (mean ms, launches per step)."""
@@ -473,7 +474,7 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = E_global / (dt / args.steps)
 
-    # edge kernels timed inside eager steps (HIP events on their stream), after the
+    # edge kernels timed inside eager steps (HIP events of their dispatches), after the
     # timed region so they cannot perturb it
     kt = time_edge_kernels_in_step(step, zero, args.kernel_steps)
     Hs, Ds = stack.sent2word.layer.num_heads, stack.sent2word.layer.head_dim
@@ -526,9 +527,10 @@ def main():
                      "bytes_formula": "SURVEY 8(d) B_f = 4 n_src (HD+H) + 8 n_dst + 4 + 5 E_T + 4 n_dst (HD+2H)",
                      "epilogue_bytes_per_launch": epilogue_bytes_fwd(rel_s, Hs, Ds),
                      "avg_launch_us": k_ms * 1e3,
-                     "timing": f"HIP events around each launch on its stream inside {args.kernel_steps} eager "
-                               "training steps (in-step cache state); cross-check: rocprofv3 kernel trace "
-                               "of the same command under profiles/"},
+                     "timing": f"HIP events recorded by the kernel's own dispatch packet on its stream "
+                               f"(hipExtLaunchKernel) inside {args.kernel_steps} eager training steps "
+                               "(in-step cache state); cross-check: rocprofv3 kernel trace of the same "
+                               "command under profiles/"},
         "edge_aggregate": {"bytes_per_step": e_bytes, "time_us_per_step": e_ms * 1e3,
                            "achieved": e_bytes / (e_ms * 1e-3) / 1e9, "unit": "GB/s",
                            "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernels": edge_rows},

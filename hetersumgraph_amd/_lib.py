@@ -29,7 +29,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
            "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
-           "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8")
+           "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
+           "hsg_kclock_pending")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -65,6 +66,8 @@ _SIGS = {
     "hsg_attn_params_finish": [_I, _I, _I] + [_P] * 9 + [_I, _P],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
+    "hsg_kclock_arm": [_P, _P],
+    "hsg_kclock_pending": [],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_bf16": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_f32_mfma": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
@@ -150,10 +153,12 @@ def version() -> str:
 
 class KernelClock:
     """In-step kernel timing for bench.py: while a clock is active (``with
-    KernelClock() as clk``), tagged launches are bracketed by HIP events recorded on
-    the launching stream, inside an ordinary (eager) training step -- so each
-    kernel runs after the step's real predecessors, with the caches they leave.
-    Off (the default), the hook costs one global read per launch."""
+    KernelClock() as clk``), tagged edge launches are timed inside an ordinary
+    (eager) training step -- so each kernel runs after the step's real predecessors,
+    with the caches they leave.  The two HIP events of a launch are recorded by the
+    kernels' own dispatch packets (``hsg_kclock_arm`` -> hipExtLaunchKernel: start at
+    the entry point's first kernel, stop at its last), not by event packets around
+    them.  Off (the default), the hook costs one global read per launch."""
 
     def __init__(self):
         self.events = {}
@@ -168,14 +173,19 @@ class KernelClock:
         CLOCK = None
 
     def start(self, tag, device):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(torch.cuda.current_stream(device))
-        return (tag, e)
+        st = torch.cuda.current_stream(device)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(st)                   # creates the events; the kernels re-record them
+        e1.record(st)
+        load().hsg_kclock_arm(e0.cuda_event, e1.cuda_event)
+        return (tag, e0, e1)
 
     def stop(self, token, device):
-        tag, e0 = token
-        e1 = torch.cuda.Event(enable_timing=True)
-        e1.record(torch.cuda.current_stream(device))
+        tag, e0, e1 = token
+        if load().hsg_kclock_pending():
+            load().hsg_kclock_arm(None, None)
+            raise RuntimeError(f"kernel clock {tag}: the launch path did not record the armed events")
         self.events.setdefault(tag, []).append((e0, e1))
 
     def durations_ms(self):

@@ -18,6 +18,7 @@
 //       access is a contiguous 256-B wave transaction.
 //   Per-wave LDS holds one 64-edge chunk of {alpha[j][k], neighbour rank[j]}.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <math.h>
 #include <stdlib.h>
@@ -912,14 +913,35 @@ int launch_status() {
     return e == hipSuccess ? 0 : (int)e;
 }
 
+// Measurement hook (bench.py's in-step kernel clock, hsg_kclock_arm): armed events are
+// recorded by the next edge kernels' own dispatch packets (hipExtLaunchKernel) --
+// start by the first kernel of an entry point, stop by its last -- so the measured
+// interval is the kernels themselves, without event packets around them.  One-shot.
+hipEvent_t g_kc_start = nullptr, g_kc_stop = nullptr;
+hipEvent_t kc_take(hipEvent_t &e, bool use) {
+    if (!use) return nullptr;
+    hipEvent_t r = e;
+    e = nullptr;
+    return r;
+}
+#define HSG_KLAUNCH(FIRST, LAST, KERNEL, GRID, BLOCK, ST, ...)                                              \
+    do {                                                                                                    \
+        if (((FIRST) && g_kc_start) || ((LAST) && g_kc_stop)) {                                            \
+            hipEvent_t e0_ = kc_take(g_kc_start, FIRST), e1_ = kc_take(g_kc_stop, LAST);                    \
+            hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, 0, ST, e0_, e1_, 0, __VA_ARGS__);                    \
+        } else {                                                                                            \
+            hipLaunchKernelGGL(KERNEL, GRID, BLOCK, 0, ST, __VA_ARGS__);                                    \
+        }                                                                                                   \
+    } while (0)
+
 template <int TAU, int WPN, int OCC = 1>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
                  float *out, float *m, float *l) {
 #define HSG_FWD(NF_)                                                                                     \
     case NF_:                                                                                            \
-        hipLaunchKernelGGL((k_gat_fwd<NF_, TAU, WPN, OCC>), grid, dim3(256), 0, st, R, H, D, lph, slope, Z, \
-                           sg, tau, org, h, out, m, l);                                                  \
+        HSG_KLAUNCH(true, true, (k_gat_fwd<NF_, TAU, WPN, OCC>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
+                    sg, tau, org, h, out, m, l);                                                         \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
@@ -1047,8 +1069,8 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
                         const float *Z, const float *sg, const float *tau, const float *h, const float *m,
                         const float *l, const float *dout, float *G, float *dpre, float *dtp) {
 #define HSG_EP(DV_)                                                                                    \
-    hipLaunchKernelGGL((k_gat_bwd_dst_ep<DV_, TAU, WPN>), grid, dim3(256), 0, st, R, H, D, lph, om, slope, \
-                       Z, sg, tau, h, m, l, dout, G, dpre, dtp)
+    HSG_KLAUNCH(true, false, (k_gat_bwd_dst_ep<DV_, TAU, WPN>), grid, dim3(256), st, R, H, D, lph, om, slope, \
+                Z, sg, tau, h, m, l, dout, G, dpre, dtp)
     if (D <= 4) HSG_EP(4);
     else if (D <= 8) HSG_EP(8);
     else HSG_EP(16);
@@ -1063,8 +1085,8 @@ int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
                      float *dtp) {
 #define HSG_BD(NE_)                                                                                   \
     case NE_:                                                                                         \
-        hipLaunchKernelGGL((k_gat_bwd_dst<NE_, TAU, OCC>), grid, dim3(256), 0, st, R, H, D, lph, om,   \
-                           slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp);                           \
+        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC>), grid, dim3(256), st, R, H, D, lph, om, \
+                    slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp);                                 \
         break;
     switch (ne) {
         HSG_BD(1) HSG_BD(2) HSG_BD(3) HSG_BD(4) HSG_BD(5) HSG_BD(6) HSG_BD(7) HSG_BD(8)
@@ -1089,8 +1111,8 @@ int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
                      const float *dpre, const float *a1, const float *Z, float *dZ, float *dsig, float *da1p) {
 #define HSG_BS(NF_)                                                                                        \
     case NF_:                                                                                              \
-        hipLaunchKernelGGL((k_gat_bwd_src<NF_, TAU, WPN, OCC>), grid, dim3(256), 0, st, R, H, D, lph, slope, \
-                           sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                                 \
+        HSG_KLAUNCH(false, true, (k_gat_bwd_src<NF_, TAU, WPN, OCC>), grid, dim3(256), st, R, H, D, lph, slope, \
+                    sg, tau, m, l, G, dpre, a1, Z, dZ, dsig, da1p);                                     \
         break;
     switch (nf) {
         HSG_BS(1) HSG_BS(2) HSG_BS(3) HSG_BS(4) HSG_BS(5) HSG_BS(6) HSG_BS(7) HSG_BS(8)
@@ -1247,6 +1269,14 @@ int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, fl
                        (hipStream_t)stream, n, H, D, lanes_per_head(H), Z, a1, sigma);
     return launch_status();
 }
+
+int hsg_kclock_arm(void *start_event, void *stop_event) {
+    g_kc_start = (hipEvent_t)start_event;
+    g_kc_stop = (hipEvent_t)stop_event;
+    return 0;
+}
+
+int hsg_kclock_pending(void) { return (g_kc_start ? 1 : 0) + (g_kc_stop ? 2 : 0); }
 
 const char *hsg_version(void) { return "hsg 0.1 gfx950 (fp32 WSWGAT edge kernels)"; }
 

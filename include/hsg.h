@@ -93,6 +93,15 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
 /* Number of partial rows hsg_gat_bwd_src writes into da1_part. */
 int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
 
+/* Measurement hook (bench.py's in-step kernel clock; not part of the reference
+ * surface): the next hsg_gat_fwd records start_event / stop_event (hipEvent_t created
+ * with timing) from its kernel's own dispatch packet (hipExtLaunchKernel); the next
+ * hsg_gat_bwd_dst records start_event at its kernel and the following hsg_gat_bwd_src
+ * stop_event at its kernel.  One-shot: a consumed event is disarmed.  Either may be
+ * NULL.  hsg_kclock_pending: bit 0 / bit 1 set while start / stop is still armed. */
+int hsg_kclock_arm(void *start_event, void *stop_event);
+int hsg_kclock_pending(void);
+
 /* sigma[u, k] = <Z[u, k, :], a1[k, :]> -- the z_src part of attn_fc
  * (GATLayer.py:91-92 / 130-131); a1 = attn_fc.weight[0, :D] per head. */
 int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,
