@@ -144,6 +144,16 @@ struct DropJobs {
     int njobs;
 };
 
+// The step's dropout seed: seed += 1 and the backward-stable snapshot of the new value
+// in one launch (was an in-place add plus a clone: two graph nodes).
+__global__ __launch_bounds__(64) void k_seed_advance(int64_t *seed, int64_t *snap) {
+    if (threadIdx.x == 0) {
+        const int64_t s = seed[0] + 1;
+        seed[0] = s;
+        snap[0] = s;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_dropmask_multi(DropJobs j, const int64_t *seedp) {
     int q = 0;
     while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
@@ -934,6 +944,12 @@ int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t of
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(k_dropmask, dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, in, H, p, seed, offset,
                        bits);
+    return status();
+}
+
+int hsg_seed_advance(int64_t *seed, int64_t *snap, void *stream) {
+    if (!seed || !snap) return HSG_EINVAL;
+    hipLaunchKernelGGL(k_seed_advance, dim3(1), dim3(64), 0, (hipStream_t)stream, seed, snap);
     return status();
 }
 

@@ -32,9 +32,18 @@ class DropoutRNG:
         return self._snap, self.offset
 
     def advance(self):
-        """New masks for the next step (device-side add: graph-capturable)."""
-        self.seed.add_(1)
-        self._snap = None
+        """New masks for the next step (device-side: graph-capturable).  On a GPU one
+        launch (hsg_seed_advance) increments the seed and writes the new value into a
+        fresh snapshot, which the following take() calls hand out."""
+        if self.seed.is_cuda:
+            from ._lib import check, load
+            snap = torch.empty_like(self.seed)
+            st = torch.cuda.current_stream(self.seed.device).cuda_stream
+            check(load().hsg_seed_advance(self.seed.data_ptr(), snap.data_ptr(), st), "hsg_seed_advance")
+            self._snap = snap
+        else:
+            self.seed.add_(1)
+            self._snap = None
 
 
 def get(device) -> DropoutRNG:

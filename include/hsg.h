@@ -286,6 +286,9 @@ int hsg_dropmask_words(int n, int in, int H);
 float hsg_dropmask_scale(float p);
 int hsg_dropmask(int n, int in, int H, float p, const int64_t *seed, uint32_t offset, uint32_t *bits,
                  void *stream);
+/* One-launch seed step of the dropout stream (rng.DropoutRNG.advance): seed[0] += 1 and
+ * snap[0] = the new seed (the snapshot the step's forward and backward share). */
+int hsg_seed_advance(int64_t *seed, int64_t *snap, void *stream);
 /* njobs (1..8) masks in one launch, job q identical to
  * hsg_dropmask(n[q], in[q], H[q], p[q], seed, offset[q], bits[q]): the fused stack draws
  * the masks of all its head projections up front. */
