@@ -30,7 +30,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
            "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
            "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
-           "hsg_kclock_pending", "hsg_seed_advance")
+           "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -69,6 +69,8 @@ _SIGS = {
     "hsg_kclock_arm": [_P, _P],
     "hsg_kclock_pending": [],
     "hsg_seed_advance": [_P, _P, _P],
+    "hsg_gat_bwd_dst_noh_supported": [_RELP, _I, _I],
+    "hsg_gat_bwd_dst_noh": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_bf16": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],
     "hsg_gemm_f32_mfma": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _I, _P, _P, _I, _I, _I, _I, _P, _P, _P],

@@ -253,7 +253,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 if (f < HD) {
                     const size_t o = (size_t)v * HD + f;
                     const float hv = acc[i];
-                    hout[o] = hv;
+                    if (hout) hout[o] = hv;
                     if (origin) out[o] = elu1(hv) + org[i];
                 }
             }
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, in
             if (f < HD) {
                 const size_t o = (size_t)v * HD + f;
                 const float hv = acc[i];
-                hout[o] = hv;
+                if (hout) hout[o] = hv;
                 if (origin) out[o] = elu1(hv) + org[i];
             }
         }
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H,
         const int q = t + kRowsThreads * i;
         if (q < nslot) {
             const size_t o = (size_t)(v0 + srow[i]) * HD + scol[i];
-            *reinterpret_cast<f32x4_t *>(hout + o) = acc[i];
+            if (hout) *reinterpret_cast<f32x4_t *>(hout + o) = acc[i];
             if (origin) {
                 f32x4_t y;
 #pragma unroll
@@ -610,7 +610,14 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 // features d = l + lph*i; per edge the G.Z dot is a group sum.  The first lph
 // edges' (src, pre) are loaded before the G/h/dOut rows so that chain overlaps
 // them, then broadcast to the head group with a lane shuffle.
-template <int NE, int TAU_MODE, int OCC = 1>
+// NOH (no saved h; fused-stack S2W, origin present): G takes elu'(h) from
+// e = x - origin = elu(h) (1 for e > 0, else e + 1 = exp(h); continuous at 0, so the
+// rounding of x - origin moves G by ~ulp(x)), and rho = G_v.h_v = sum_e alpha_e
+// (G_v.Z_u) over the typed edges (h_v = sum_e alpha_e Z_u; phantoms carry no message)
+// is summed in a first pass over the edges whose dots are staged in LDS (the first
+// kCh edges; later ones are recomputed in the second pass).
+constexpr int kCh = 16;
+template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
                                                     const float *__restrict__ Z,
@@ -621,15 +628,19 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
                                                     const float *__restrict__ lv,
                                                     const float *__restrict__ dout,
                                                     float *__restrict__ G, float *__restrict__ dpre,
-                                                    float *__restrict__ dtau_part) {
+                                                    float *__restrict__ dtau_part,
+                                                    const float *__restrict__ xo,
+                                                    const float *__restrict__ org) {
     __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
-    __shared__ float s_g[HSG_WAVES][512], s_gh[HSG_WAVES][512];   // G_v and G_v * h_v, flat (H*D <= 512)
+    __shared__ float s_g[HSG_WAVES][512];                           // G_v, flat (H*D <= 512)
+    __shared__ float s_gh[NOH ? 1 : HSG_WAVES][NOH ? 1 : 512];      // G_v * h_v
+    __shared__ float s_dot[NOH ? HSG_WAVES : 1][NOH ? kCh * HSG_HMAX : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
     const bool kact = k < H;
     float *sd = s_dtau[wid];
-    float *sg = s_g[wid], *sgh = s_gh[wid];
+    float *sg = s_g[wid], *sgh = s_gh[NOH ? 0 : wid], *sdt = s_dot[NOH ? wid : 0];
     if constexpr (TAU_MODE == HSG_TAU_TABLE) {
         for (int i = lane; i < HSG_NT * HSG_HMAX; i += 64) sd[i] = 0.f;
         wave_lds_sync();
@@ -650,7 +661,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
             pre0 = sigma[u0 * H + k] + tau[t0 * H + k];
         }
         // G = dOut * elu'(h) over the row with the flat lane mapping (every access a
-        // contiguous 256-B wave transaction), staged in LDS with G*h; the (k, l) lanes
+        // contiguous 256-B wave transaction), staged in LDS (with G*h); the (k, l) lanes
         // then pick their head's features from there
         constexpr int NF = 8;                     // 64 * NF >= H*D (<= 512)
 #pragma unroll
@@ -658,11 +669,18 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
             const int f = lane + 64 * i;
             if (f < HD) {
                 const size_t o = (size_t)v * HD + f;
-                const float hv = hsv[o], dv = dout[o];
-                const float gv = origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv;
+                const float dv = dout[o];
+                float gv;
+                if constexpr (NOH) {
+                    const float e = xo[o] - org[o];
+                    gv = e > 0.f ? dv : dv * (e + 1.f);
+                } else {
+                    const float hv = hsv[o];
+                    gv = origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv;
+                    sgh[f] = gv * hv;
+                }
                 G[o] = gv;
                 sg[f] = gv;
-                sgh[f] = gv * hv;
             }
         }
         wave_lds_sync();
@@ -675,17 +693,17 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
             const bool ok = kact && d < D;
             const int f = kc * D + min(d, D - 1);
             g[i] = ok ? sg[f] : 0.f;
-            rho += ok ? sgh[f] : 0.f;
+            if constexpr (!NOH) rho += ok ? sgh[f] : 0.f;
         }
         wave_lds_sync();                          // the next destination rewrites the stage
         if (end == beg) continue;   // uniform per wave: no typed in-edge, no gradient
-        rho = group_sum(rho, lph);
+        if constexpr (!NOH) rho = group_sum(rho, lph);
         const float inv = kact ? 1.f / lvv : 0.f;
         const int gl = k * lph;                         // first lane of this head group
-        // edges in pairs: both Z rows are fetched before either dot is reduced
-        for (int e0 = beg; e0 < end; e0 += 2) {
-            int u[2], t[2];
-            float pre[2];
+        // one pair of edges: (src, tau row, pre) of both, then both Z rows fetched before
+        // either dot is reduced -- or the dots from the stage (NOH second pass)
+        auto edge_pair = [&](int e0, bool staged, float (&dot)[2], int (&t)[2], float (&pre)[2]) {
+            int u[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int e = min(e0 + q, end - 1);
@@ -700,6 +718,11 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
                     pre[q] = kact ? sigma[u[q] * H + k] + tau[t[q] * H + k] : 0.f;
                 }
             }
+            if (staged) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q) dot[q] = sdt[min(e0 + q - beg, kCh - 1) * H + kc];
+                return;
+            }
             float zv[2][NE];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -707,7 +730,6 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
 #pragma unroll
                 for (int i = 0; i < NE; ++i) zv[q][i] = zr[min(l + lph * i, D - 1)];
             }
-            float dot[2];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 dot[q] = 0.f;
@@ -715,6 +737,53 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
                 for (int i = 0; i < NE; ++i) dot[q] = fmaf(g[i], zv[q][i], dot[q]);   // g = 0 past D
                 dot[q] = group_sum(dot[q], lph);
             }
+        };
+        if constexpr (NOH) {
+            if (end - beg <= 2) {                 // one pair: dots stay in registers, one pass
+                float dot[2], pre[2];
+                int t[2];
+                edge_pair(beg, false, dot, t, pre);
+                float al[2], rs = 0.f;
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    al[q] = __expf(leaky(pre[q], slope) - M) * inv;
+                    if (beg + q < end) rs = fmaf(al[q], dot[q], rs);
+                }
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int e = beg + q;
+                    if (e < end && kact && l == 0) {
+                        const float ds = al[q] * (dot[q] - rs);
+                        const float dp = pre[q] > 0.f ? ds : ds * slope;
+                        dpre[(size_t)e * H + k] = dp;
+                        if constexpr (TAU_MODE == HSG_TAU_TABLE) sd[t[q] * H + k] += dp;
+                    }
+                }
+                continue;
+            }
+        }
+        if constexpr (NOH) {                      // pass 1: rho = sum_e alpha_e dot_e, dots staged
+            float rs = 0.f;
+            for (int e0 = beg; e0 < end; e0 += 2) {
+                float dot[2], pre[2];
+                int t[2];
+                edge_pair(e0, false, dot, t, pre);
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int e = e0 + q;
+                    if (e < end) {
+                        rs = fmaf(__expf(leaky(pre[q], slope) - M) * inv, dot[q], rs);
+                        if (kact && l == 0 && e - beg < kCh) sdt[(e - beg) * H + k] = dot[q];
+                    }
+                }
+            }
+            rho = rs;
+            wave_lds_sync();
+        }
+        for (int e0 = beg; e0 < end; e0 += 2) {
+            float dot[2], pre[2];
+            int t[2];
+            edge_pair(e0, NOH && e0 + 1 - beg < kCh, dot, t, pre);
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int e = e0 + q;
@@ -727,6 +796,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
                 }
             }
         }
+        if constexpr (NOH) wave_lds_sync();       // the next destination restages the dots
     }
     if constexpr (TAU_MODE == HSG_TAU_TABLE) {
         __syncthreads();
@@ -1078,20 +1148,27 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
     return launch_status();
 }
 
-template <int TAU, int OCC = 1>
+template <int TAU, int OCC = 1, bool NOH = false>
 int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, int om,
                      float slope, const float *Z, const float *sg, const float *tau, const float *h,
                      const float *m, const float *l, const float *dout, float *G, float *dpre,
-                     float *dtp) {
-#define HSG_BD(NE_)                                                                                   \
-    case NE_:                                                                                         \
-        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC>), grid, dim3(256), st, R, H, D, lph, om, \
-                    slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp);                                 \
+                     float *dtp, const float *x = nullptr, const float *org = nullptr) {
+#define HSG_BD(NE_)                                                                                        \
+    case NE_:                                                                                              \
+        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH>), grid, dim3(256), st, R, H, D, lph, om, \
+                    slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp, x, org);                               \
         break;
-    switch (ne) {
-        HSG_BD(1) HSG_BD(2) HSG_BD(3) HSG_BD(4) HSG_BD(5) HSG_BD(6) HSG_BD(7) HSG_BD(8)
-        HSG_BD(16) HSG_BD(32) HSG_BD(64)
-        default: return HSG_EINVAL;
+    if constexpr (NOH) {                 // the shapes the fused stack's S2W pass uses
+        switch (ne) {
+            HSG_BD(4) HSG_BD(5) HSG_BD(6) HSG_BD(7) HSG_BD(8) HSG_BD(16)
+            default: return HSG_EINVAL;
+        }
+    } else {
+        switch (ne) {
+            HSG_BD(1) HSG_BD(2) HSG_BD(3) HSG_BD(4) HSG_BD(5) HSG_BD(6) HSG_BD(7) HSG_BD(8)
+            HSG_BD(16) HSG_BD(32) HSG_BD(64)
+            default: return HSG_EINVAL;
+        }
     }
 #undef HSG_BD
     return launch_status();
@@ -1133,7 +1210,7 @@ extern "C" {
 int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
                 const float *sigma, const float *tau, const float *origin, float *h, float *out,
                 float *m, float *l, void *stream) {
-    if (!rel || !shape_ok(H, D) || (origin && !out)) return HSG_EINVAL;
+    if (!rel || !shape_ok(H, D) || (origin && !out) || (!origin && !h)) return HSG_EINVAL;
     if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     if (rel->n_dst == 0) return 0;
     const RelPtrs R = rel_ptrs(rel);
@@ -1225,6 +1302,39 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
                                                tau, h, m, l, dout, G, dpre, dtau_part);
     return bwd_dst_dispatch<HSG_TAU_PER_EDGE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
                                               sigma, tau, h, m, l, dout, G, dpre, dtau_part);
+}
+
+int hsg_gat_bwd_dst_noh_supported(const hsg_rel *rel, int H, int D) {
+    if (!rel || !shape_ok(H, D) || D <= 16 || dst_wpn(rel) != 1) return 0;
+    const int ne = ne_bucket((D + lanes_per_head(H) - 1) / lanes_per_head(H));
+    return (ne >= 4 && ne <= 8) || ne == 16;
+}
+
+int hsg_gat_bwd_dst_noh(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                        const float *sigma, const float *tau, const float *x, const float *origin,
+                        const float *m, const float *l, const float *dout, float *G, float *dpre,
+                        float *dtau_part, void *stream) {
+    if (!hsg_gat_bwd_dst_noh_supported(rel, H, D) || !x || !origin) return HSG_EINVAL;
+    if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
+    const int lph = lanes_per_head(H);
+    const RelPtrs R = rel_ptrs(rel);
+    const dim3 grid(hsg_gat_bwd_blocks(rel));
+    hipStream_t st = (hipStream_t)stream;
+    if (rel->n_dst == 0) {
+        if (tau_mode == HSG_TAU_TABLE && dtau_part)
+            return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
+        return 0;
+    }
+    const int ne = ne_bucket((D + lph - 1) / lph);
+    const char *oe = getenv("HSG_GAT_NOH_OCC");                           // dev A/B
+    if (oe && atoi(oe) == 5 && tau_mode == HSG_TAU_TABLE)
+        return bwd_dst_dispatch<HSG_TAU_TABLE, 5, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
+                                                        nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
+    if (tau_mode == HSG_TAU_TABLE)
+        return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
+                                                        nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
+    return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
+                                                       nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
 }
 
 int hsg_gat_bwd_src_blocks(const hsg_rel *rel) {

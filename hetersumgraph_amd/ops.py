@@ -16,6 +16,7 @@ training step can be captured into a HIP graph.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -116,12 +117,17 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
-def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None):
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None, keep_h=True):
     """Forward of one multi-head application with the TF-IDF-table edge term:
     3 launches (attention parameters -> tau table, sigma, edge pass; 2 when
     ``tables`` = :func:`attn_tables` of this layer is passed in).  ``out``: a contiguous
     [n_dst, H*D] buffer for the result (with an origin).  ``sigma``: the source logits
-    when the head projection already produced them.  Returns (out, saved)."""
+    when the head projection already produced them.  ``keep_h=False`` (with an origin,
+    where hsg_gat_bwd_dst_noh covers the shape, and HSG_GAT_NOH=1): h is not stored; the
+    backward takes elu'(h) from out - origin and G.h from the edge dots.  Opt-in: at
+    cfg2 the S2W forward drops 22.6 -> 18.3 us but the dst pass, which then reads out
+    and origin instead of h, rises 33 -> 39.6 us (step +8 us).  Returns
+    (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
     if Z.shape != (n_src, HD):
@@ -134,7 +140,9 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         sigma = Z.new_empty(n_src, H)
         check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
-    h = Z.new_empty(n_dst, HD)
+    no_h = (not keep_h and origin is not None and os.environ.get("HSG_GAT_NOH", "0") == "1"
+            and bool(lib.hsg_gat_bwd_dst_noh_supported(relp, H, D)))
+    h = None if no_h else Z.new_empty(n_dst, HD)
     if origin is None:
         out = None
     elif out is None:
@@ -145,7 +153,8 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
                           ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
     _clock_stop(tok, Z)
-    saved = (Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, origin is not None)
+    saved = (Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, origin is not None,
+             (out, origin) if no_h else None)
     return (out if origin is not None else h), saved
 
 
@@ -158,11 +167,11 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     caller runs :func:`attn_params_finish` once for all applications of the layer.
     The origin gradient is ``dout`` itself."""
     lib = load()
-    Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin = saved
+    Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin, xo = saved
     dout = dout.contiguous()
     st = stream_of(Z)
     relp = ctypes.byref(rel.cstruct())
-    G = torch.empty_like(h)
+    G = torch.empty_like(dout)
     dpre = Z.new_empty(rel.n_typed, H)
     nbd = lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
@@ -170,9 +179,14 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     nbs = lib.hsg_gat_bwd_src_blocks(relp)
     da1p = Z.new_empty(nbs, H * D)
     tok = _clock_start(("gat_bwd", rel.kind), Z)
-    check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
-                              ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                              ptr(dtp), st), "hsg_gat_bwd_dst")
+    if xo is not None:                  # forward without h (keep_h=False)
+        check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                      ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                      ptr(dtp), st), "hsg_gat_bwd_dst_noh")
+    else:
+        check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
+                                  ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                  ptr(dtp), st), "hsg_gat_bwd_dst")
     check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
                               ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
           "hsg_gat_bwd_src")
@@ -232,7 +246,7 @@ class _GatHeadsTable(torch.autograd.Function):
     def backward(ctx, dout):
         saved = tuple(ctx.saved_tensors) + ctx.rest
         attn, T, wf, bf = saved[1:5]
-        has_origin = saved[-1]
+        has_origin = saved[15]
         dattn, dwf, dT = torch.empty_like(attn), torch.empty_like(wf), torch.empty_like(T)
         dbf = torch.empty_like(bf) if bf is not None else None
         need = ctx.needs_input_grad

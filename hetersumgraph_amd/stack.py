@@ -120,7 +120,7 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
-                              out=x_out, sigma=sigma)
+                              out=x_out, sigma=sigma, keep_h=False)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
                           lay.p_ffn, lay.eps, H_out=H_out, wsplit=wsplit, rng=draws[1])

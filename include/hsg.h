@@ -61,7 +61,8 @@ typedef struct hsg_rel {
  *   m_v   = max(max_e s_e, 0 if phantom_v>0),  l_v = sum_e exp(s_e-m_v) + phantom_v*exp(-m_v)
  *   h[v]  = sum_e exp(s_e-m_v)/l_v * Z[src_e, k, :]      (0 if v has no in-edges)
  *   out   = origin ? elu(h) + origin : h
- * Saved for backward: h, m, l ([n_dst, H] each). */
+ * Saved for backward: h, m, l ([n_dst, H] each).  With an origin, h may be NULL (not
+ * stored): the backward is then hsg_gat_bwd_dst_noh. */
 int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
                 const float *Z, const float *sigma, const float *tau, const float *origin,
                 float *h, float *out, float *m, float *l, void *stream);
@@ -78,6 +79,17 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
 
 /* Number of partial rows hsg_gat_bwd_dst writes into dtau_part. */
 int hsg_gat_bwd_blocks(const hsg_rel *rel);
+
+/* hsg_gat_bwd_dst with origin_mode = 1 for a forward that did not store h
+ * (hsg_gat_fwd with h = NULL): elu'(h) from x - origin (x = the forward's out) and
+ * G_v.h_v = sum_e alpha_ek G_v.Z_u over the typed edges.  Same outputs and dtau_part
+ * rows as hsg_gat_bwd_dst; hsg_gat_bwd_dst_noh_supported(rel, H, D) tells whether the
+ * shape has this form (the feature-split pass: D > 16, short segments). */
+int hsg_gat_bwd_dst_noh_supported(const hsg_rel *rel, int H, int D);
+int hsg_gat_bwd_dst_noh(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
+                        const float *Z, const float *sigma, const float *tau,
+                        const float *x, const float *origin, const float *m, const float *l,
+                        const float *dout, float *G, float *dpre, float *dtau_part, void *stream);
 
 /* Backward, source-centric half (CSC): for every source u
  *   dZ[u, k, :]  = sum_{e: src_e = u} alpha_ek * G[dst_e, k, :]  (+ dsigma[u,k]*a1[k,:] if a1)

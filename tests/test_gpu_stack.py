@@ -70,10 +70,14 @@ def _zero(mods, T, Xw, Xs):
         t.grad = None
 
 
-@pytest.mark.parametrize("kind,train,word_grad,reps,n_iter", [
-    ("hsg", True, False, 1, 2), ("hsg", True, True, 2, 2), ("hsg", False, True, 1, 1),
-    ("hdsg", True, True, 1, 2), ("hsg", True, False, 1, 3)])
-def test_fused_stack_matches_layerwise(monkeypatch, kind, train, word_grad, reps, n_iter):
+@pytest.mark.parametrize("kind,train,word_grad,reps,n_iter,noh", [
+    ("hsg", True, False, 1, 2, 0), ("hsg", True, True, 2, 2, 0), ("hsg", False, True, 1, 1, 0),
+    ("hdsg", True, True, 1, 2, 0), ("hsg", True, False, 1, 3, 0),
+    # the fused stack's S2W edge pass without a stored h (hsg_gat_bwd_dst_noh) against
+    # the layer-wise path, which keeps h
+    ("hsg", True, True, 2, 2, 1), ("hdsg", True, True, 1, 2, 1), ("hsg", False, True, 1, 1, 1)])
+def test_fused_stack_matches_layerwise(monkeypatch, kind, train, word_grad, reps, n_iter, noh):
+    monkeypatch.setenv("HSG_GAT_NOH", str(noh))
     G = _graph(kind, 3)
     w2s, s2w, T = _modules(7, 0.1)
     for m in (w2s, s2w):
