@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int SPH = (D + 15) / 16, NS = H * SPH, NG = (NS + SG - 1) / SG;
     const int lane = threadIdx.x & 63;
-    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int task = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int rt = task / NG, gq = task - rt * NG;
     const int i0 = rt * 16;
     if (i0 >= n) return;                          // whole wave: no barriers in this kernel
@@ -999,21 +999,25 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
     }
     int pf = 1;                                                                       // register ring depth (2, 4: no gain, tools/ab.py)
     if (const char *e = getenv("HSG_HPROJ_PF")) pf = atoi(e);                         // dev A/B (1, 2, 4)
+    // one wave per block: the small S2W grid (420 waves at cfg2) spreads over more CUs
+    // (8.84 -> 8.34 us per launch in the trace; step -3 us and +-0 us in two A/Bs)
+    int wpb = 1;
+    if (const char *e = getenv("HSG_HPROJ_WPB")) wpb = atoi(e) == 4 ? 4 : (atoi(e) == 2 ? 2 : 1);   // dev A/B
 #define HSG_HF(SG_)                                                                                              \
     {                                                                                                            \
         const long tasks = (long)((n + 15) / 16) * ((ns + SG_ - 1) / SG_);                                       \
-        const dim3 grid((unsigned)((tasks + 3) / 4));                                                            \
+        const dim3 grid((unsigned)((tasks + wpb - 1) / wpb)), blk(64 * wpb);                                     \
         if (vec && pf == 4)                                                                                      \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 4>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 4>), grid, blk, 0, (hipStream_t)stream, n, in, H, D,       \
                                X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
         else if (vec && pf == 2)                                                                                 \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 2>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 2>), grid, blk, 0, (hipStream_t)stream, n, in, H, D,       \
                                X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
         else if (vec)                                                                                            \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, true>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true>), grid, blk, 0, (hipStream_t)stream, n, in, H, D, X,       \
                                ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
         else                                                                                                     \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, false>), grid, dim3(256), 0, (hipStream_t)stream, n, in, H, D, X, \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, false>), grid, blk, 0, (hipStream_t)stream, n, in, H, D, X,      \
                                ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
     }
     if (sg == 1) HSG_HF(1) else if (sg == 2) HSG_HF(2) else HSG_HF(4)
