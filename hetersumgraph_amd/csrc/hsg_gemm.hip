@@ -500,8 +500,12 @@ struct Stage3 {
 // are issued while tile kt is multiplied, two tiles of MFMA work to hide their
 // latency).  Two barriers per K tile.  NL = 1 is a bf16-operand probe of the same
 // pipeline (dev only).  The epilogue (and split-K / column partials) is k_gemm's.
+// 64x64 transpose-read tiles (the weight gradients): 5 waves per SIMD (102 -> 96 VGPRs,
+// no spill), so the weight-gradient
+// grid (2,560 blocks at cfg2) runs in exactly two rounds of resident blocks instead of
+// 2.5 at 4 per CU
 template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL, int IGLP = -1, int NT = 256>
-__global__ __launch_bounds__(NT, NT == 256 ? 2 : 1) void k_gemm3(GemmArgs p) {
+__global__ __launch_bounds__(NT, NT == 256 ? (BM * BN == 64 * 64 && !AK && !BKC ? 5 : 2) : 1) void k_gemm3(GemmArgs p) {
     constexpr int WGN = NT / 128;                          // waves along N (2 along M)
     constexpr int WM = BM / 2, WN = BN / WGN;
     constexpr int TM = WM / 32, TN = WN / 32;
