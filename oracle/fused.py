@@ -13,7 +13,10 @@ Reference lines restated:
   typed_relation  -- GATLayer.py:105-107 / 143-145 (filters) + DGL 0.4 pull's
                      in-edge set (113 / 149) incl. untyped "phantom" in-edges
   wswgat_layer    -- GAT.py:45-59, GATStackLayer.py:55-59, GATLayer.py:89-102,
-                     110-116, 128-152, and PositionwiseFeedForward 35-44
+                     110-116, 128-152, and PositionwiseFeedForward 35-44;
+                     train mode takes explicit keep-masks for the per-head input
+                     dropout (GATStackLayer.py:56) and the FFN output dropout
+                     (GATLayer.py:41) -- oracle/masks.py computes the kernels' ones
 """
 from __future__ import annotations
 
@@ -60,8 +63,10 @@ def n_heads(params, prefix=""):
     return i
 
 
-def gat_heads(rel, X, params, T, prefix=""):
-    """Concatenated head outputs (before ELU) -- GATStackLayer.py:55-59."""
+def gat_heads(rel, X, params, T, prefix="", keep=None, scale=1.0):
+    """Concatenated head outputs (before ELU) -- GATStackLayer.py:55-59.
+    ``keep``: train mode, bool [H, n_src, in] per-head input keep-masks
+    (GATStackLayer.py:56, ``head(g, self.dropout(h))``), kept values x ``scale``."""
     H = n_heads(params, prefix)
     e_src = torch.from_numpy(rel["e_src"])
     e_dst = torch.from_numpy(rel["e_dst"])
@@ -70,8 +75,9 @@ def gat_heads(rel, X, params, T, prefix=""):
     phantom = torch.from_numpy(rel["phantom"]).to(X.dtype)
     tfe = torch.where((tf >= 0).unsqueeze(1), T[tf.clamp_min(0)], torch.zeros((), dtype=X.dtype))
     outs = []
-    for hd in _heads(params, prefix, H):
-        z = X @ hd["fc"].t()                                   # GATLayer.py:110 / 146
+    for k, hd in enumerate(_heads(params, prefix, H)):
+        Xk = X if keep is None else X * (torch.as_tensor(keep[k]).to(X.dtype) * scale)
+        z = Xk @ hd["fc"].t()                                  # GATLayer.py:110 / 146
         D = z.shape[1]
         dfeat = tfe @ hd["feat_w"].t()
         if hd["feat_b"] is not None:
@@ -92,20 +98,26 @@ def gat_heads(rel, X, params, T, prefix=""):
     return torch.cat(outs, 1)
 
 
-def ffn(x, params, prefix=""):
-    """PositionwiseFeedForward (GATLayer.py:35-44), eval mode."""
+def ffn(x, params, prefix="", keep=None, scale=1.0):
+    """PositionwiseFeedForward (GATLayer.py:35-44).  ``keep``: train mode, the bool
+    [n, d] keep-mask of the output dropout (GATLayer.py:41), kept values x ``scale``."""
     w1 = params[f"{prefix}ffn.w_1.weight"].squeeze(-1)
     w2 = params[f"{prefix}ffn.w_2.weight"].squeeze(-1)
     y = F.relu(x @ w1.t() + params[f"{prefix}ffn.w_1.bias"]) @ w2.t() + params[f"{prefix}ffn.w_2.bias"]
+    if keep is not None:
+        y = y * (torch.as_tensor(keep).to(y.dtype) * scale)
     return F.layer_norm(y + x, (x.shape[1],), params[f"{prefix}ffn.layer_norm.weight"],
                         params[f"{prefix}ffn.layer_norm.bias"], 1e-5)
 
 
-def wswgat_layer(kind, rel, Xw, Xs, params, T, prefix=""):
-    """WSWGAT.forward(g, w, s) (GAT.py:45-59), eval mode."""
+def wswgat_layer(kind, rel, Xw, Xs, params, T, prefix="", masks=None):
+    """WSWGAT.forward(g, w, s) (GAT.py:45-59).  Eval mode, or train mode with
+    ``masks`` = (head keep [H, n_src, in], head scale, FFN keep [n_dst, d], FFN
+    scale) -- e.g. oracle/masks.py's restatement of the kernels' masks."""
     origin, neighbor = (Xs, Xw) if kind == "W2S" else (Xw, Xs)
-    h = F.elu(gat_heads(rel, neighbor, params, T, prefix)) + origin
-    return ffn(h, params, prefix)
+    hk, hs, fk, fs = masks if masks is not None else (None, 1.0, None, 1.0)
+    h = F.elu(gat_heads(rel, neighbor, params, T, prefix, keep=hk, scale=hs)) + origin
+    return ffn(h, params, prefix, keep=fk, scale=fs)
 
 
 def as_params(module_or_dict, dtype=torch.float64, requires_grad=True):

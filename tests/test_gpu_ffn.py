@@ -35,8 +35,9 @@ def test_ffn_eval_matches_fp64(n, d, dh):
 
 
 def test_ffn_dropout_semantics():
-    """Train mode: drop rate ~p, kept values scaled by 1/(1-p), backward uses the
-    forward's mask, and a new seed gives a new mask."""
+    """Train mode: drop rate ~p, kept values scaled by 1/(1-p), and a new call gives a
+    new mask (the numeric forward/backward with the same mask:
+    test_ffn_train_matches_fp64_with_same_mask)."""
     from hetersumgraph_amd import rng
     from hetersumgraph_amd.ffn import ffn_forward
     torch.manual_seed(0)
@@ -59,13 +60,44 @@ def test_ffn_dropout_semantics():
     assert abs(rate - p) < 0.005, rate
     out2 = ffn_forward(x0, w1, b1, w2z, b2o, g, b, p_drop=p)
     assert not torch.equal(out2 > 0, kept)             # new offset -> new mask
-    rng.get("cuda").advance()
-    # gradient flows only through kept elements of the dropout branch
-    xr = torch.randn(n, d, device="cuda", requires_grad=True)
-    w1r = w1.clone().requires_grad_()
-    out3 = ffn_forward(xr, w1r, b1, w2, b2, g, b, p_drop=p)
-    out3.sum().backward()
-    assert torch.isfinite(xr.grad).all() and torch.isfinite(w1r.grad).all()
+
+
+@pytest.mark.parametrize("n,d,dh,seed", [(3000, 300, 512, 21), (1120, 64, 512, 22), (37, 64, 512, 23),
+                                         (77, 300, 100, 24)])
+def test_ffn_train_matches_fp64_with_same_mask(n, d, dh, seed):
+    """Train mode (dropout 0.1, GATLayer.py:41) -- forward and every gradient against
+    an fp64 torch reference fed the same keep-mask, computed on the host from
+    (seed, offset) by oracle/masks.py (bit-exact vs the kernels:
+    test_gpu_dropout_masks.py).  d = 300: split GEMMs + hsg_ln_fwd / hsg_ln_bwd; d = 64:
+    the one-launch hsg_ffn_small_fwd / _bwd.  Tolerances as the eval test."""
+    from hetersumgraph_amd import rng
+    from hetersumgraph_amd.ffn import ffn_forward
+    from oracle import masks
+    p = 0.1
+    torch.manual_seed(seed)
+    x = torch.randn(n, d, dtype=torch.float64)
+    ps = [torch.randn(dh, d, dtype=torch.float64) / d ** 0.5, 0.1 * torch.randn(dh, dtype=torch.float64),
+          torch.randn(d, dh, dtype=torch.float64) / dh ** 0.5, 0.1 * torch.randn(d, dtype=torch.float64),
+          1 + 0.1 * torch.randn(d, dtype=torch.float64), 0.1 * torch.randn(d, dtype=torch.float64)]
+    R = torch.randn(n, d, dtype=torch.float64)
+    dl = [t.float().cuda().requires_grad_() for t in [x] + ps]
+    rng.manual_seed(seed)
+    out = ffn_forward(*dl, p_drop=p)
+    off = rng.get("cuda").offset
+    (out * R.float().cuda()).sum().backward()
+    keep = torch.from_numpy(masks.ffn_keep(seed, off, n, d, p)).double()
+    scale = masks.ffn_scale(p)
+    leaves = [t.clone().requires_grad_() for t in [x] + ps]
+    xr, w1, b1, w2, b2, g, b = leaves
+    y = (F.relu(xr @ w1.t() + b1) @ w2.t() + b2) * keep * scale
+    ref = F.layer_norm(y + xr, (d,), g, b, 1e-5)
+    (ref * R).sum().backward()
+    assert 0.05 < 1 - keep.mean().item() < 0.15
+    assert (out.detach().cpu().double() - ref.detach()).abs().max().item() < 2e-5
+    for name, a, r in zip(("x", "w1", "b1", "w2", "b2", "gamma", "beta"), dl, leaves):
+        scale_g = r.grad.abs().max().item()
+        err = (a.grad.cpu().double() - r.grad).abs().max().item()
+        assert err <= 1e-4 * max(scale_g, 1.0), (name, err, scale_g)
 
 
 @pytest.mark.parametrize("n,p", [(1120, 0.1), (1120, 0.0), (37, 0.1), (1, 0.3), (16 * 97 + 5, 0.1)])

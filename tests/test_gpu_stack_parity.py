@@ -9,9 +9,14 @@ at the BASELINE.json workload sizes:
 * cfg5 -- 32 NYT50-shaped docs (N=80, W=900, k=14; 160 phantom in-edges per
   sentence), in fp32 and in the bf16-GEMM-operand mode BASELINE.json names for it.
 
-Eval mode (dropout cannot match the oracle draw for draw); outputs and the
-gradients of both input states, the shared _TFembed table and every parameter
-(reference key names) after ``s.backward(R)``.
+Eval mode (test_stack_vs_oracle_full_size), and TRAIN mode -- the configuration
+bench.py times: dropout 0.1 on every head's input (GATStackLayer.py:56) and on
+every FFN output (GATLayer.py:41) -- with the oracle fed the same keep-masks,
+computed on the host from (seed, offset) by oracle/masks.py, which restates the
+kernels' mask generators bit for bit (test_gpu_dropout_masks.py)
+(test_train_stack_vs_oracle_full_size).  Outputs and the gradients of both input
+states, the shared _TFembed table and every parameter (reference key names) after
+``s.backward(R)``.
 
 Tolerances (written here):
 * outputs: fp32 <= 2e-5 absolute (LayerNorm outputs are O(1)); bf16-GEMM <= 2e-2;
@@ -66,8 +71,25 @@ def check_grad(fails, name, got, ref, fro_tol, bad_frac, worst_tol, scale_ref=No
         fails.append((name, s))
 
 
-def oracle_stack(z, seed):
-    """fp64 oracle: s1 = W2S(w0, s0); then n_iter x (w = S2W(w, s); s = W2S(w, s))."""
+def train_masks(drop_seed, off0, n_w, n_s, p=0.1):
+    """The keep-masks of the fused stack's forward, application by application
+    (W2S, then n_iter x (S2W, W2S)), in the order stack._GatStack draws them: per
+    application one head-projection call (offset +1) then one FFN call (+1)."""
+    from oracle import masks
+    hs, fs = masks.hproj_scale(p), masks.ffn_scale(p)
+    out, off = [], off0
+    for kind in ["W2S"] + ["S2W", "W2S"] * N_ITER:
+        n_src, d_in, H, n_dst, d = (n_w, 300, 8, n_s, 64) if kind == "W2S" else (n_s, 64, 6, n_w, 300)
+        hk = masks.hproj_keep(drop_seed, off + 1, n_src, d_in, H, p)
+        fk = masks.ffn_keep(drop_seed, off + 2, n_dst, d, p)
+        out.append((hk, hs, fk, fs))
+        off += 2
+    return out
+
+
+def oracle_stack(z, seed, masks=None):
+    """fp64 oracle: s1 = W2S(w0, s0); then n_iter x (w = S2W(w, s); s = W2S(w, s)).
+    ``masks``: train mode, one (head keep, scale, FFN keep, scale) per application."""
     from oracle import fused
     a = concat_arrays(z)
     rws = fused.typed_relation("W2S", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
@@ -76,16 +98,20 @@ def oracle_stack(z, seed):
     Xw, Xs, T = (t.double().requires_grad_() for t in (Xw, Xs, T))
     w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
     p1, p2 = fused.as_params(w2s), fused.as_params(s2w)
-    w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T)
+    m = iter(masks) if masks is not None else None
+    nxt = (lambda: next(m)) if m is not None else (lambda: None)
+    w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T, masks=nxt())
     for _ in range(N_ITER):
-        w = fused.wswgat_layer("S2W", rsw, w, s, p2, T)
-        s = fused.wswgat_layer("W2S", rws, w, s, p1, T)
+        w = fused.wswgat_layer("S2W", rsw, w, s, p2, T, masks=nxt())
+        s = fused.wswgat_layer("W2S", rws, w, s, p1, T, masks=nxt())
     R = torch.from_numpy(np.random.default_rng(seed).standard_normal(tuple(s.shape)))
     (s * R).sum().backward()
     return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, p1=p1, p2=p2, R=R)
 
 
-def gpu_stack(z, seed, R):
+def gpu_stack(z, seed, R, train_seed=None):
+    """The fused stack on the GPU; ``train_seed``: train mode (dropout 0.1) with the
+    dropout stream reseeded to it (returns the offset the stack's draws start at)."""
     from hetersumgraph_amd.HiGraph import register_tfidf_table
     from hetersumgraph_amd.stack import fused_stack_ok, gat_stack
     dev = torch.device("cuda")
@@ -97,31 +123,31 @@ def gpu_stack(z, seed, R):
     register_tfidf_table(G, T)
     w2s, s2w = seeded_gat_params(seed * 100 + 1, seed * 100 + 2)
     w2s, s2w = w2s.to(dev), s2w.to(dev)
+    off0 = None
+    if train_seed is not None:
+        from hetersumgraph_amd import rng
+        w2s.train()
+        s2w.train()
+        rng.manual_seed(train_seed)
+        off0 = rng.get(dev).offset
     assert fused_stack_ok(G, w2s, s2w, T, Xw, Xs)
     s = gat_stack(G, w2s, s2w, T, Xw, Xs, N_ITER)
+    if train_seed is not None:
+        assert rng.get(dev).offset == off0 + 2 * (2 * N_ITER + 1)     # one head + one FFN draw per application
     assert type(s.grad_fn).__name__.startswith("_GatStack")        # the timed node, not the layer path
     s.backward(R.to(dev, torch.float32))
     torch.cuda.synchronize()
-    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w)
+    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w, off0=off0)
 
 
 CASES = [("cfg2", "f32", 31), ("cfg4", "f32", 32), ("cfg5", "f32", 33), ("cfg5", "bf16", 33)]
 
 
-@pytest.mark.parametrize("config,dtype,seed", CASES)
-def test_stack_vs_oracle_full_size(config, dtype, seed):
-    from hetersumgraph_amd import synth
-    from hetersumgraph_amd.dense import gemm_dtype
+def compare(config, dtype, r, o, n_docs, n_edges):
     from hetersumgraph_amd.module.GATStackLayer import reference_named_grads
-    docs = synth.make_batch_docs(config, seed=0)
-    z = synth_fixture(docs)
-    n_edges = int(z["g_n_edges"].sum())
-    o = oracle_stack(z, seed)
-    with gemm_dtype(dtype):
-        r = gpu_stack(z, seed, o["R"])
     out_tol, fro_tol, worst_tol = (2e-5, 2e-4, 1e-2) if dtype == "f32" else (2e-2, 5e-2, 1e-1)
     err = (_f64(r["s"]) - o["s"]).abs().max().item()
-    print(f"{config} {dtype}: {len(docs)} docs, {n_edges} edges, output max|diff| {err:.3e}")
+    print(f"{config} {dtype}: {n_docs} docs, {n_edges} edges, output max|diff| {err:.3e}")
     assert err <= out_tol
     bad_frac = 0.005 if dtype == "f32" else 1.0
     fails = []
@@ -151,3 +177,41 @@ def test_stack_vs_oracle_full_size(config, dtype, seed):
             n += 1
     assert n == 8 * 3 + 6 * 4 + 12
     assert not fails, fails
+
+
+@pytest.mark.parametrize("config,dtype,seed", CASES)
+def test_stack_vs_oracle_full_size(config, dtype, seed):
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.dense import gemm_dtype
+    docs = synth.make_batch_docs(config, seed=0)
+    z = synth_fixture(docs)
+    n_edges = int(z["g_n_edges"].sum())
+    o = oracle_stack(z, seed)
+    with gemm_dtype(dtype):
+        r = gpu_stack(z, seed, o["R"])
+    compare(config, dtype, r, o, len(docs), n_edges)
+
+
+TRAIN_CASES = [("cfg2", "f32", 41), ("cfg4", "f32", 42), ("cfg5", "f32", 43), ("cfg5", "bf16", 44)]
+
+
+@pytest.mark.parametrize("config,dtype,seed", TRAIN_CASES)
+def test_train_stack_vs_oracle_full_size(config, dtype, seed):
+    """The timed configuration: train mode, dropout 0.1 (head inputs and FFN outputs),
+    the fused stack's kernels (hsg_dropmask_multi, the head-projection forward with
+    the sigma epilogue, hsg_hproj_dx / _dw through the same bits, the masked LN /
+    narrow-FFN backward) against the fp64 oracle with the host-computed masks, at
+    full cfg2 / cfg4 / cfg5 size -- same tolerances as eval mode."""
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.dense import gemm_dtype
+    docs = synth.make_batch_docs(config, seed=0)
+    z = synth_fixture(docs)
+    n_edges = int(z["g_n_edges"].sum())
+    drop_seed = 1000 + seed
+    R = torch.from_numpy(np.random.default_rng(seed).standard_normal((int(z["n_s"]), 64)))
+    with gemm_dtype(dtype):
+        r = gpu_stack(z, seed, R, train_seed=drop_seed)
+    ms = train_masks(drop_seed, r["off0"], int(z["n_w"]), int(z["n_s"]))
+    o = oracle_stack(z, seed, masks=ms)
+    assert torch.equal(o["R"], R)
+    compare(config, dtype, r, o, len(docs), n_edges)
