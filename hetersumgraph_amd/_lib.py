@@ -66,7 +66,7 @@ _SIGS = {
     "hsg_attn_params_finish": [_I, _I, _I] + [_P] * 9 + [_I, _P],
     "hsg_attn_src_logits": [_I, _I, _I, _P, _P, _P, _P],
     "hsg_version": [],
-    "hsg_kclock_arm": [_P, _P],
+    "hsg_kclock_arm": [_P, _P, _P],
     "hsg_kclock_pending": [],
     "hsg_seed_advance": [_P, _P, _P],
     "hsg_gat_bwd_dst_noh_supported": [_RELP, _I, _I],
@@ -181,15 +181,21 @@ class KernelClock:
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(st)                   # creates the events; the kernels re-record them
         e1.record(st)
-        load().hsg_kclock_arm(e0.cuda_event, e1.cuda_event)
+        load().hsg_kclock_arm(st.cuda_stream, e0.cuda_event, e1.cuda_event)
         return (tag, e0, e1)
 
     def stop(self, token, device):
         tag, e0, e1 = token
         if load().hsg_kclock_pending():
-            load().hsg_kclock_arm(None, None)
+            load().hsg_kclock_arm(None, None, None)
             raise RuntimeError(f"kernel clock {tag}: the launch path did not record the armed events")
         self.events.setdefault(tag, []).append((e0, e1))
+
+    @staticmethod
+    def disarm():
+        """Drop this thread's armed events (error path: the entry point raised before
+        its launches consumed them, so they must not outlive their Event objects)."""
+        load().hsg_kclock_arm(None, None, None)
 
     def durations_ms(self):
         """tag -> list of per-launch durations (ms); synchronises."""

@@ -987,7 +987,15 @@ int launch_status() {
 // recorded by the next edge kernels' own dispatch packets (hipExtLaunchKernel) --
 // start by the first kernel of an entry point, stop by its last -- so the measured
 // interval is the kernels themselves, without event packets around them.  One-shot.
-hipEvent_t g_kc_start = nullptr, g_kc_stop = nullptr;
+// The armed state is THREAD-LOCAL and bound to one stream: only launches from the
+// arming thread onto that stream consume it, so entry points called from other
+// threads, or on other streams of the same thread, never see it (the C ABI stays
+// reentrant across threads and streams).
+struct KClock {
+    hipStream_t stream = nullptr;
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+thread_local KClock t_kc;
 hipEvent_t kc_take(hipEvent_t &e, bool use) {
     if (!use) return nullptr;
     hipEvent_t r = e;
@@ -996,8 +1004,8 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
 }
 #define HSG_KLAUNCH(FIRST, LAST, KERNEL, GRID, BLOCK, ST, ...)                                              \
     do {                                                                                                    \
-        if (((FIRST) && g_kc_start) || ((LAST) && g_kc_stop)) {                                            \
-            hipEvent_t e0_ = kc_take(g_kc_start, FIRST), e1_ = kc_take(g_kc_stop, LAST);                    \
+        if (t_kc.stream == (ST) && (((FIRST) && t_kc.start) || ((LAST) && t_kc.stop))) {                  \
+            hipEvent_t e0_ = kc_take(t_kc.start, FIRST), e1_ = kc_take(t_kc.stop, LAST);                    \
             hipExtLaunchKernelGGL(KERNEL, GRID, BLOCK, 0, ST, e0_, e1_, 0, __VA_ARGS__);                    \
         } else {                                                                                            \
             hipLaunchKernelGGL(KERNEL, GRID, BLOCK, 0, ST, __VA_ARGS__);                                    \
@@ -1380,13 +1388,14 @@ int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, fl
     return launch_status();
 }
 
-int hsg_kclock_arm(void *start_event, void *stop_event) {
-    g_kc_start = (hipEvent_t)start_event;
-    g_kc_stop = (hipEvent_t)stop_event;
+int hsg_kclock_arm(void *stream, void *start_event, void *stop_event) {
+    t_kc.stream = (hipStream_t)stream;
+    t_kc.start = (hipEvent_t)start_event;
+    t_kc.stop = (hipEvent_t)stop_event;
     return 0;
 }
 
-int hsg_kclock_pending(void) { return (g_kc_start ? 1 : 0) + (g_kc_stop ? 2 : 0); }
+int hsg_kclock_pending(void) { return (t_kc.start ? 1 : 0) + (t_kc.stop ? 2 : 0); }
 
 const char *hsg_version(void) { return "hsg 0.1 gfx950 (fp32 WSWGAT edge kernels)"; }
 

@@ -32,6 +32,13 @@ def _clock_start(tag, t):
 def _clock_stop(tok, t):
     if tok is not None:
         _lib.CLOCK.stop(tok, t.device)
+
+
+def _clock_abort(tok):
+    if tok is not None:
+        _lib.KernelClock.disarm()
+
+
 from .relation import N_BOX
 
 LEAKY_SLOPE = 0.01   # F.leaky_relu default (GATLayer.py:92, 131)
@@ -150,8 +157,12 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     m = Z.new_empty(n_dst, H)
     l = Z.new_empty(n_dst, H)
     tok = _clock_start(("gat_fwd", rel.kind), Z)
-    check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                          ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+    try:
+        check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+    except BaseException:
+        _clock_abort(tok)
+        raise
     _clock_stop(tok, Z)
     saved = (Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, origin is not None,
              (out, origin) if no_h else None)
@@ -179,17 +190,21 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     nbs = lib.hsg_gat_bwd_src_blocks(relp)
     da1p = Z.new_empty(nbs, H * D)
     tok = _clock_start(("gat_bwd", rel.kind), Z)
-    if xo is not None:                  # forward without h (keep_h=False)
-        check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                                      ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                                      ptr(dtp), st), "hsg_gat_bwd_dst_noh")
-    else:
-        check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
-                                  ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                                  ptr(dtp), st), "hsg_gat_bwd_dst")
-    check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
-                              ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
-          "hsg_gat_bwd_src")
+    try:
+        if xo is not None:                  # forward without h (keep_h=False)
+            check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                          ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                          ptr(dtp), st), "hsg_gat_bwd_dst_noh")
+        else:
+            check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
+                                      ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                      ptr(dtp), st), "hsg_gat_bwd_dst")
+        check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                                  ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
+              "hsg_gat_bwd_src")
+    except BaseException:
+        _clock_abort(tok)
+        raise
     _clock_stop(tok, Z)
     if stage is not None and len(stage) == 3:       # (batch, key, workspace): staged with every application
         batch, key, ws = stage

@@ -106,12 +106,15 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
 int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
 
 /* Measurement hook (bench.py's in-step kernel clock; not part of the reference
- * surface): the next hsg_gat_fwd records start_event / stop_event (hipEvent_t created
- * with timing) from its kernel's own dispatch packet (hipExtLaunchKernel); the next
- * hsg_gat_bwd_dst records start_event at its kernel and the following hsg_gat_bwd_src
- * stop_event at its kernel.  One-shot: a consumed event is disarmed.  Either may be
- * NULL.  hsg_kclock_pending: bit 0 / bit 1 set while start / stop is still armed. */
-int hsg_kclock_arm(void *start_event, void *stop_event);
+ * surface): the next hsg_gat_fwd launched FROM THE CALLING THREAD ON `stream` records
+ * start_event / stop_event (hipEvent_t created with timing) from its kernel's own
+ * dispatch packet (hipExtLaunchKernel); the next hsg_gat_bwd_dst records start_event
+ * at its kernel and the following hsg_gat_bwd_src stop_event at its kernel.  One-shot:
+ * a consumed event is disarmed.  Either event may be NULL (disarm).  The armed state
+ * is thread-local and bound to `stream`, so launches from other threads or onto other
+ * streams are unaffected.  hsg_kclock_pending: bit 0 / bit 1 set while the calling
+ * thread's start / stop is still armed. */
+int hsg_kclock_arm(void *stream, void *start_event, void *stop_event);
 int hsg_kclock_pending(void);
 
 /* sigma[u, k] = <Z[u, k, :], a1[k, :]> -- the z_src part of attn_fc
