@@ -34,7 +34,8 @@ _FNS = {"f32": "hsg_gemm_f32", "f32mfma": "hsg_gemm_f32_mfma", "bf16": "hsg_gemm
 def set_gemm_dtype(dtype):
     """'f32' (fp32-accurate, 3-limb bf16 split), 'f32mfma' (exact-f32 instruction) or
     'bf16' (bf16 operands, fp32 accumulate) for every GEMM issued through
-    :func:`gemm` (FFN, sentence CNN)."""
+    :func:`gemm` without an explicit ``dtype`` (the FFN, the sentence CNN).  The
+    head projection (train: hsg_hproj_*, eval: :func:`linear`) stays fp32."""
     global _GEMM_DTYPE
     if dtype not in _FNS:
         raise ValueError(f"gemm dtype must be one of {sorted(_FNS)}, not {dtype!r}")
@@ -207,19 +208,21 @@ def splits_for(M, N, K, n_cu=256):
 
 class _Linear(torch.autograd.Function):
     """Z = X W^T on hsg_gemm_f32 with its backward (dX = dZ W, dW = dZ^T X): the
-    eval-mode head projection fc (GATLayer.py:110 / 146) without a vendor GEMM."""
+    eval-mode head projection fc (GATLayer.py:110 / 146) without a vendor GEMM.
+    Always fp32-accurate ('f32'), whatever the process-wide GEMM mode: the training
+    head projection (hsg_hproj_*) is fp32 too, so eval and train project alike."""
 
     @staticmethod
     def forward(ctx, X, W):
         ctx.save_for_backward(X, W)
-        return gemm(X, W, b_t=True)
+        return gemm(X, W, b_t=True, dtype="f32")
 
     @staticmethod
     def backward(ctx, dZ):
         X, W = ctx.saved_tensors
         dZ = dZ.contiguous()
-        dX = gemm(dZ, W) if ctx.needs_input_grad[0] else None
-        dW = gemm(dZ, X, a_t=True) if ctx.needs_input_grad[1] else None
+        dX = gemm(dZ, W, dtype="f32") if ctx.needs_input_grad[0] else None
+        dW = gemm(dZ, X, a_t=True, dtype="f32") if ctx.needs_input_grad[1] else None
         return dX, dW
 
 

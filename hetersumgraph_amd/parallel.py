@@ -17,6 +17,8 @@ documents.  :func:`shard_fraction` gives n_r / N from the deterministic shard
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -129,6 +131,12 @@ class GradientReducer:
     The fused WSWGAT stack returns its parameter gradients through autograd
     (hetersumgraph_amd/stack.py), so its hooks fire when the stack node's backward
     ends -- before the encoder's backward runs.
+
+    One reduced backward per :meth:`finish`.  Gradient accumulation runs the
+    earlier micro-batches under :meth:`no_sync` (hooks idle, gradients accumulate
+    locally in ``p.grad``) and the last one outside it, whose hooks then reduce the
+    accumulated sums.  A second backward with hooks before :meth:`finish` raises
+    instead of silently reducing only the first one.
     """
 
     def __init__(self, params, group=None, bucket_bytes=2 << 20, scale=None):
@@ -143,6 +151,7 @@ class GradientReducer:
         self.ready = [0] * len(self.buckets)
         self.next = 0                        # next bucket to launch
         self.pending = []
+        self._sync = True
         self.hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params] \
             if self.world > 1 else []
 
@@ -153,8 +162,24 @@ class GradientReducer:
             self.pending.append(_launch(live, self.scale, self.world, self.group))
         self.next += 1
 
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Backward passes inside this context only accumulate into ``p.grad`` (the
+        micro-batches before the last one of a gradient-accumulation step)."""
+        prev, self._sync = self._sync, False
+        try:
+            yield
+        finally:
+            self._sync = prev
+
     def _on_grad(self, p):
-        self.ready[self.where[id(p)]] += 1
+        if not self._sync:
+            return
+        bi = self.where[id(p)]
+        if self.next == len(self.buckets) or self.ready[bi] >= len(self.buckets[bi]):
+            raise RuntimeError("GradientReducer: a second backward before finish() -- its gradients would not "
+                               "be reduced; run the earlier micro-batches under no_sync()")
+        self.ready[bi] += 1
         while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next]):
             self._launch_next()
 

@@ -118,7 +118,7 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
     elif lay.p_attn > 0:
         Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, bits=draws[0], wt=wt)
     else:
-        Z, hsaved = gemm(neighbor, lay.W, b_t=True), None
+        Z, hsaved = gemm(neighbor, lay.W, b_t=True, dtype="f32"), None      # fp32 in every GEMM mode, as hproj
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
                               out=x_out, sigma=sigma, keep_h=False)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
@@ -174,9 +174,9 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
             hproj_bwd(hsaved, dZ, dX=nb_grad, dX_acc=nb_acc, dW=dW, dW_acc=a_W, batch=batch, key=id(lay))
         else:                                   # eval-mode projection Z = neighbor W^T
             if nb_grad is not None:
-                gemm(dZ, lay.W, out=nb_grad, add=nb_grad if nb_acc else None)
+                gemm(dZ, lay.W, out=nb_grad, add=nb_grad if nb_acc else None, dtype="f32")
             if dW is not None:
-                gemm(dZ, neighbor, a_t=True, out=dW, add=dW if a_W else None)
+                gemm(dZ, neighbor, a_t=True, out=dW, add=dW if a_W else None, dtype="f32")
     return dx
 
 

@@ -54,7 +54,7 @@ def _loss(docs, params, T, seed_base=0):
     return total / len(docs)
 
 
-def _worker(rank, world, port, bucket_bytes, skewed, hooks):
+def _worker(rank, world, port, bucket_bytes, skewed, hooks, accum=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -74,7 +74,26 @@ def _worker(rank, world, port, bucket_bytes, skewed, hooks):
         assert frac == len(mine) / len(docs)
         local = _params()
         scale = frac if skewed else None
-        if hooks:
+        if hooks and accum:
+            # gradient accumulation: the shard's documents in two micro-batches, the
+            # first under no_sync(), each loss weighted by its share of the shard
+            red = GradientReducer(list(local.values()), bucket_bytes=bucket_bytes, scale=scale)
+            h = len(mine) // 2
+            with red.no_sync():
+                (_loss(mine[:h], local, T) * (h / len(mine))).backward()
+            assert red.next == 0 and not red.pending
+            (_loss(mine[h:], local, T) * ((len(mine) - h) / len(mine))).backward()
+            red.finish()
+            # a second hooked backward before finish() must raise, not drop gradients
+            extra = _params()
+            red2 = GradientReducer(list(extra.values()), bucket_bytes=bucket_bytes, scale=scale)
+            _loss(mine, extra, T).backward()
+            with pytest.raises(RuntimeError, match="second backward"):
+                _loss(mine, extra, T).backward()
+            red2.finish()
+            red2.remove()
+            red.remove()
+        elif hooks:
             red = GradientReducer(list(local.values()), bucket_bytes=bucket_bytes, scale=scale)
             _loss(mine, local, T).backward()
             red.finish()
@@ -98,6 +117,13 @@ def _worker(rank, world, port, bucket_bytes, skewed, hooks):
 def test_sharded_allreduce_equals_full_batch(bucket_bytes, skewed, hooks):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), bucket_bytes, skewed, hooks), nprocs=world, join=True)
+
+
+def test_reducer_gradient_accumulation_and_misuse():
+    """two backwards before finish() -- accumulation under no_sync() gives
+    the full-batch gradient; an unguarded second hooked backward raises."""
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), 65536, True, True, True), nprocs=world, join=True)
 
 
 def test_shard_documents_balanced_and_deterministic():
