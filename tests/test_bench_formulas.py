@@ -39,5 +39,22 @@ def test_full_stack_floor(cfg2_rels):
     items = bench.step_work(rw, rs, 2, "f32")
     floor, edge, dense, gflop = bench.full_stack_floor(items)
     assert 74 <= gflop <= 80
-    assert 0.45e-3 <= dense <= 0.52e-3
+    assert 0.45e-3 <= dense <= 0.54e-3          # incl. the ~20 us of split-K slab bytes
     assert abs(edge - 207.1e6 / 8e12) < 1e-7
+    # the S2W weight gradients' split-K slabs: 64 x [300 x 512] fp32 per weight, each
+    # written and read once (dense.gemm_slabs)
+    slabs = {n: b for n, b, _, _ in items if n.startswith("ffn_dw_slabs")}
+    assert round(slabs["ffn_dw_slabs_S2W"] / 1e6, 1) == round(2 * 2 * 4 * 64 * 300 * 512 / 1e6, 1)
+
+
+def test_dense_roofline_peak_follows_the_path():
+    """the f32 (split) GEMM issues six bf16 products per fp32-accurate
+    product, so its roofline is the bf16 MFMA peak on 6x the useful flops; the
+    fp32-equivalent figure is kept separately."""
+    import bench
+    r = bench.dense_roofline("hsg_gemm_f32_psw", 19200, 100.0, 5.9e9, 0.059, "f32")
+    assert r["peak"] == bench.BF16_MFMA_PEAK_TFLOPS and abs(r["achieved"] - 600.0) < 1e-9
+    assert abs(r["frac"] - 600.0 / 2500.0) < 1e-12
+    assert abs(r["fp32_equivalent"]["frac"] - 100.0 / bench.FP32_MFMA_PEAK_TFLOPS) < 1e-12
+    b = bench.dense_roofline("hsg_gemm_*", 19200, 900.0, 5.9e9, 0.0066, "bf16")
+    assert b["achieved"] == 900.0 and "fp32_equivalent" not in b
