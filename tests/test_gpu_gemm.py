@@ -165,7 +165,7 @@ PSW_SHAPES = [(1, 1, 4), (33, 17, 20), (130, 300, 300), (777, 512, 300), (1000, 
               (19200, 512, 300)]
 
 
-@pytest.mark.parametrize("plan", ["1", "2", "3", "4", "5", "6"])
+@pytest.mark.parametrize("plan", ["1", "2", "3", "4", "5", "6", "7", "27", "30"])
 @pytest.mark.parametrize("M,N,K", PSW_SHAPES)
 @pytest.mark.parametrize("trans", [False, True])
 def test_psw_layouts(M, N, K, trans, plan, monkeypatch):
@@ -181,6 +181,27 @@ def test_psw_layouts(M, N, K, trans, plan, monkeypatch):
     R = A.double() @ (W.double() if trans else W.double().t())
     err = (C.double() - R).abs().max().item()
     assert err <= 1e-5 * max(1.0, K ** 0.5) * 4, err
+
+
+@pytest.mark.parametrize("M,N,K", [(19200, 512, 300), (19200, 300, 512), (1600, 300, 512), (777, 512, 300)])
+@pytest.mark.parametrize("plan", ["7", "27"])
+def test_psw_split_is_fp32_class(M, N, K, plan, monkeypatch):
+    """The pre-split-weight GEMM (in-kernel split of the fp32 activation operand) is
+    fp32-class: per element |C - C_fp64| / sum_k |a_k b_k| within 1.5x of the exact-f32
+    instruction's and below 2e-6, on operands spread over many binades."""
+    from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights
+    monkeypatch.setenv("HSG_GEMM5", plan)
+    torch.manual_seed(K + 1)
+    A = mk(M, K) * torch.exp(2 * torch.randn(1, device="cuda"))
+    A = A * torch.exp(torch.randn_like(A))
+    W = mk(N, K) * torch.exp(torch.randn(N, K, device="cuda"))
+    (S,) = split_weights((W, False))
+    ref = A.double() @ W.double().t()
+    unit = A.double().abs() @ W.double().abs().t()
+    e_psw = ((gemm_psw(A, S).double() - ref).abs() / unit).max().item()
+    e_f32 = ((gemm(A, W, b_t=True, dtype="f32mfma").double() - ref).abs() / unit).max().item()
+    print(f"{M}x{N}x{K} plan {plan}: psw {e_psw:.2e}, f32 mfma {e_f32:.2e}")
+    assert e_psw <= 1.5 * e_f32 + 1e-8 and e_psw < 2e-6
 
 
 def test_psw_epilogues_and_colsums():
