@@ -80,21 +80,28 @@ def test_gat_vs_reference_golden(name, seed, dense):
     assert max_err(r["o1"], z["out64_w2s"]) <= 1e-5
     assert max_err(r["o2"].detach().cpu()[rows], z["out64_s2w"]) <= 1e-5
     bad = 2 if name == "gat_cfg1" else 0
-    assert_grad_close(r["Xs"].grad, z["grad_Xs"], max_bad_rows=bad)
-    assert_grad_close(r["T"].grad, z["grad_T"], rtol=1e-3, max_bad_rows=bad)
+    # cfg1 holds an fp32 ReLU-gate tie in the S2W FFN: word 479, hidden unit 189 has the
+    # fp64 pre-activation 1.05e-7 against |x|.|w1| = 9.27 (1.1e-8 relative, below fp32
+    # resolution), so either gate is a correct fp32 result; when it closes, sentence
+    # row 48 of grad_Xs moves by 0.30 = 1.07 % of max|ref| (tools/flip_diag.py).  The
+    # flipped rows' bound is 2 % there; an indexing bug moves a row by O(max|ref|).
+    worst = 2e-2 if bad else 1e-2
+    assert_grad_close(r["Xs"].grad, z["grad_Xs"], max_bad_rows=bad, worst=worst)
+    assert_grad_close(r["T"].grad, z["grad_T"], rtol=1e-3, max_bad_rows=bad, worst=worst)
     if "grad_Xw" in z:
-        assert_grad_close(r["Xw"].grad, z["grad_Xw"], max_bad_rows=bad)
+        assert_grad_close(r["Xw"].grad, z["grad_Xw"], max_bad_rows=bad, worst=worst)
     else:
-        assert_grad_close(r["Xw"].grad.cpu()[rows], z["grad_Xw_rows"], max_bad_rows=bad)
+        assert_grad_close(r["Xw"].grad.cpu()[rows], z["grad_Xw_rows"], max_bad_rows=bad, worst=worst)
     from hetersumgraph_amd.module.GATStackLayer import reference_named_grads
     for tag, mod in (("w2s", r["w2s"]), ("s2w", r["s2w"])):
         for k, grad in reference_named_grads(mod):
             key = f"grad.{tag}.{k}"
             # a ReLU-gate flip in one input row (cfg1: word 479) perturbs every row of
             # a weight gradient, so there the bound is relative to the largest entry
+            # (and db1[189] itself moves by 1.2 % of max|ref| when the tied gate closes)
             prtol = 5e-3 if bad else 1e-3
             if key in z:
-                assert_grad_close(grad, z[key], rtol=prtol, max_bad_rows=bad)
+                assert_grad_close(grad, z[key], rtol=prtol, max_bad_rows=bad, worst=worst)
             elif "proj." + key in z:
                 got = projections(grad, seed, key)
                 ref = z["proj." + key]
