@@ -616,8 +616,10 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 // (G_v.Z_u) over the typed edges (h_v = sum_e alpha_e Z_u; phantoms carry no message)
 // is summed in a first pass over the edges whose dots are staged in LDS (the first
 // kCh edges; later ones are recomputed in the second pass).
+// GIN (with NOH): the G rows are given (hsg_gemm_f32_psw_elug produced them in the
+// FFN backward's epilogue): read instead of dOut / x / origin, and not written.
 constexpr int kCh = 16;
-template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false>
+template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false, bool GIN = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
                                                     const float *__restrict__ Z,
@@ -669,17 +671,20 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
             const int f = lane + 64 * i;
             if (f < HD) {
                 const size_t o = (size_t)v * HD + f;
-                const float dv = dout[o];
                 float gv;
-                if constexpr (NOH) {
+                if constexpr (GIN) {
+                    gv = G[o];
+                } else if constexpr (NOH) {
+                    const float dv = dout[o];
                     const float e = xo[o] - org[o];
                     gv = e > 0.f ? dv : dv * (e + 1.f);
                 } else {
+                    const float dv = dout[o];
                     const float hv = hsv[o];
                     gv = origin_mode ? (hv > 0.f ? dv : dv * __expf(hv)) : dv;
                     sgh[f] = gv * hv;
                 }
-                G[o] = gv;
+                if constexpr (!GIN) G[o] = gv;
                 sg[f] = gv;
             }
         }
@@ -1156,15 +1161,15 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
     return launch_status();
 }
 
-template <int TAU, int OCC = 1, bool NOH = false>
+template <int TAU, int OCC = 1, bool NOH = false, bool GIN = false>
 int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, int om,
                      float slope, const float *Z, const float *sg, const float *tau, const float *h,
                      const float *m, const float *l, const float *dout, float *G, float *dpre,
                      float *dtp, const float *x = nullptr, const float *org = nullptr) {
 #define HSG_BD(NE_)                                                                                        \
     case NE_:                                                                                              \
-        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH>), grid, dim3(256), st, R, H, D, lph, om, \
-                    slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp, x, org);                               \
+        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH, GIN>), grid, dim3(256), st, R, H, D, lph, \
+                    om, slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp, x, org);                           \
         break;
     if constexpr (NOH) {                 // the shapes the fused stack's S2W pass uses
         switch (ne) {
@@ -1343,6 +1348,29 @@ int hsg_gat_bwd_dst_noh(const hsg_rel *rel, int H, int D, int tau_mode, float sl
                                                         nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
     return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
                                                        nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
+}
+
+int hsg_gat_bwd_dst_g(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                      const float *sigma, const float *tau, const float *m, const float *l, const float *G,
+                      float *dpre, float *dtau_part, void *stream) {
+    if (!hsg_gat_bwd_dst_noh_supported(rel, H, D) || !G) return HSG_EINVAL;
+    if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
+    const int lph = lanes_per_head(H);
+    const RelPtrs R = rel_ptrs(rel);
+    const dim3 grid(hsg_gat_bwd_blocks(rel));
+    hipStream_t st = (hipStream_t)stream;
+    if (rel->n_dst == 0) {
+        if (tau_mode == HSG_TAU_TABLE && dtau_part)
+            return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
+        return 0;
+    }
+    const int ne = ne_bucket((D + lph - 1) / lph);
+    float *Gw = const_cast<float *>(G);                 // read only (GIN)
+    if (tau_mode == HSG_TAU_TABLE)
+        return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
+                                                              nullptr, m, l, nullptr, Gw, dpre, dtau_part);
+    return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
+                                                             nullptr, m, l, nullptr, Gw, dpre, dtau_part);
 }
 
 int hsg_gat_bwd_src_blocks(const hsg_rel *rel) {

@@ -72,6 +72,10 @@ struct GemmArgs {
     float *colpart;       // optional: per-block-row column sums of C, [ceil(M/BM)][N]
     int splits;           // K slices (tile ids run over splits x tiles_m x tiles_n)
     int xcd;              // 1: XCD-aware tile order (see xcd_tile)
+    // HSG_EPI_ADD_ELUG only (epi_rows): C2 = C * elu'(h) with e = aux2 - aux3 (ld: ldaux)
+    const float *aux2 = nullptr;
+    const float *aux3 = nullptr;
+    float *C2 = nullptr;
 };
 
 // Workgroup b is dispatched to XCD b % 8, and so is tile t (the persistent grid is a
@@ -951,45 +955,80 @@ __device__ __forceinline__ void epi_store(const f32x16 (&acc)[TN], int row0, int
 // rows per step; lanes past RPS * QPR idle.  Each lane keeps one quad, so its column
 // sums are per-lane partials over its rows.
 template <int BN>
-__device__ __forceinline__ void epi_rows(const float *wl, int row0, int col0, int lane, const GemmArgs &p,
-                                         f32x4 &csum) {
-    constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
-    constexpr int STEPS = (32 + RPS - 1) / RPS;
-    __builtin_amdgcn_s_waitcnt(0xc07f);                     // lgkmcnt(0): the wave's own LDS writes
-    __builtin_amdgcn_wave_barrier();
-    const int q = lane % QPR, rs = lane / QPR;
-    const int n = col0 + 4 * q;
-    const bool qok = rs < RPS && n < p.N;                  // N % 4 == 0 (host-checked): whole quads
-    f32x4 bn = {0.f, 0.f, 0.f, 0.f};
-    if (p.bias && qok) bn = *reinterpret_cast<const f32x4 *>(p.bias + n);
-    f32x4 aux[STEPS];
-    if (p.epi != HSG_EPI_STORE) {
+struct EpiRows {
+    static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
+    static constexpr int STEPS = (32 + RPS - 1) / RPS;
+    f32x4 bn, aux[STEPS], ex[STEPS];
+
+    // the epilogue's global operands (bias, aux, and for HSG_EPI_ADD_ELUG x - origin),
+    // requested together; k_gemm7 issues this before its last K tile's MFMAs so the
+    // round trip overlaps them
+    __device__ __forceinline__ void load(const GemmArgs &p, int row0, int col0, int lane) {
+        const int q = lane % QPR, rs = lane / QPR;
+        const int n = col0 + 4 * q;
+        const int nc = min(n, p.N - 4);                    // N % 4 == 0 (host-checked): whole quads
+        bn = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (p.bias) bn = *reinterpret_cast<const f32x4 *>(p.bias + nc);
+        if (p.epi != HSG_EPI_STORE) {
 #pragma unroll
-        for (int t = 0; t < STEPS; ++t) {
-            const int m = min(row0 + min(t * RPS + rs, 31), p.M - 1);
-            aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + min(n, p.N - 4));
-        }
-    }
-    csum = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < STEPS; ++t) {
-        const int r = t * RPS + rs, m = row0 + r;
-        if (!qok || r >= 32 || m >= p.M) continue;
-        f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
-        if (p.epi == HSG_EPI_RELU_BWD) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
-        } else {
-            v += bn;
-            if (p.epi == HSG_EPI_ADD) v += aux[t];
-            if (p.relu) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+            for (int t = 0; t < STEPS; ++t) {
+                const int m = min(row0 + min(t * RPS + rs, 31), p.M - 1);
+                aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + nc);
             }
         }
-        *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
-        csum += v;
+        if (p.epi == HSG_EPI_ADD_ELUG) {                   // e = x - origin = elu(h)
+#pragma unroll
+            for (int t = 0; t < STEPS; ++t) {
+                const int m = min(row0 + min(t * RPS + rs, 31), p.M - 1);
+                const size_t o = (size_t)m * p.ldaux + nc;
+                ex[t] = *reinterpret_cast<const f32x4 *>(p.aux2 + o) - *reinterpret_cast<const f32x4 *>(p.aux3 + o);
+            }
+        }
     }
+
+    __device__ __forceinline__ void finish(const float *wl, int row0, int col0, int lane, const GemmArgs &p,
+                                           f32x4 &csum) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS writes
+        __builtin_amdgcn_wave_barrier();
+        const int q = lane % QPR, rs = lane / QPR;
+        const int n = col0 + 4 * q;
+        const bool qok = rs < RPS && n < p.N;
+        csum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < STEPS; ++t) {
+            const int r = t * RPS + rs, m = row0 + r;
+            if (!qok || r >= 32 || m >= p.M) continue;
+            f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
+            if (p.epi == HSG_EPI_RELU_BWD) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
+            } else {
+                v += bn;
+                if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
+                if (p.relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+            }
+            *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+            if (p.epi == HSG_EPI_ADD_ELUG) {
+                // G = dOut * elu'(h): 1 for e = elu(h) > 0, else e + 1 = exp(h) (continuous at 0)
+                f32x4 g;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
+                *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
+            }
+            csum += v;
+        }
+    }
+};
+
+template <int BN>
+__device__ __forceinline__ void epi_rows(const float *wl, int row0, int col0, int lane, const GemmArgs &p,
+                                         f32x4 &csum) {
+    EpiRows<BN> e;
+    e.load(p, row0, col0, lane);
+    e.finish(wl, row0, col0, lane, p, csum);
 }
 
 // 64-row column partials (hsg_gemm_row_tiles) from epi_rows' per-lane sums: waves
@@ -1013,8 +1052,11 @@ __device__ __forceinline__ void epi_rows_colpart(float *red, const f32x4 &cs, in
 }
 
 bool epi_rows_ok(const GemmArgs &p) {
-    return !((p.N & 3) || (p.ldc & 3) || (((uintptr_t)p.C) & 15) || (p.bias && (((uintptr_t)p.bias) & 15)) ||
-             (p.aux && ((p.ldaux & 3) || (((uintptr_t)p.aux) & 15))));
+    const auto al = [](const void *q) { return (((uintptr_t)q) & 15) == 0; };
+    if ((p.N & 3) || (p.ldc & 3) || !al(p.C) || (p.bias && !al(p.bias)) ||
+        (p.aux && ((p.ldaux & 3) || !al(p.aux))))
+        return false;
+    return p.epi != HSG_EPI_ADD_ELUG || (al(p.aux2) && al(p.aux3) && al(p.C2));
 }
 
 template <int BN, int S, int IGLP = -1, bool ELDS = false, bool HOIST = false>
@@ -1216,6 +1258,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
+    EpiRows<BN> ep;
 
     auto issue = [&](int it) {
         float *st = lds + (it % S) * STAGE_FL;
@@ -1250,6 +1293,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (it + S - 1 < nt) issue(it + S - 1);
+        if (it == nt - 1) ep.load(p, m0 + wid * 32, n0, lane);   // overlaps the last tile's MFMAs
         const float *sa = lds + (it % S) * STAGE_FL;
         const __bf16 *sb = reinterpret_cast<const __bf16 *>(sa + A_FL);
         bf16x8 a[2][3];
@@ -1292,7 +1336,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
 #pragma unroll
             for (int e = 0; e < 4; ++e) wl[(16 * i + rq + e) * (BN + 4) + 16 * j + c] = acc[i][j][e];
     f32x4 cs;
-    epi_rows<BN>(wl, m0 + wid * 32, n0, lane, p, cs);
+    if (nt == 0) ep.load(p, m0 + wid * 32, n0, lane);
+    ep.finish(wl, m0 + wid * 32, n0, lane, p, cs);
     if (p.colpart) epi_rows_colpart<BN>(lds, cs, wid, lane, ty, n0, p);
 }
 
@@ -1933,6 +1978,20 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 28 && epi_rows_ok(p)) return launch7<64, 2, false>(p, pl, Np, Kp, st);   // truncation split
     if (plan == 30 && epi_rows_ok(p)) return N <= 320 ? launch7<80, 2>(p, pl, Np, Kp, st) : launch7<128, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2>(p, pl, Np, Kp, st);
+}
+
+int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                          const float *aux, const float *x, const float *origin, float *G, int ld, void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G) return HSG_EINVAL;
+    if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N)
+        return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, nullptr, aux, ld, HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr,
+               1, 1, x, origin, G};
+    if (!epi_rows_ok(p)) return HSG_EINVAL;
+    return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
 }
 
 #ifdef HSG_GEMM_CENSUS

@@ -24,7 +24,7 @@ import os
 import torch
 
 from . import _lib
-from ._lib import HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr, stream_of
+from ._lib import HSG_EINVAL, HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr, stream_of
 
 
 _GEMM_DTYPE = os.environ.get("HSG_GEMM_DTYPE", "f32")
@@ -160,6 +160,25 @@ def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, c
                                _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part),
                                stream_of(A)), "hsg_gemm_f32_psw")
     return out
+
+
+def gemm_psw_elug(A, Bs, out, x, origin, G):
+    """out = out + A @ B^T (the FFN backward's dx += dH W1) and, in the same epilogue,
+    G = out * elu'(h) with elu(h) = x - origin (hsg_gemm_f32_psw_elug: the edge
+    layer's ELU gate, GAT.py:56-57, moved out of its dst pass).  Returns False (nothing
+    launched) when the shape / alignment does not allow the fused epilogue."""
+    lib = load()
+    M, K = A.shape
+    N = Bs.N
+    ts = (out, x, origin, G)
+    if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in ts):
+        return False
+    rc = lib.hsg_gemm_f32_psw_elug(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
+                                   ptr(origin), ptr(G), N, stream_of(A))
+    if rc == HSG_EINVAL:
+        return False
+    check(rc, "hsg_gemm_f32_psw_elug")
+    return True
 
 
 def gemm_slabs(A, B, a_t=False, b_t=False):

@@ -26,7 +26,7 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, gemm_psw, get_gemm_dtype, row_tiles, split_weights
+from .dense import gemm, gemm_psw, gemm_psw_elug, get_gemm_dtype, row_tiles, split_weights
 
 LN_EPS = 1e-5
 
@@ -99,7 +99,7 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
 
 
-def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
+def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
     """Backward of :func:`ffn_fwd`.  ``dst`` = (dw1, acc_w1, dw2, acc_w2, db1, db2,
     dgamma, dbeta, acc_b): gradient buffers shaped [d_hid, d], [d, d_hid], [d_hid],
     [d], [d], [d] (None when not needed), each written or -- with its accumulate
@@ -109,7 +109,10 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
     applications of a layer (pass dw1 = dw2 = None).  ``batch`` (a
     reduce.SlabBatch) with ``key``: the bias / LayerNorm column sums are recorded
     there (one job per output across every call with the same key) instead of run
-    here.  Returns dx (a fresh tensor)."""
+    here.  ``elug`` = (origin, G): the FFN input x is the edge layer's elu(h) + origin,
+    and its ELU gate G = dx * elu'(h) goes into G from the last GEMM's epilogue
+    (hsg_gemm_f32_psw_elug) -- only on the pre-split-weight path.  Returns dx (a fresh
+    tensor), or (dx, G produced?) with ``elug``."""
     lib = load()
     x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off, wsplit = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
@@ -119,6 +122,7 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
     d_hid = H.shape[1]
     dy = act_grads[0] if act_grads is not None else torch.empty_like(x)
     dx = torch.empty_like(x)
+    g_done = False
     if _fused_ok(lib, x, w1, w2) and H.is_contiguous() and y.is_contiguous():
         # one launch: LN/dropout backward, dH = (dy W2) * relu'(H), dx = ds + dH W1
         nb = rt = lib.hsg_ffn_small_bwd_blocks(n)
@@ -138,7 +142,10 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
         dH_out = act_grads[1] if act_grads is not None else None
         if wsplit is not None:
             dH = gemm_psw(dy, wsplit[2], relu_mask=H, colsum_part=hpart, out=dH_out)
-            gemm_psw(dH, wsplit[3], out=dx, add=dx)
+            if elug is not None and gemm_psw_elug(dH, wsplit[3], dx, x, elug[0], elug[1]):
+                g_done = True
+            else:
+                gemm_psw(dH, wsplit[3], out=dx, add=dx)
         else:
             dH = gemm(dy, w2, relu_mask=H, splits=1, colsum_part=hpart,   # [n, d_hid] + db1 partials
                       out=dH_out)
@@ -154,13 +161,13 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None):
         for o, name, off in ((dg, "g", 0), (dbt, "bt", d), (db2, "b2", 2 * d)):
             if o is not None:
                 batch.add((key, name), o, d, 3 * d, off, 1.0, acc, part, nb)
-        return dx
+        return (dx, g_done) if elug is not None else dx
     if any(o is not None for o in outs):
         db1, dg, dbt, db2 = [o if o is not None else x.new_empty(n_)
                              for o, n_ in zip(outs, (d_hid, d, d, d))]   # scratch for unneeded ones
         check(lib.hsg_ffn_colsums(rt, d_hid, ptr(hpart), ptr(db1), nb, d, ptr(part), ptr(dg), ptr(dbt), ptr(db2),
                                   int(bool(acc)), st), "hsg_ffn_colsums")
-    return dx
+    return (dx, g_done) if elug is not None else dx
 
 
 class _FFN(torch.autograd.Function):

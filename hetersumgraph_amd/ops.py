@@ -124,7 +124,8 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
-def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None, keep_h=True):
+def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None, keep_h=True,
+                  no_h=False):
     """Forward of one multi-head application with the TF-IDF-table edge term:
     3 launches (attention parameters -> tau table, sigma, edge pass; 2 when
     ``tables`` = :func:`attn_tables` of this layer is passed in).  ``out``: a contiguous
@@ -133,7 +134,10 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     where hsg_gat_bwd_dst_noh covers the shape, and HSG_GAT_NOH=1): h is not stored; the
     backward takes elu'(h) from out - origin and G.h from the edge dots.  Opt-in: at
     cfg2 the S2W forward drops 22.6 -> 18.3 us but the dst pass, which then reads out
-    and origin instead of h, rises 33 -> 39.6 us (step +8 us).  Returns
+    and origin instead of h, rises 33 -> 39.6 us (step +8 us).  ``no_h``:
+    the same without the switch -- for a caller whose backward hands
+    :func:`gat_table_bwd` the G rows from the FFN's last GEMM epilogue
+    (hsg_gemm_f32_psw_elug), so the dst pass reads neither h nor x / origin.  Returns
     (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
@@ -147,7 +151,7 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         sigma = Z.new_empty(n_src, H)
         check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
-    no_h = (not keep_h and origin is not None and os.environ.get("HSG_GAT_NOH", "0") == "1"
+    no_h = ((no_h or (not keep_h and os.environ.get("HSG_GAT_NOH", "0") == "1")) and origin is not None
             and bool(lib.hsg_gat_bwd_dst_noh_supported(relp, H, D)))
     h = None if no_h else Z.new_empty(n_dst, HD)
     if origin is None:
@@ -169,20 +173,24 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     return (out if origin is not None else h), saved
 
 
-def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
+def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None):
     """Backward of :func:`gat_table_fwd`: 3 launches (dst pass, src pass with the
     d a1 partials, parameter backward).  Returns dZ (None with dZ=False).  ``dst`` =
     (dattn, dwf, dbf, dT, acc_head, acc_T): gradient buffers written or added into
     (dbf None on W2S).  ``stage`` = (workspace, accumulate) instead: only reduce this
     application's partials into a per-layer workspace (hsg_attn_params_stage); the
     caller runs :func:`attn_params_finish` once for all applications of the layer.
-    The origin gradient is ``dout`` itself."""
+    The origin gradient is ``dout`` itself.  ``G``: the rows dOut * elu'(h), already
+    made by the FFN's last GEMM (a forward without h): the dst pass reads them
+    (hsg_gat_bwd_dst_g)."""
     lib = load()
     Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin, xo = saved
     dout = dout.contiguous()
     st = stream_of(Z)
     relp = ctypes.byref(rel.cstruct())
-    G = torch.empty_like(dout)
+    g_given = G is not None
+    if not g_given:
+        G = torch.empty_like(dout)
     dpre = Z.new_empty(rel.n_typed, H)
     nbd = lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
@@ -191,7 +199,12 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None):
     da1p = Z.new_empty(nbs, H * D)
     tok = _clock_start(("gat_bwd", rel.kind), Z)
     try:
-        if xo is not None:                  # forward without h (keep_h=False)
+        if g_given:                         # G from the FFN epilogue (forward without h)
+            if xo is None:
+                raise ValueError("gat_table_bwd: G rows given for a forward that stored h")
+            check(lib.hsg_gat_bwd_dst_g(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau), ptr(m),
+                                        ptr(l), ptr(G), ptr(dpre), ptr(dtp), st), "hsg_gat_bwd_dst_g")
+        elif xo is not None:                # forward without h (keep_h=False)
             check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
                                           ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
                                           ptr(dtp), st), "hsg_gat_bwd_dst_noh")

@@ -119,8 +119,12 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
         Z, hsaved = hproj_fwd(neighbor, lay.W, H, D, lay.p_attn, bits=draws[0], wt=wt)
     else:
         Z, hsaved = gemm(neighbor, lay.W, b_t=True, dtype="f32"), None      # fp32 in every GEMM mode, as hproj
+    # with the FFN on the pre-split-weight GEMMs, its backward's last GEMM also makes the
+    # edge layer's G rows (hsg_gemm_f32_psw_elug), so the forward need not store h
+    # (HSG_GAT_GEPI=0: h stored and G made in the dst pass, for A/B tests)
+    g_epi = wsplit is not None and not isinstance(wsplit, str) and os.environ.get("HSG_GAT_GEPI", "1") != "0"
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
-                              out=x_out, sigma=sigma, keep_h=False)
+                              out=x_out, sigma=sigma, keep_h=False, no_h=g_epi)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     out, fsaved = ffn_fwd(x, lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2, lay.gamma, lay.beta,
                           lay.p_ffn, lay.eps, H_out=H_out, wsplit=wsplit, rng=draws[1])
@@ -154,6 +158,11 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     Returns the origin's gradient (the FFN's residual-branch dx)."""
     hsaved, neighbor, gsaved, fsaved = saved
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+    # forward without h and the FFN on the pre-split path: the G rows of the edge
+    # backward come out of the FFN's last GEMM (dx epilogue)
+    G = None
+    elug = (gsaved[16][1], torch.empty_like(fsaved[0])) if gsaved[16] is not None and fsaved[11] is not None \
+        else None
     if act_grads is None:
         dw1, a_w1 = grads.dst(lay.w1)
         dw2, a_w2 = grads.dst(lay.w2)
@@ -162,12 +171,15 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     (db1, db2, dg, dbt), a_b = grads.group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
                                 dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b),
-                 act_grads=act_grads, batch=batch, key=id(lay))
+                 act_grads=act_grads, batch=batch, key=id(lay), elug=elug)
+    if elug is not None:
+        dx, g_done = dx
+        G = elug[1] if g_done else None
     need_dz = nb_grad is not None or lay.W.requires_grad
     if stage is not None:
-        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage)
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage, G=G)
     else:
-        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(grads, lay, T))
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(grads, lay, T), G=G)
     if need_dz:
         dW, a_W = grads.dst(lay.W)
         if hsaved is not None:

@@ -91,6 +91,13 @@ int hsg_gat_bwd_dst_noh(const hsg_rel *rel, int H, int D, int tau_mode, float sl
                         const float *x, const float *origin, const float *m, const float *l,
                         const float *dout, float *G, float *dpre, float *dtau_part, void *stream);
 
+/* hsg_gat_bwd_dst_noh with the G rows given (origin_mode 1, e.g. from
+ * hsg_gemm_f32_psw_elug): G is read, not written; dpre and dtau_part as
+ * hsg_gat_bwd_dst.  Supported where hsg_gat_bwd_dst_noh_supported. */
+int hsg_gat_bwd_dst_g(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
+                      const float *Z, const float *sigma, const float *tau, const float *m, const float *l,
+                      const float *G, float *dpre, float *dtau_part, void *stream);
+
 /* Backward, source-centric half (CSC): for every source u
  *   dZ[u, k, :]  = sum_{e: src_e = u} alpha_ek * G[dst_e, k, :]  (+ dsigma[u,k]*a1[k,:] if a1)
  *   dsigma[u, k] = sum_{e: src_e = u} dpre[e, k]                 (written if dsigma != NULL)
@@ -178,6 +185,7 @@ size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 #define HSG_EPI_STORE 0
 #define HSG_EPI_RELU_BWD 1
 #define HSG_EPI_ADD 2
+#define HSG_EPI_ADD_ELUG 3   /* hsg_gemm_f32_psw_elug only */
 size_t hsg_gemm_workspace_floats(int M, int N, int K, int splits);   /* splits 0: the automatic plan */
 int hsg_gemm_auto_splits(int M, int N, int K);
 int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig,
@@ -207,6 +215,16 @@ int hsg_wsplit(int njobs, const float *const *W, const int *N, const int *K, con
 int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *planes,
                      float *C, int ldc, const float *bias, const float *aux, int ldaux,
                      int epi, int relu, float *colsum_part, void *stream);
+/* The FFN backward's last GEMM with the edge layer's ELU gate fused into its epilogue
+ * (GAT.py:56-57 backward; replaces the dOut -> G step of hsg_gat_bwd_dst):
+ *   C = aux + A B^T          (dx = ds + dH W1: the FFN input's gradient, = the origin's)
+ *   G = C * elu'(h),  elu'(h) = 1 if e > 0 else e + 1,  e = x - origin = elu(h)
+ * x: the edge layer's output (the FFN input), origin: its residual input; aux, x,
+ * origin and G share the row pitch `ld`.  N % 4 == 0 and 16-byte aligned rows
+ * (HSG_EINVAL otherwise: the caller keeps the split path).  The G rows feed
+ * hsg_gat_bwd_dst_g. */
+int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                          const float *aux, const float *x, const float *origin, float *G, int ld, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,

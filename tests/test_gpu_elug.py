@@ -1,0 +1,86 @@
+"""The edge layer's ELU gate fused into the FFN backward's last GEMM
+(hsg_gemm_f32_psw_elug) and the dst pass that reads the resulting G rows
+(hsg_gat_bwd_dst_g) -- GAT.py:56-57 backward (G = dOut * elu'(h)), GATLayer.py:95-102
+backward -- against fp64 torch and against the dst pass that makes G itself."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("M,N,K", [(19200, 300, 512), (777, 300, 512), (130, 64, 96)])
+def test_psw_elug_matches_fp64(M, N, K):
+    from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
+    torch.manual_seed(M)
+    dH = torch.randn(M, K, device="cuda")
+    W1 = torch.randn(K, N, device="cuda") / K ** 0.5          # dx += dH W1: B = W1^T planes
+    (S,) = split_weights((W1, True))
+    ds = torch.randn(M, N, device="cuda")
+    origin = torch.randn(M, N, device="cuda")
+    h = 2 * torch.randn(M, N, device="cuda")
+    h[::7] = 0.0                                               # elu' at the kink
+    x = torch.nn.functional.elu(h) + origin
+    out = ds.clone()
+    G = torch.empty_like(ds)
+    assert gemm_psw_elug(dH, S, out, x, origin, G)
+    ref = ds.double() + dH.double() @ W1.double()
+    e = (x.double() - origin.double())
+    gref = torch.where(e > 0, ref, ref * (e + 1))
+    assert (out.double() - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    # G against the exact gate exp(h): the rounding of x - origin moves it by ~ulp(x)
+    gexact = torch.where(h.double() > 0, ref, ref * torch.exp(h.double()))
+    assert (G.double() - gref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    assert (G.double() - gexact).abs().max().item() <= 2e-4 * max(1.0, ref.abs().max().item())
+
+
+def test_psw_elug_declines_unaligned():
+    from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
+    W1 = torch.randn(64, 30, device="cuda")
+    (S,) = split_weights((W1, True))                           # N = 30: not whole quads
+    t = torch.randn(50, 30, device="cuda")
+    assert not gemm_psw_elug(torch.randn(50, 64, device="cuda"), S, t.clone(), t, t, torch.empty_like(t))
+
+
+def test_dst_pass_with_given_G_equals_noh_pass():
+    """hsg_gat_bwd_dst_g with the G rows hsg_gat_bwd_dst_noh wrote: bitwise the same
+    dpre and d tau partials (the same kernel body, G read instead of made)."""
+    import ctypes
+    from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd._lib import HSG_TAU_TABLE, load, ptr
+    from hetersumgraph_amd.relation import N_BOX
+    lib = load()
+    rng = np.random.default_rng(3)
+    docs = [synth.make_hsg_doc(rng, N=35, W=600, k=36) for _ in range(4)]
+    G_ = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
+    G_.to(torch.device("cuda"))
+    rel = G_.relation("S2W")
+    relp = ctypes.byref(rel.cstruct())
+    H, D = 6, 50
+    assert lib.hsg_gat_bwd_dst_noh_supported(relp, H, D)
+    torch.manual_seed(0)
+    Z = torch.randn(rel.n_src, H * D, device="cuda")
+    sigma = torch.randn(rel.n_src, H, device="cuda")
+    tau = torch.randn(N_BOX + 1, H, device="cuda")
+    m = torch.randn(rel.n_dst, H, device="cuda").abs()
+    l = torch.rand(rel.n_dst, H, device="cuda") + 1
+    x = torch.randn(rel.n_dst, H * D, device="cuda")
+    org = torch.randn(rel.n_dst, H * D, device="cuda")
+    dout = torch.randn(rel.n_dst, H * D, device="cuda")
+    nb = lib.hsg_gat_bwd_blocks(relp)
+    outs = []
+    Gn = torch.empty_like(dout)
+    for given in (False, True):
+        dpre = torch.empty(rel.n_typed, H, device="cuda")
+        dtp = torch.empty(nb, N_BOX + 1, H, device="cuda")
+        if given:
+            rc = lib.hsg_gat_bwd_dst_g(relp, H, D, HSG_TAU_TABLE, 0.01, ptr(Z), ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                                       ptr(Gn), ptr(dpre), ptr(dtp), None)
+        else:
+            rc = lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, 0.01, ptr(Z), ptr(sigma), ptr(tau), ptr(x),
+                                         ptr(org), ptr(m), ptr(l), ptr(dout), ptr(Gn), ptr(dpre), ptr(dtp), None)
+        assert rc == 0
+        torch.cuda.synchronize()
+        outs.append((dpre, dtp))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -71,13 +71,18 @@ def _zero(mods, T, Xw, Xs):
 
 
 @pytest.mark.parametrize("kind,train,word_grad,reps,n_iter,noh", [
-    ("hsg", True, False, 1, 2, 0), ("hsg", True, True, 2, 2, 0), ("hsg", False, True, 1, 1, 0),
-    ("hdsg", True, True, 1, 2, 0), ("hsg", True, False, 1, 3, 0),
-    # the fused stack's S2W edge pass without a stored h (hsg_gat_bwd_dst_noh) against
-    # the layer-wise path, which keeps h
+    ("hsg", True, False, 1, 2, 2), ("hsg", True, True, 2, 2, 2), ("hsg", False, True, 1, 1, 2),
+    ("hdsg", True, True, 1, 2, 2), ("hsg", True, False, 1, 3, 2),
+    # the fused stack's S2W edge pass with a stored h and G made in the dst pass
+    # (HSG_GAT_GEPI=0), and without h with G from x - origin in the dst pass
+    # (hsg_gat_bwd_dst_noh), against the layer-wise path, which keeps h; noh = 2 is the
+    # default: no h, G from the FFN's last GEMM epilogue (hsg_gemm_f32_psw_elug +
+    # hsg_gat_bwd_dst_g)
+    ("hsg", True, True, 2, 2, 0), ("hsg", True, False, 1, 2, 0),
     ("hsg", True, True, 2, 2, 1), ("hdsg", True, True, 1, 2, 1), ("hsg", False, True, 1, 1, 1)])
 def test_fused_stack_matches_layerwise(monkeypatch, kind, train, word_grad, reps, n_iter, noh):
-    monkeypatch.setenv("HSG_GAT_NOH", str(noh))
+    monkeypatch.setenv("HSG_GAT_NOH", str(int(noh == 1)))
+    monkeypatch.setenv("HSG_GAT_GEPI", str(int(noh == 2)))
     G = _graph(kind, 3)
     w2s, s2w, T = _modules(7, 0.1)
     for m in (w2s, s2w):

@@ -10,7 +10,7 @@ import torch  # noqa: E402
 
 from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights  # noqa: E402
 
-PLANS = {"7": "g5 BN64 iglp0 (r2)", "27": "g7 64 lds RNE", "28": "g7 64 lds trunc"}
+PLANS = {"7": "g5 BN64 iglp0 (r2)", "27": "g7 64 lds RNE prefetch"}
 
 
 def timed(f, reps=20):
