@@ -444,7 +444,9 @@ def main():
         # After a graph replay every gradient is final at once, so there is nothing to
         # overlap with: ONE flat bucket (7 MB at cfg2) pays one collective latency
         # instead of one per 2 MiB bucket (the eager train step overlaps its buckets
-        # with the backward instead: parallel.GradientReducer)
+        # with the backward instead: parallel.GradientReducer).  The fused stack writes
+        # every gradient into one flat buffer (stack._Grads), which is reduced in place:
+        # one scale pass + one all-reduce, no concatenation or copy-back
         from hetersumgraph_amd.parallel import allreduce_gradients
         allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
 
@@ -513,6 +515,10 @@ def main():
         dt = float(t.item())
     ms_per_step = dt / args.steps * 1e3
     value = E_global / (dt / args.steps)
+    from hetersumgraph_amd.parallel import flat_gradients
+    dp_exchange = ("none (one rank)" if world == 1 else
+                   "one in-place all-reduce of the flat gradient buffer" if flat_gradients(params) is not None
+                   else "bucketed all-reduce (concatenated copies)")
 
     # edge kernels timed inside eager steps (HIP events of their dispatches), after the
     # timed region so they cannot perturb it
@@ -557,7 +563,7 @@ def main():
                    "edge_kernels_ln_head_projection": "f32",
                    "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
                    "typed_edges_per_direction": rel_w.n_typed,
-                   "dropout": args.dropout, "parallelism": f"dp{world}",
+                   "dropout": args.dropout, "parallelism": f"dp{world}", "dp_exchange": dp_exchange,
                    "hip_graph": bool(use_graph)},
         "roofline": {"kernel": "hsg_gat_fwd (S2W: sentence->word, H=6 x D=50)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -96,6 +96,30 @@ def _finish(pending, world):
                                       zip(torch.split(flat, [g.numel() for g in bucket]), bucket)])
 
 
+def flat_gradients(params):
+    """A 1-D tensor over the one buffer behind every ``p.grad`` of ``params`` when the
+    gradients tile that buffer exactly (the fused stack's backward writes them as
+    views of one flat tensor, stack._Grads; AccumulateGrad installs them without a
+    copy), else None.  Reducing it in place reduces every ``p.grad``."""
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return None
+    st = grads[0].untyped_storage()
+    es = grads[0].element_size()
+    if any(g.untyped_storage().data_ptr() != st.data_ptr() or g.dtype != grads[0].dtype or not g.is_contiguous()
+           for g in grads):
+        return None
+    total = sum(g.numel() for g in grads)
+    if total * es != st.nbytes():
+        return None
+    o = 0
+    for g in sorted(grads, key=lambda t: t.storage_offset()):
+        if g.storage_offset() != o:
+            return None
+        o += g.numel()
+    return torch.empty(0, dtype=grads[0].dtype, device=grads[0].device).set_(st, 0, (total,))
+
+
 def allreduce_gradients(params, group=None, bucket_bytes=2 << 20, scale=None):
     """Reduce ``p.grad`` over the process group in flat buckets of at most
     ``bucket_bytes`` (all issued asynchronously, then waited): the mean when
@@ -106,6 +130,21 @@ def allreduce_gradients(params, group=None, bucket_bytes=2 << 20, scale=None):
         return
     world = dist.get_world_size(group)
     if world == 1:
+        return
+    flat = flat_gradients(params) if bucket_bytes >= (1 << 30) else None
+    if flat is not None:
+        # the gradients already form one flat buffer: reduce it in place (no cat /
+        # copy-back); the doc-weighted sum scales it first (one elementwise pass)
+        if scale is not None:
+            flat.mul_(scale)
+            op = dist.ReduceOp.SUM
+        elif dist.get_backend(group) == "nccl":
+            op = dist.ReduceOp.AVG
+        else:
+            op = dist.ReduceOp.SUM
+        dist.all_reduce(flat, op=op, group=group)
+        if scale is None and op == dist.ReduceOp.SUM:
+            flat.div_(world)
         return
     grads = [p.grad for p in params if p.grad is not None]
     pending = [_launch(b, scale, world, group) for b in _buckets(grads, bucket_bytes)]

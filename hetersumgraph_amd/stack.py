@@ -47,10 +47,33 @@ from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_t
 class _Grads:
     """The parameter-gradient buffers of one backward of the stack, keyed by
     parameter: created (written, not zero-filled) by a parameter's first
-    contribution, added into by the later ones.  Returned to autograd at the end."""
+    contribution, added into by the later ones.  Returned to autograd at the end.
 
-    def __init__(self):
+    All buffers are views of ONE flat tensor, in parameter order, so that a
+    data-parallel reducer can all-reduce the stack's gradients in place as a single
+    bucket once autograd has installed them as ``p.grad`` (parallel.flat_gradients)
+    -- no concatenation before the collective and no copy back after it."""
+
+    def __init__(self, params=()):
         self.buf = {}
+        live = [p for p in params if p is not None and p.requires_grad]
+        self.flat = None
+        self.views = {}
+        if live:
+            self.flat = torch.empty(sum(p.numel() for p in live), dtype=live[0].dtype, device=live[0].device)
+            o = 0
+            for p in live:
+                self.views[id(p)] = self.flat[o:o + p.numel()].view_as(p)
+                o += p.numel()
+
+    def _new(self, p, zero=False):
+        g = self.views.get(id(p))
+        if g is None:
+            g = torch.zeros_like(p) if zero else torch.empty_like(p)
+        elif zero:
+            g.zero_()
+        self.buf[id(p)] = g
+        return g
 
     def dst(self, p):
         """(buffer, accumulate) for p's gradient; (None, False) if p needs none."""
@@ -58,8 +81,7 @@ class _Grads:
             return None, False
         g = self.buf.get(id(p))
         if g is None:
-            g = self.buf[id(p)] = torch.empty_like(p)
-            return g, False
+            return self._new(p), False
         return g, True
 
     def group(self, ps):
@@ -70,12 +92,12 @@ class _Grads:
             return [None] * len(ps), False
         if all(id(p) not in self.buf for p in live):
             for p in live:
-                self.buf[id(p)] = torch.empty_like(p)
+                self._new(p)
             acc = False
         else:
             for p in live:
                 if id(p) not in self.buf:
-                    self.buf[id(p)] = torch.zeros_like(p)
+                    self._new(p, zero=True)
             acc = True
         return [self.buf[id(p)] if (p is not None and p.requires_grad) else None for p in ps], acc
 
@@ -271,7 +293,7 @@ class _GatStack(torch.autograd.Function):
         # attention-parameter partials of all applications of a layer meet in one
         # stage workspace; the parameter transform runs once per layer at the end
         stages, gbufs = {}, {}
-        pgrads = _Grads()
+        pgrads = _Grads(ctx.params)
         batch = SlabBatch()
         for lay, saved, nb, org, a in reversed(ctx.apps):
             dout = grads.pop((org[0], org[1] + 1))
@@ -321,6 +343,8 @@ class _GatStack(torch.autograd.Function):
         dw0 = grads.get(("w", 0)) if need_w0 else None
         ds0 = grads.get(("s", 0)) if need_s0 else None
         out = tuple(pgrads.get(p) for p in ctx.params)
+        # a parameter that got no contribution has no gradient (None), as before; its
+        # stretch of the flat buffer is left untouched (never read by the reducer)
         ctx.params = None
         return (None, dw0, ds0) + out
 

@@ -58,6 +58,7 @@ def main():
     params = [p for p in local.parameters() if p.requires_grad]
     # full-batch reference step on this device
     loss_of(docs, full, dev).backward()
+    ref_grads = [p.grad.detach().clone() for p in full.parameters()]
     ref_norm = torch.nn.utils.clip_grad_norm_(full.parameters(), 1.0)
     # data-parallel step: shard, backward with overlapped buckets, clip
     mine = shard_documents(docs, rank, world)
@@ -74,6 +75,18 @@ def main():
         err = (a.grad - b.grad).abs().max().item() / scale
         worst = max(worst, err)
         assert err <= 2e-5, (n, err)
+    # bench.py's exchange after a graph replay: the fused stack wrote every gradient
+    # into one flat buffer, reduced in place as one bucket (parallel.flat_gradients)
+    from hetersumgraph_amd.parallel import allreduce_gradients, flat_gradients
+    for p in params:
+        p.grad = None
+    loss_of(mine, local, dev).backward()
+    assert flat_gradients(params) is not None
+    allreduce_gradients(params, scale=shard_fraction(docs, rank, world), bucket_bytes=1 << 30)
+    for (n, a), b in zip(local.named_parameters(), ref_grads):
+        scale = max(b.abs().max().item(), 1e-8)
+        err = (a.grad - b).abs().max().item() / scale
+        assert err <= 2e-5, ("flat", n, err)
     print(f"rank {rank}: {len(mine)} docs, grad norm {norm.item():.6e} (full batch {ref_norm.item():.6e}), "
           f"max rel grad err {worst:.2e}", flush=True)
     dist.barrier()

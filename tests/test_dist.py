@@ -143,3 +143,29 @@ def test_shard_documents_balanced_and_deterministic():
     two = [shard_documents([D(e) for e in (100, 10, 10, 10)], r, 2) for r in range(2)]
     assert [len(s) for s in two] == [2, 2]
     assert [shard_documents(docs, r, 3) for r in range(3)] == shards
+
+
+def test_flat_gradients_detects_one_buffer():
+    """parallel.flat_gradients: gradients installed by autograd as views of one flat
+    tensor (what stack._Grads returns) are recognised and reduced in place; any
+    other layout falls back (None)."""
+    from hetersumgraph_amd.parallel import flat_gradients
+    p, q = torch.nn.Parameter(torch.zeros(3)), torch.nn.Parameter(torch.zeros(2, 2))
+
+    class F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, y):
+            return x.sum() + y.sum()
+
+        @staticmethod
+        def backward(ctx, g):
+            flat = torch.arange(7.0)
+            return flat[0:3].view(3), flat[3:7].view(2, 2)
+
+    F.apply(p, q).backward()
+    f = flat_gradients([q, p])                      # any order of the parameter list
+    assert f is not None and f.numel() == 7
+    f.mul_(2)
+    assert torch.equal(p.grad, torch.tensor([0.0, 2.0, 4.0])) and q.grad[1, 1].item() == 12.0
+    q.grad = q.grad.clone()                          # another buffer: no single flat view
+    assert flat_gradients([p, q]) is None
