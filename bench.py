@@ -297,7 +297,8 @@ def time_dense_kernel(stack, n_rows, reps):
     out = x.new_empty(n_rows, w1.shape[0])
     ws = ffn_wsplit(x, w1, b1, w2, b2)
     if ws is not None:
-        run, name = (lambda: gemm_psw(x, ws[0], bias=b1, relu=True, out=out)), "hsg_gemm_f32_psw"
+        run = lambda: gemm_psw(x, ws[0], bias=b1, relu=True, out=out)
+        name = "hsg_gemm_bf16_psw" if ws[0].mode == "bf16" else "hsg_gemm_f32_psw"
     else:
         run, name = (lambda: gemm(x, w1, b_t=True, bias=b1, relu=True, out=out)), "hsg_gemm_*"
     st = torch.cuda.current_stream()

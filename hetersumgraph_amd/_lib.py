@@ -31,7 +31,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
            "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
-           "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug")
+           "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
+           "hsg_gemm_bf16_slabs")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -109,10 +110,12 @@ _SIGS = {
     "hsg_wsplit_dims": [_I, _I, _P, _P],
     "hsg_dropmask_multi": [_I, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
+    "hsg_gemm_bf16_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
     "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_wsplit": [_I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
-    "hsg_gemm_f32_psw_elug": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _P],
+    "hsg_gemm_f32_psw_elug": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P],
+    "hsg_gemm_bf16_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
     "hsg_gat_bwd_dst_g": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 _RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_wsplit_dims": None, "hsg_gemm_workspace_floats": ctypes.c_size_t,

@@ -1233,14 +1233,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm5(GemmArgs p, const __bf16 *__re
 // four cfg2 S2W FFN shapes; the wide tiles (80 | 128) were not faster.
 // ---------------------------------------------------------------------------------
 typedef float f32x4v7 __attribute__((ext_vector_type(4)));
-template <int BN, int S, bool RNE = true>
+// PM: 0 = fp32-accurate (RNE 3-limb split, six products), 1 = the same with the
+// truncation split (dev), 2 = bf16 mode (hsg_gemm_bf16 semantics: A and the weight
+// rounded to bf16 RNE, ONE product: only limb plane 0 of the weight is staged)
+template <int BN, int S, int PM = 0>
 __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
     constexpr int A_FL = BM * 32;                          // floats of the A tile
     constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
-    constexpr int STAGE_FL = A_FL + 3 * B_BF / 2;          // stage size in floats
+    constexpr int NL = PM == 2 ? 1 : 3;                    // weight limb planes staged
+    constexpr int STAGE_FL = A_FL + NL * B_BF / 2;         // stage size in floats
     constexpr int BPC = BN / 16;                           // 1-KB pieces (16 rows) per limb plane tile
-    constexpr int NBP = (3 * BPC + 3) / 4;                 // B DMA instructions per wave per K tile
+    constexpr int NBP = (NL * BPC + 3) / 4;                // B DMA instructions per wave per K tile
     constexpr int NLD = BM / 32 + NBP;                     // all DMA instructions per wave per K tile
     static_assert(BN % 16 == 0, "BN must be a multiple of 16");
     __shared__ __attribute__((aligned(16))) float lds[S * STAGE_FL];
@@ -1267,10 +1271,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
         __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
 #pragma unroll
         for (int pc = 0; pc < NBP; ++pc) {
-            // 3 * BPC pieces over 4 waves; a wave short of pieces repeats the last one
+            // NL * BPC pieces over 4 waves; a wave short of pieces repeats the last one
             // (the same bytes to the same LDS address), so every wave issues NBP DMAs
             // and one vmcnt count serves all of them
-            const int piece = min(pc * 4 + wid, 3 * BPC - 1);
+            const int piece = min(pc * 4 + wid, NL * BPC - 1);
             const int limb = piece / BPC, prow = (piece % BPC) * 16;
             const int r = prow + (lane >> 2);
             const int c = (lane & 3) ^ ((r >> 2) & 3);
@@ -1302,8 +1306,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
             const int r = wid * 32 + 16 * i + li, sw = swz(r);
             const f32x4 x = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb) ^ sw)]);
             const f32x4 y = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb + 1) ^ sw)]);
-            if constexpr (RNE) split_rne8(x, y, a[i][0], a[i][1], a[i][2]);
-            else split_trunc8(x, y, a[i][0], a[i][1], a[i][2]);
+            if constexpr (PM == 0) {
+                split_rne8(x, y, a[i][0], a[i][1], a[i][2]);
+            } else if constexpr (PM == 1) {
+                split_trunc8(x, y, a[i][0], a[i][1], a[i][2]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[i][0][e] = (__bf16)(e < 4 ? x[e] : y[e - 4]);   // RNE
+            }
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -1311,15 +1321,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
             const int off = r * 32 + 8 * (kb ^ ((r >> 2) & 3));
             bf16x8 b[3];
 #pragma unroll
-            for (int l = 0; l < 3; ++l) b[l] = *reinterpret_cast<const bf16x8 *>(&sb[l * B_BF + off]);
+            for (int l = 0; l < NL; ++l) b[l] = *reinterpret_cast<const bf16x8 *>(&sb[l * B_BF + off]);
+            if constexpr (PM == 2) {
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {       // small products first
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[2], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[0], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[1], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
+                for (int i = 0; i < 2; ++i)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {   // small products first
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
+                }
             }
         }
         __builtin_amdgcn_iglp_opt(0);
@@ -1341,14 +1357,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
     if (p.colpart) epi_rows_colpart<BN>(lds, cs, wid, lane, ty, n0, p);
 }
 
-template <int BN, int S, bool RNE = true>
+template <int BN, int S, int PM = 0>
 int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
     p.k_tiles_per_split = Kp / 32;
     if ((p.N + BN - 1) / BN * BN > Np) return HSG_EINVAL;   // B tile rows must exist in the planes
     if (!epi_rows_ok(p)) return HSG_EINVAL;                 // the float4 epilogue needs whole aligned quads
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
-    hipLaunchKernelGGL((k_gemm7<BN, S, RNE>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
+    hipLaunchKernelGGL((k_gemm7<BN, S, PM>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -1693,6 +1709,22 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         if (e && e[0] == '0') mode = MODE_F32_MFMA;
         else dw3 = true;
     }
+    // bf16 mode: the split kernel's plans with ONE limb (the RNE bf16 rounding of each
+    // operand, one product) -- the same staging, tiles and transpose reads as the f32
+    // mode; HSG_GEMM_BF16_OLD=1 keeps the register-staged k_gemm<..., BF> tiles (A/B)
+    if (mode == MODE_BF16 && !getenv("HSG_GEMM_BF16_OLD")) {
+        int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
+        if (!ak && !bk) rc = launch3<64, 64, 32, 1, 1, 0>(p, ak, bk, splits, st);
+        else if (t3 == 1) rc = launch3<128, 64, 32, 1, 1>(p, ak, bk, splits, st);
+        else rc = launch3<64, 64, 32, 1, 1>(p, ak, bk, splits, st);
+        if (rc || splits == 1 || slabs_only) return rc;
+        const size_t total = (size_t)M * N;
+        int blocks = (int)((total + 255) / 256);
+        if (blocks > 2048) blocks = 2048;
+        hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, st, p, splits);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : (int)e;
+    }
     int g4 = 0;                                             // dev switch: k_gemm4 plans
     if (const char *f = getenv("HSG_GEMM4")) g4 = atoi(f);
     if (mode == MODE_F32_SPLIT && ak && bk && (K & 3) == 0 && g4 > 0) {
@@ -1771,6 +1803,15 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
         if (e[0] == 'm') mode = MODE_F32_MFMA;
     return gemm_impl(mode, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
+}
+
+int hsg_gemm_bf16_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
+                        int b_kcontig, int splits, float *workspace, void *stream) {
+    const int kt_total = (K + kBK - 1) / kBK;
+    if (splits < 2 || splits > kt_total || !workspace) return HSG_EINVAL;
+    float dummy_c;
+    return gemm_impl(MODE_BF16, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, &dummy_c, N, nullptr, nullptr, 0,
+                     HSG_EPI_STORE, 0, splits, workspace, nullptr, stream, true);
 }
 
 int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig, const float *B, int ldb,
@@ -1975,13 +2016,29 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 26) return launch5<128, 2, 0, true, true>(p, pl, Np, Kp, st);
     if (plan == 27 && epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
     if (plan == 27 || plan == 28 || plan == 30) return launch5<64, 2, 0>(p, pl, Np, Kp, st);   // unaligned / ragged quads
-    if (plan == 28 && epi_rows_ok(p)) return launch7<64, 2, false>(p, pl, Np, Kp, st);   // truncation split
+    if (plan == 28 && epi_rows_ok(p)) return launch7<64, 2, 1>(p, pl, Np, Kp, st);   // truncation split
     if (plan == 30 && epi_rows_ok(p)) return N <= 320 ? launch7<80, 2>(p, pl, Np, Kp, st) : launch7<128, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2>(p, pl, Np, Kp, st);
 }
 
+int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                      const float *bias, const float *aux, int ldaux, int epi, int relu, float *colsum_part,
+                      void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
+    if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K) return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
+    if (!epi_rows_ok(p)) return HSG_EINVAL;      // the caller keeps hsg_gemm_bf16 on the unsplit weight
+    return launch7<64, 2, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
-                          const float *aux, const float *x, const float *origin, float *G, int ld, void *stream) {
+                          const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
+                          void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G) return HSG_EINVAL;
     if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N)
         return HSG_EINVAL;
@@ -1991,6 +2048,7 @@ int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const vo
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, nullptr, aux, ld, HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr,
                1, 1, x, origin, G};
     if (!epi_rows_ok(p)) return HSG_EINVAL;
+    if (bf16) return launch7<64, 2, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
     return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
 }
 

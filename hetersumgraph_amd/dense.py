@@ -102,10 +102,12 @@ class SplitWeight:
     """A weight operand B [N][K] held as its three bf16 limb planes [3][Np][Kp]
     (hsg_wsplit), for gemm_psw: made once per step, reused by every GEMM that
     multiplies by B (the FFN's W1 / W2 in the forward, W1^T / W2^T in the backward)."""
-    __slots__ = ("planes", "N", "K")
+    __slots__ = ("planes", "N", "K", "W", "trans", "mode")
 
-    def __init__(self, planes, N, K):
+    def __init__(self, planes, N, K, W=None, trans=False, mode="f32"):
         self.planes, self.N, self.K = planes, N, K
+        self.W, self.trans = W, trans          # the fp32 weight (fallback path)
+        self.mode = mode                       # GEMM mode of the step that split it: 'f32' | 'bf16'
 
 
 def split_dims(N, K):
@@ -128,7 +130,7 @@ def split_weights(*specs):
         N, K = (W.shape[1], W.shape[0]) if trans else (W.shape[0], W.shape[1])
         Np, Kp = split_dims(N, K)
         planes = torch.empty(3 * Np * Kp, dtype=torch.bfloat16, device=W.device)
-        out.append(SplitWeight(planes, N, K))
+        out.append(SplitWeight(planes, N, K, W, bool(trans), "bf16" if _GEMM_DTYPE == "bf16" else "f32"))
         Ns.append(N); Ks.append(K); lds.append(W.stride(0)); trs.append(int(trans))
         Ws.append(W.data_ptr()); Ps.append(planes.data_ptr())
     n = len(specs)
@@ -141,7 +143,9 @@ def split_weights(*specs):
 
 def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, colsum_part=None):
     """C = A @ B^T [+ bias] [relu] | * (relu_mask > 0) | + add, with B a SplitWeight
-    (hsg_gemm_f32_psw; fp32-accurate as gemm(..., dtype='f32'))."""
+    (hsg_gemm_f32_psw: fp32-accurate as gemm(..., dtype='f32'); a weight split in the
+    'bf16' mode runs hsg_gemm_bf16_psw: its plane 0 = RNE(W), one bf16 product, as
+    gemm(..., dtype='bf16'))."""
     lib = load()
     if not A.is_cuda or A.dtype != torch.float32:
         raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
@@ -156,6 +160,14 @@ def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, c
         epi, aux = HSG_EPI_RELU_BWD, relu_mask
     elif add is not None:
         epi, aux = HSG_EPI_ADD, add
+    if Bs.mode == "bf16":
+        rc = lib.hsg_gemm_bf16_psw(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias), ptr(aux),
+                                   _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part), stream_of(A))
+        if rc == HSG_EINVAL and Bs.W is not None:           # unaligned / ragged quads: the unsplit weight
+            return gemm(A, Bs.W, b_t=not Bs.trans, out=out, bias=bias, relu=relu, relu_mask=relu_mask, add=add,
+                        splits=1 if colsum_part is not None else 0, colsum_part=colsum_part, dtype="bf16")
+        check(rc, "hsg_gemm_bf16_psw")
+        return out
     check(lib.hsg_gemm_f32_psw(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias), ptr(aux),
                                _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part),
                                stream_of(A)), "hsg_gemm_f32_psw")
@@ -174,7 +186,7 @@ def gemm_psw_elug(A, Bs, out, x, origin, G):
     if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in ts):
         return False
     rc = lib.hsg_gemm_f32_psw_elug(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
-                                   ptr(origin), ptr(G), N, stream_of(A))
+                                   ptr(origin), ptr(G), N, int(Bs.mode == "bf16"), stream_of(A))
     if rc == HSG_EINVAL:
         return False
     check(rc, "hsg_gemm_f32_psw_elug")
@@ -182,11 +194,12 @@ def gemm_psw_elug(A, Bs, out, x, origin, G):
 
 
 def gemm_slabs(A, B, a_t=False, b_t=False):
-    """The split-K partial products of op(A) @ op(B) (hsg_gemm_f32_slabs, 'f32' mode):
+    """The split-K partial products of op(A) @ op(B) (hsg_gemm_f32_slabs in the 'f32'
+    mode, hsg_gemm_bf16_slabs in 'bf16'):
     (workspace [splits*M*N], splits), summed later by hsg_slab_reduce -- or None when
     the automatic plan does not split this shape or the GEMM mode is not 'f32'."""
     lib = load()
-    if _GEMM_DTYPE != "f32" or not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
+    if _GEMM_DTYPE not in ("f32", "bf16") or not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32:
         return None
     M, K = (A.shape[1], A.shape[0]) if a_t else (A.shape[0], A.shape[1])
     K2, N = (B.shape[1], B.shape[0]) if b_t else (B.shape[0], B.shape[1])
@@ -201,8 +214,9 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     splits = int(os.environ.get("HSG_DW_SPLITS", "64"))          # dev A/B
     splits = max(2, min(splits, (K + 31) // 32))
     ws = A.new_empty(lib.hsg_gemm_workspace_floats(M, N, K, splits))
-    check(lib.hsg_gemm_f32_slabs(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), splits, ptr(ws),
-                                 stream_of(A)), "hsg_gemm_f32_slabs")
+    fn = lib.hsg_gemm_bf16_slabs if _GEMM_DTYPE == "bf16" else lib.hsg_gemm_f32_slabs
+    check(fn(M, N, K, ptr(A), _ld(A), int(not a_t), ptr(B), _ld(B), int(b_t), splits, ptr(ws), stream_of(A)),
+          "hsg_gemm_*_slabs")
     return ws, splits
 
 

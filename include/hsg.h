@@ -224,7 +224,16 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
  * (HSG_EINVAL otherwise: the caller keeps the split path).  The G rows feed
  * hsg_gat_bwd_dst_g. */
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
-                          const float *aux, const float *x, const float *origin, float *G, int ld, void *stream);
+                          const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
+                          void *stream);
+/* hsg_gemm_bf16 (A and the weight rounded to bf16 RNE, fp32 accumulation: config 5's
+ * mode) on the pre-split weight: only its limb plane 0 = RNE(W) is read, one bf16
+ * MFMA product per element pair.  Same arguments as hsg_gemm_f32_psw; N % 4 == 0 and
+ * 16-byte aligned C / aux rows (HSG_EINVAL otherwise).  hsg_gemm_f32_psw_elug with
+ * bf16 != 0 has these numerics too. */
+int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                      const float *bias, const float *aux, int ldaux, int epi, int relu, float *colsum_part,
+                      void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
@@ -235,6 +244,10 @@ int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const vo
 int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig,
                        const float *B, int ldb, int b_kcontig, int splits, float *workspace,
                        void *stream);
+/* The same for hsg_gemm_bf16 (operands rounded to bf16 RNE, one product). */
+int hsg_gemm_bf16_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig,
+                        const float *B, int ldb, int b_kcontig, int splits, float *workspace,
+                        void *stream);
 /* Deferred column sums of partial slabs, njobs (1..24) outputs in one deterministic
  * launch: out[q][b][c] = (accumulate[q] ? out[q][b][c] : 0) + scale[q] * sum over
  * job q's nseg[q] (1..4) segments s (in order) of the rows r in the b-th of

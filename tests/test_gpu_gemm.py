@@ -338,3 +338,24 @@ def test_slab_reduce_float4_columns_bitwise_equal_scalar(cols, pitch, coff, out_
         for r in range(out_rows):
             ref[r] += 0.75 * sg[r * pr:(r + 1) * pr, coff:coff + cols].double().sum(0)
     assert torch.allclose(vec.view(out_rows, cols).double(), ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(19200, 512, 300), (1000, 300, 512), (777, 64, 300), (33, 20, 20)])
+def test_psw_bf16_mode_is_the_rounded_product(M, N, K):
+    """bf16 GEMM mode on the pre-split weight (hsg_gemm_bf16_psw; plane 0 = RNE(W)):
+    equals an fp32 GEMM of the bf16-rounded operands up to summation order, and agrees
+    with hsg_gemm_bf16 on the unsplit weight (which it falls back to for ragged N)."""
+    from hetersumgraph_amd.dense import gemm, gemm_dtype, gemm_psw, split_weights
+    torch.manual_seed(M + N)
+    A = mk(M, K)
+    W = mk(N, K)
+    with gemm_dtype("bf16"):
+        (S,) = split_weights((W, False))
+        assert S.mode == "bf16"
+        b = torch.randn(N, device="cuda")
+        C = gemm_psw(A, S, bias=b, relu=True)
+        C2 = gemm(A, W, b_t=True, bias=b, relu=True)
+    ref = torch.relu(A.bfloat16().double() @ W.bfloat16().double().t() + b.double())
+    scale = max(1.0, ref.abs().max().item())
+    assert (C.double() - ref).abs().max().item() <= 1e-5 * scale * max(1.0, K ** 0.5)
+    assert (C2.double() - ref).abs().max().item() <= 1e-5 * scale * max(1.0, K ** 0.5)

@@ -22,6 +22,8 @@ def run(config="cfg2"):
     from hetersumgraph_amd import rng as hsg_rng
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from hetersumgraph_amd.dense import set_gemm_dtype
+    set_gemm_dtype(os.environ.get("HSG_PROFILE_DTYPE", "f32"))       # bench.py --dtype
     docs, G, _, _ = bench.make_shard(config, 0, 1, 0)
     G.to(dev)
     torch.manual_seed(0)
