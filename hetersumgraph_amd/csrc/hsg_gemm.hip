@@ -986,6 +986,7 @@ struct EpiRows {
         }
     }
 
+    template <bool NS = false>    // NS: dev diagnostic, no C store (tools/gemm5_sweep.py plan 34)
     __device__ __forceinline__ void finish(const float *wl, int row0, int col0, int lane, const GemmArgs &p,
                                            f32x4 &csum) {
         __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS writes
@@ -1010,7 +1011,7 @@ struct EpiRows {
                     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
                 }
             }
-            *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+            if (!NS || v[0] == 1234.5f) *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
             if (p.epi == HSG_EPI_ADD_ELUG) {
                 // G = dOut * elu'(h): 1 for e = elu(h) > 0, else e + 1 = exp(h) (continuous at 0)
                 f32x4 g;
@@ -1236,18 +1237,21 @@ typedef float f32x4v7 __attribute__((ext_vector_type(4)));
 // PM: 0 = fp32-accurate (RNE 3-limb split, six products), 1 = the same with the
 // truncation split (dev), 2 = bf16 mode (hsg_gemm_bf16 semantics: A and the weight
 // rounded to bf16 RNE, ONE product: only limb plane 0 of the weight is staged)
-template <int BN, int S, int PM = 0>
-__global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
+template <int BN, int S, int PM = 0, int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
     constexpr int A_FL = BM * 32;                          // floats of the A tile
     constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
     constexpr int NL = PM == 2 ? 1 : 3;                    // weight limb planes staged
+    constexpr bool NOMFMA = PM >= 5;                       // dev diagnostics (plans 34-38)
+    constexpr bool NOSPLIT = PM >= 6, NOB = PM == 7, NOA = PM == 8;
     constexpr int STAGE_FL = A_FL + NL * B_BF / 2;         // stage size in floats
     constexpr int BPC = BN / 16;                           // 1-KB pieces (16 rows) per limb plane tile
     constexpr int NBP = (NL * BPC + 3) / 4;                // B DMA instructions per wave per K tile
     constexpr int NLD = BM / 32 + NBP;                     // all DMA instructions per wave per K tile
+    constexpr int EPI_FL = BM * (BN + 4);                  // the epilogue's row images reuse the stages
     static_assert(BN % 16 == 0, "BN must be a multiple of 16");
-    __shared__ __attribute__((aligned(16))) float lds[S * STAGE_FL];
+    __shared__ __attribute__((aligned(16))) float lds[S * STAGE_FL > EPI_FL ? S * STAGE_FL : EPI_FL];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
@@ -1267,10 +1271,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
     auto issue = [&](int it) {
         float *st = lds + (it % S) * STAGE_FL;
         const int k0 = it * 32;
-        glds_tile<BM>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
+        if constexpr (!NOA) glds_tile<BM>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
         __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
 #pragma unroll
-        for (int pc = 0; pc < NBP; ++pc) {
+        for (int pc = 0; pc < (NOB ? 0 : NBP); ++pc) {
             // NL * BPC pieces over 4 waves; a wave short of pieces repeats the last one
             // (the same bytes to the same LDS address), so every wave issues NBP DMAs
             // and one vmcnt count serves all of them
@@ -1298,6 +1302,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
         asm volatile("" ::: "memory");
         if (it + S - 1 < nt) issue(it + S - 1);
         if (it == nt - 1) ep.load(p, m0 + wid * 32, n0, lane);   // overlaps the last tile's MFMAs
+        (void)NOSPLIT;
         const float *sa = lds + (it % S) * STAGE_FL;
         const __bf16 *sb = reinterpret_cast<const __bf16 *>(sa + A_FL);
         bf16x8 a[2][3];
@@ -1306,7 +1311,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
             const int r = wid * 32 + 16 * i + li, sw = swz(r);
             const f32x4 x = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb) ^ sw)]);
             const f32x4 y = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb + 1) ^ sw)]);
-            if constexpr (PM == 0) {
+            if constexpr (NOSPLIT) {
+                a[i][0] = __builtin_bit_cast(bf16x8, x);
+                a[i][1] = __builtin_bit_cast(bf16x8, y);
+                a[i][2] = a[i][0];
+            } else if constexpr (PM == 0 || PM == 4 || PM == 5) {
                 split_rne8(x, y, a[i][0], a[i][1], a[i][2]);
             } else if constexpr (PM == 1) {
                 split_trunc8(x, y, a[i][0], a[i][1], a[i][2]);
@@ -1322,7 +1331,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
             bf16x8 b[3];
 #pragma unroll
             for (int l = 0; l < NL; ++l) b[l] = *reinterpret_cast<const bf16x8 *>(&sb[l * B_BF + off]);
-            if constexpr (PM == 2) {
+            if constexpr (NOMFMA) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int l = 0; l < 3; ++l)
+                        acc[i][j][l] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, a[i][l])[0] ^
+                                                                      __builtin_bit_cast(u32x4, b[l])[1]);
+            } else if constexpr (PM == 2) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
@@ -1353,18 +1369,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm7(GemmArgs p, const __bf16 *__re
             for (int e = 0; e < 4; ++e) wl[(16 * i + rq + e) * (BN + 4) + 16 * j + c] = acc[i][j][e];
     f32x4 cs;
     if (nt == 0) ep.load(p, m0 + wid * 32, n0, lane);
-    ep.finish(wl, m0 + wid * 32, n0, lane, p, cs);
+    ep.template finish<PM == 4>(wl, m0 + wid * 32, n0, lane, p, cs);
     if (p.colpart) epi_rows_colpart<BN>(lds, cs, wid, lane, ty, n0, p);
 }
 
-template <int BN, int S, int PM = 0>
+template <int BN, int S, int PM = 0, int OCC = 2>
 int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
     p.k_tiles_per_split = Kp / 32;
     if ((p.N + BN - 1) / BN * BN > Np) return HSG_EINVAL;   // B tile rows must exist in the planes
     if (!epi_rows_ok(p)) return HSG_EINVAL;                 // the float4 epilogue needs whole aligned quads
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
-    hipLaunchKernelGGL((k_gemm7<BN, S, PM>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
+    hipLaunchKernelGGL((k_gemm7<BN, S, PM, OCC>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -2018,7 +2034,35 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 27 || plan == 28 || plan == 30) return launch5<64, 2, 0>(p, pl, Np, Kp, st);   // unaligned / ragged quads
     if (plan == 28 && epi_rows_ok(p)) return launch7<64, 2, 1>(p, pl, Np, Kp, st);   // truncation split
     if (plan == 30 && epi_rows_ok(p)) return N <= 320 ? launch7<80, 2>(p, pl, Np, Kp, st) : launch7<128, 2>(p, pl, Np, Kp, st);
+    if (plan == 34 && epi_rows_ok(p)) return launch7<64, 2, 4>(p, pl, Np, Kp, st);   // dev: no C store
+    if (plan == 35 && epi_rows_ok(p)) return launch7<64, 2, 5>(p, pl, Np, Kp, st);   // dev: no MFMA
+    if (plan == 36 && epi_rows_ok(p)) return launch7<64, 2, 6>(p, pl, Np, Kp, st);   // dev: loads only
+    if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
+    if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
     return launch5<64, 2>(p, pl, Np, Kp, st);
+}
+
+// bf16-mode k_gemm7 (one product per tile): dev plans for the tile / depth / occupancy sweep
+static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
+    int plan = 0;
+    if (const char *f = getenv("HSG_GEMM7B")) plan = atoi(f);
+    switch (plan) {
+    case 1: return launch7<64, 3, 2>(p, pl, Np, Kp, st);
+    case 2: return launch7<64, 4, 2>(p, pl, Np, Kp, st);
+    case 3: return launch7<128, 2, 2>(p, pl, Np, Kp, st);
+    case 4: return launch7<128, 3, 2>(p, pl, Np, Kp, st);
+    case 5: return (p.N + 255) / 256 * 256 <= Np ? launch7<256, 2, 2>(p, pl, Np, Kp, st)
+                                                 : launch7<128, 2, 2>(p, pl, Np, Kp, st);
+    case 6: return launch7<64, 2, 2, 4>(p, pl, Np, Kp, st);
+    case 7: return launch7<64, 3, 2, 3>(p, pl, Np, Kp, st);
+    case 8: return launch7<128, 2, 2, 3>(p, pl, Np, Kp, st);
+    case 9: return launch7<64, 2, 2>(p, pl, Np, Kp, st);
+    default:
+        // tools/gemm5_sweep.py BF16=1 at cfg5's 28800 word rows (3 interleaved rounds):
+        // N = 512 runs 31.1 us on 128-wide tiles against 37.8 on 64 (half the A re-reads);
+        // N = 300 is 29.1 us on 64 and 31.0 on 128 (384-wide padding)
+        return p.N > 320 ? launch7<128, 2, 2>(p, pl, Np, Kp, st) : launch7<64, 2, 2>(p, pl, Np, Kp, st);
+    }
 }
 
 int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
@@ -2033,7 +2077,7 @@ int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *
     hsg_wsplit_dims(N, K, &Np, &Kp);
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
     if (!epi_rows_ok(p)) return HSG_EINVAL;      // the caller keeps hsg_gemm_bf16 on the unsplit weight
-    return launch7<64, 2, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+    return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
 }
 
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
@@ -2048,7 +2092,7 @@ int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const vo
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, nullptr, aux, ld, HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr,
                1, 1, x, origin, G};
     if (!epi_rows_ok(p)) return HSG_EINVAL;
-    if (bf16) return launch7<64, 2, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+    if (bf16) return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
     return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
 }
 

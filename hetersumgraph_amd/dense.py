@@ -212,6 +212,9 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     # -17..-21 us against the 32 of hsg_gemm_f32's own plan; 24 / 48 / 96 / 128 are
     # slower, tools/ab.py)
     splits = int(os.environ.get("HSG_DW_SPLITS", "64"))          # dev A/B
+    minrows = int(os.environ.get("HSG_DW_MINROWS", "0"))         # dev A/B: rows per K slice
+    if minrows > 0:
+        splits = min(splits, K // minrows)
     splits = max(2, min(splits, (K + 31) // 32))
     ws = A.new_empty(lib.hsg_gemm_workspace_floats(M, N, K, splits))
     fn = lib.hsg_gemm_bf16_slabs if _GEMM_DTYPE == "bf16" else lib.hsg_gemm_f32_slabs

@@ -8,9 +8,16 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights  # noqa: E402
+from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, split_weights  # noqa: E402
 
-PLANS = {"7": "g5 BN64 iglp0 (r2)", "27": "g7 64 lds RNE prefetch"}
+# BF16=1: the bf16-mode kernel (hsg_gemm_bf16_psw) under HSG_GEMM7B plans instead
+BF16 = os.environ.get("BF16") == "1"
+# 34-38: k_gemm7 dev diagnostics (no C store / no MFMA / loads only / A only / B only)
+PLANS = {"27": "g7 64 lds RNE prefetch", "34": "dev: no C store", "35": "dev: no MFMA", "36": "dev: loads only",
+         "37": "dev: A loads only", "38": "dev: B loads only"}
+if BF16:
+    PLANS = {"0": "default (128 | 64 by N)", "9": "64 S2", "3": "128 S2"}
+ENV = "HSG_GEMM7B" if BF16 else "HSG_GEMM5"
 
 
 def timed(f, reps=20):
@@ -27,6 +34,9 @@ def timed(f, reps=20):
 
 
 n, d, dh = int(os.environ.get("ROWS", 19200)), 300, 512
+if BF16:
+    from hetersumgraph_amd.dense import set_gemm_dtype  # noqa: E402
+    set_gemm_dtype("bf16")
 W1 = torch.randn(dh, d, device="cuda") * 0.05
 W2 = torch.randn(d, dh, device="cuda") * 0.05
 x = torch.randn(n, d, device="cuda")
@@ -39,7 +49,8 @@ cases = [("ffn1 x.W1^T", x, W1, True, s1), ("ffn2 h.W2^T", H, W2, True, s2),
          ("dH = dy.W2", dy, W2, False, s2t), ("dx = dH.W1", H, W1, False, s1t)]
 ROUNDS = int(os.environ.get("ROUNDS", 5))
 for name, A, W, b_t, S in cases:
-    ref = A.double() @ (W.double().t() if b_t else W.double())
+    Ar, Wr = (A.bfloat16(), W.bfloat16()) if BF16 else (A, W)
+    ref = Ar.double() @ (Wr.double().t() if b_t else Wr.double())
     M, N = ref.shape
     K = A.shape[1]
     out = torch.empty(M, N, device="cuda")
@@ -47,11 +58,11 @@ for name, A, W, b_t, S in cases:
     errs = {}
     for _ in range(ROUNDS):                 # plans interleaved: box drift hits all alike
         for g5 in PLANS:
-            os.environ["HSG_GEMM5"] = g5
+            os.environ[ENV] = g5
             times[g5].append(timed(lambda: gemm_psw(A, S, out=out)))
             if g5 not in errs:
                 errs[g5] = ((out.double() - ref).abs().max() / ref.abs().max()).item()
-    os.environ.pop("HSG_GEMM5", None)
+    os.environ.pop(ENV, None)
     print(f"{name:14s} {M}x{N}x{K}", flush=True)
     for g5, tag in PLANS.items():
         t = sorted(times[g5])
