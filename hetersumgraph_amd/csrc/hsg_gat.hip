@@ -942,6 +942,123 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
     }
 }
 
+// Head-lane src pass for narrow heads (D = DV = 8, short CSC segments: the W2S word
+// sources, ~2 sentence edges each at config 2).  Lane = (source slot s, head k) with
+// hp = nextpow2(H) lanes per source, so a wave carries 64 / hp sources at once and each
+// lane owns its head's D features end to end: the per-edge alpha, dpre and the G-row
+// quads are the lane's own loads -- no LDS staging of alphas, no cross-lane sums -- and
+// the grid needs 64 / hp times fewer waves than one source per wave (cfg2 W2S: 2,400
+// waves, all resident, instead of 19,200 in 2.3 rounds of dependent chains).  Edge
+// pairs are requested together; accumulation is in edge order (fmaf per edge, as
+// gather_rows), dsigma in edge order.  d a1 block partials are summed over the
+// block's sources in (wave, slot) order: deterministic.
+template <int DV, int TAU_MODE>
+__global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D, int hp, float slope,
+                                                        const float *__restrict__ sigma,
+                                                        const float *__restrict__ tau,
+                                                        const float *__restrict__ mv,
+                                                        const float *__restrict__ lv,
+                                                        const float *__restrict__ G,
+                                                        const float *__restrict__ dpre,
+                                                        const float *__restrict__ a1,
+                                                        const float *__restrict__ Z,
+                                                        float *__restrict__ dZ, float *__restrict__ dsigma,
+                                                        float *__restrict__ da1_part) {
+    static_assert(DV % 4 == 0, "features move as float4");
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    constexpr int NQ = DV / 4;
+    __shared__ float s_tau[HSG_NT * HSG_HMAX];
+    __shared__ __attribute__((aligned(16))) float s_da1[HSG_WAVES][64 * DV];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const int sl = lane / hp, k = lane - sl * hp;
+    const bool kact = k < H;
+    const int wpw = 64 / hp;                                  // sources per wave
+    if constexpr (TAU_MODE == HSG_TAU_TABLE) {
+        for (int i = threadIdx.x; i < HSG_NT * H; i += blockDim.x) s_tau[i] = tau[i];
+        __syncthreads();
+    }
+    const int kc = kact ? k : 0;
+    f4 a1v[NQ], da1[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        a1v[q] = a1 ? *reinterpret_cast<const f4 *>(a1 + kc * D + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+        da1[q] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int u0 = (blockIdx.x * HSG_WAVES + wid) * wpw; u0 < R.n_src; u0 += gridDim.x * HSG_WAVES * wpw) {
+        const int u = u0 + sl;
+        const bool act = kact && u < R.n_src;
+        const int uc = act ? u : 0;
+        const int beg = act ? R.cindptr[uc] : 0, end = act ? R.cindptr[uc + 1] : 0;
+        const float sig = sigma[uc * H + kc];
+        f4 zr[NQ], acc[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            zr[q] = da1_part ? *reinterpret_cast<const f4 *>(Z + (size_t)uc * HD + kc * D + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+            acc[q] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+        float dsig = 0.f;
+        for (int p = beg; p < end; p += 2) {
+            const bool two = p + 1 < end;
+            const int p1 = two ? p + 1 : p;
+            const int v0 = R.cdst[p], e0 = R.cperm[p], v1 = R.cdst[p1], e1 = R.cperm[p1];
+            const int t0 = tau_row<TAU_MODE>(R, e0), t1 = tau_row<TAU_MODE>(R, e1);
+            const float M0 = mv[v0 * H + k], L0 = lv[v0 * H + k], M1 = mv[v1 * H + k], L1 = lv[v1 * H + k];
+            const float d0 = dpre[(size_t)e0 * H + k], d1 = dpre[(size_t)e1 * H + k];
+            f4 g0[NQ], g1[NQ];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                g0[q] = *reinterpret_cast<const f4 *>(G + (size_t)v0 * HD + k * D + 4 * q);
+                g1[q] = *reinterpret_cast<const f4 *>(G + (size_t)v1 * HD + k * D + 4 * q);
+            }
+            float tv0, tv1;
+            if constexpr (TAU_MODE == HSG_TAU_TABLE) { tv0 = s_tau[t0 * H + k]; tv1 = s_tau[t1 * H + k]; }
+            else { tv0 = tau[(size_t)t0 * H + k]; tv1 = tau[(size_t)t1 * H + k]; }
+            const float al0 = __expf(leaky(sig + tv0, slope) - M0) / L0;
+            const float al1 = __expf(leaky(sig + tv1, slope) - M1) / L1;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[q][j] = fmaf(al0, g0[q][j], acc[q][j]);
+            dsig += d0;
+            if (two) {
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) acc[q][j] = fmaf(al1, g1[q][j], acc[q][j]);
+                dsig += d1;
+            }
+        }
+        if (act) {
+            if (dsigma) dsigma[u * H + k] = dsig;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                f4 r = acc[q];
+                if (a1) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) r[j] = fmaf(dsig, a1v[q][j], r[j]);
+                }
+                *reinterpret_cast<f4 *>(dZ + (size_t)u * HD + k * D + 4 * q) = r;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) da1[q][j] = fmaf(dsig, zr[q][j], da1[q][j]);
+            }
+        }
+    }
+    if (da1_part) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) *reinterpret_cast<f4 *>(&s_da1[wid][lane * DV + 4 * q]) = da1[q];
+        __syncthreads();
+        for (int f = threadIdx.x; f < HD; f += blockDim.x) {
+            const int kk = f / D, d = f - kk * D;
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < HSG_WAVES; ++w)
+                for (int ss = 0; ss < wpw; ++ss) a += s_da1[w][(ss * hp + kk) * DV + d];
+            da1_part[(size_t)blockIdx.x * HD + f] = a;
+        }
+    }
+}
+
 // ------------------------------------------------------ sigma = <Z_k, a1_k> ----
 __global__ __launch_bounds__(256) void k_attn_src_logits(int n, int H, int D, int lph,
                                                         const float *__restrict__ Z,
@@ -1393,6 +1510,19 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
         return 0;
     }
     const int wpn = src_wpn(rel), lph = lanes_per_head(H);
+    // narrow heads over short segments: the head-lane kernel (HSG_GAT_SRC_HL=0: off)
+    const char *hl = getenv("HSG_GAT_SRC_HL");
+    if (wpn == 1 && D == 8 && H <= 8 && !(hl && atoi(hl) == 0) && (((uintptr_t)G | (uintptr_t)dZ | (uintptr_t)Z |
+                                                                 (uintptr_t)a1) & 15) == 0) {
+        const int hp = next_pow2(H);
+        if (tau_mode == HSG_TAU_TABLE)
+            HSG_KLAUNCH(false, true, (k_gat_bwd_src_hl<8, HSG_TAU_TABLE>), grid, dim3(256), st, R, H, D, hp, slope,
+                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
+        else
+            HSG_KLAUNCH(false, true, (k_gat_bwd_src_hl<8, HSG_TAU_PER_EDGE>), grid, dim3(256), st, R, H, D, hp, slope,
+                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
+        return launch_status();
+    }
     if (wpn == 4 && bwd_occ()) {
         if (tau_mode == HSG_TAU_TABLE)
             return bwd_src_dispatch<HSG_TAU_TABLE, 4, 5>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G,

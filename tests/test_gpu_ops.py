@@ -207,3 +207,39 @@ def test_forward_row_tile_variants(monkeypatch, nq, H, D, dense_band, per_edge):
     for name, got, want in zip(("Z", "a1", "tau", "origin"), dl, leaves):
         scale = want.grad.abs().max().item() + 1e-6
         assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
+
+
+@pytest.mark.parametrize("hl", ["0", "1"])
+@pytest.mark.parametrize("H,n_src,max_deg,per_edge", [(8, 300, 4, False), (8, 1000, 6, True), (5, 257, 3, False),
+                                                     (8, 64, 20, False)])
+def test_src_pass_head_lane_variant(monkeypatch, hl, H, n_src, max_deg, per_edge):
+    """The head-lane src pass (k_gat_bwd_src_hl: D = 8, short CSC segments -- the W2S
+    word sources) and the one-source-per-wave kernel (HSG_GAT_SRC_HL=0) against the
+    fp64 restatement: sources without edges, H < nextpow2(H) (idle head lanes), odd
+    segment lengths (the unpaired last edge), both tau modes."""
+    from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
+    from oracle.fused import gat_aggregate_ref
+    monkeypatch.setenv("HSG_GAT_SRC_HL", hl)
+    D = 8
+    rng = np.random.default_rng(n_src + H + max_deg)
+    rel, e_src, e_dst, tf, phantom = random_relation(rng, n_src, 40, max_deg * n_src // 40)
+    reld = rel.to("cuda")
+    f64 = dict(dtype=torch.float64)
+    Z = torch.randn(n_src, H * D, **f64)
+    a1 = torch.randn(H, D, **f64) * 0.3
+    tau = torch.randn(len(e_src) if per_edge else 11, H, **f64)
+    org = torch.randn(40, H * D, **f64)
+    R = torch.randn(40, H * D, **f64)
+    leaves = [t.clone().requires_grad_() for t in (Z, a1, tau, org)]
+    rows = np.arange(len(e_src)) if per_edge else tf
+    ref = gat_aggregate_ref(e_src, e_dst, rows, phantom, 40, *leaves)
+    (ref * R).sum().backward()
+    dl = [t.float().cuda().requires_grad_() for t in (Z, a1, tau, org)]
+    out = gat_aggregate(*dl[:3], dl[3], reld, H, D, tau_mode=HSG_TAU_PER_EDGE if per_edge else HSG_TAU_TABLE)
+    (out * R.float().cuda()).sum().backward()
+    torch.cuda.synchronize()
+    err = lambda a, b: (a.detach().cpu().double() - b.detach()).abs().max().item()
+    assert err(out, ref) < 2e-5
+    for name, got, want in zip(("Z", "a1", "tau", "origin"), dl, leaves):
+        scale = want.grad.abs().max().item() + 1e-6
+        assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
