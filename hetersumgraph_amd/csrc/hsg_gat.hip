@@ -130,7 +130,10 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
 }
 
 // ---------------------------------------------------------------- forward ----
-template <int NF, int TAU_MODE, int WPN, int OCC = 1>
+// PF (one destination per wave only): the next destination's indptr / phantom are
+// requested one iteration ahead (vector loads, consumed by readfirstlane), and the
+// residual row is requested before the score phase.
+template <int NF, int TAU_MODE, int WPN, int OCC = 1, bool PF = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
@@ -162,10 +165,30 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     float *sa = s_alpha[wid];
     int *sn = s_nb[wid];
 
-    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += gridDim.x * NPB) {
+    static_assert(!PF || WPN == 1, "prefetch: one destination per wave");
+    const int vstride = gridDim.x * NPB;
+    int pf_beg = 0, pf_end = 0, pf_c = 0;
+    if constexpr (PF) {
+        const int v0 = blockIdx.x * NPB + wid / WPN;
+        if (v0 < R.n_dst) { pf_beg = R.indptr[v0]; pf_end = R.indptr[v0 + 1]; pf_c = R.phantom[v0]; }
+    }
+    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += vstride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
-        const int beg = R.indptr[v], end = R.indptr[v + 1];
-        const int c = R.phantom[v];
+        int beg, end, c;
+        float org[NF];
+        if constexpr (PF) {
+            beg = __builtin_amdgcn_readfirstlane(pf_beg);
+            end = __builtin_amdgcn_readfirstlane(pf_end);
+            c = __builtin_amdgcn_readfirstlane(pf_c);
+#pragma unroll
+            for (int i = 0; i < NF; ++i) org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
+            const int vn = v_ + vstride;
+            if (vn < R.n_dst) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
+        } else {
+            beg = R.indptr[v];
+            end = R.indptr[v + 1];
+            c = R.phantom[v];
+        }
         int eb, ee;
         subrange(beg, end, part, WPN, eb, ee);
         const int n1 = ee - eb;
@@ -203,9 +226,10 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         const bool any = end > beg;
         const float inv = any ? 1.f / sm : 0.f;
         // the residual row: independent of the gathers below
-        float org[NF];
+        if constexpr (!PF) {
 #pragma unroll
-        for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
+            for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
+        }
 
         // phase 2: alphas per 64-edge chunk, then flat-mapped aggregation
         float acc[NF];
@@ -373,19 +397,25 @@ __global__ __launch_bounds__(256) void k_gat_fwd_grp(RelPtrs R, int H, int D, in
 // H*D = 300).  A block owns RT consecutive destinations, i.e. one contiguous
 // RT*H*D-float band of origin / h / out, and streams it as float4 slots
 // (slot q -> row q / (HD/4), columns 4(q % (HD/4)) .. +3; a slot may straddle two
-// heads, so each component carries its own head index).
-//   phase A: thread p < RT*H owns (row r, head k) = (p / H, p % H): online
-//            (max, sum) over the row's CSR segment in edge order, scores parked in
-//            LDS; after the phantom fold, the same thread turns them into alphas.
+// heads, so each component carries its own head index).  Every phase is parallel
+// over the block, so one block runs ONE dependent chain for all its rows:
+//   step 0:  the origin band (independent of everything, issued first), indptr and
+//            the phantom counts of the RT rows -> LDS;
+//   phase A1: thread p over the (edge j, head k) pairs of the block's contiguous
+//            edge range: src / tf -> sigma / tau -> score in LDS (two round trips
+//            for all edges at once, coalesced src / tf);
+//   phase A2: thread p < RT*H owns (row, head): online (max, sum) over the row's
+//            scores from LDS in CSR edge order, the phantom fold, m / l out, and
+//            the alphas in place;
 //   phase B: every slot sums alpha * Z[src] (float4 gathers) over its row's edges
 //            in CSR order, then writes h and elu(h) + origin with float4 stores.
-// Block edge ranges longer than kRowsEcap edges are processed in kRowsEcap chunks
-// (scores recomputed for the chunks after the first).  The origin band is loaded
-// before phase A so the HBM stream overlaps the index -> score chain.
+// Block edge ranges longer than the LDS chunk run A1 / A2 per chunk to get the
+// softmax state first, then recompute each chunk's alphas (rows found by a binary
+// search over the staged indptr) before its gathers.
 constexpr int kRowsThreads = 256;
 constexpr int kRowsEcap = 512;            // edges staged per chunk
-constexpr int kRowsAlpha = 4096;          // floats of staged alphas (kRowsEcap x H <= this)
-constexpr int kRowsMaxPairs = 512;        // RT * H bound
+constexpr int kRowsAlpha = 4096;          // floats of staged scores / alphas (ecap x H <= this, < 2^12)
+constexpr int kRowsMaxPairs = kRowsThreads;   // RT * H bound: one (row, head) pair per thread
 
 template <int NQ, int TAU_MODE>
 __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H, int D, int RT, float slope,
@@ -396,16 +426,18 @@ __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H,
                                                                float *__restrict__ hout, float *__restrict__ out,
                                                                float *__restrict__ mout, float *__restrict__ lout) {
     __shared__ int s_ptr[kRowsMaxPairs + 1];
+    __shared__ int s_ph[kRowsMaxPairs];
     __shared__ int s_src[kRowsEcap];
     __shared__ float s_alpha[kRowsAlpha];
     __shared__ float s_m[kRowsMaxPairs], s_inv[kRowsMaxPairs];
     const int HD = H * D, HD4 = HD >> 2;
+    const float inv_h = 1.f / (float)H;
     const int ecap = min(kRowsEcap, kRowsAlpha / H);
     const int t = threadIdx.x;
     const int v0 = blockIdx.x * RT;
     const int rows = min(RT, R.n_dst - v0);
     const int nslot = rows * HD4;
-    // slot geometry and the residual band, issued first
+    // step 0: slot geometry and the residual band, issued first
     // skh: head k0 of the slot's first column and the component b from which the
     // columns belong to head k0 + 1 (b = 4: none), packed as k0 * 8 + b
     int srow[NQ], scol[NQ], skh[NQ];
@@ -422,32 +454,50 @@ __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H,
                         : f32x4_t{0.f, 0.f, 0.f, 0.f};
     }
     for (int r = t; r <= rows; r += kRowsThreads) s_ptr[r] = R.indptr[v0 + r];
+    if (t < rows) s_ph[t] = R.phantom[v0 + t];
     __syncthreads();
     const int E0 = s_ptr[0], E1 = s_ptr[rows];
-    // phase A: per (row, head) softmax state
-    for (int p = t; p < rows * H; p += kRowsThreads) {
-        const int r = p / H, k = p - (p / H) * H;
-        const int beg = s_ptr[r], end = s_ptr[r + 1];
-        float mx = -INFINITY, sm = 0.f;
-        for (int e = beg; e < end; ++e) {
+    const bool single = E1 - E0 <= ecap;
+    // the (row, head) pair this thread owns in A2
+    const int pr = div_small(t, inv_h), pk = t - pr * H;
+    const bool pown = t < rows * H;
+    const int pbeg = pown ? s_ptr[pr] : 0, pend = pown ? s_ptr[pr + 1] : 0;
+    float mx = -INFINITY, sm = 0.f;
+    for (int c0 = E0; c0 < E1; c0 += ecap) {
+        const int c1 = min(E1, c0 + ecap), ne = c1 - c0;
+        if (c0 > E0) __syncthreads();                    // A2 of the previous chunk is done
+        // A1: scores of every (edge, head) pair of the chunk
+        for (int p = t; p < ne * H; p += kRowsThreads) {
+            const int j = div_small(p, inv_h), k = p - j * H;
+            const int e = c0 + j;
             const int u = R.src[e];
-            const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
-            if (e - E0 < ecap) {
-                s_alpha[(e - E0) * H + k] = s;
-                if (k == 0) s_src[e - E0] = u;
-            }
-            if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
-            else sm += __expf(s - mx);
+            s_alpha[p] = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+            if (k == 0) s_src[j] = u;
         }
-        const int c = R.phantom[v0 + r];
+        __syncthreads();
+        // A2: online (max, sum) of the owned pair over its edges in this chunk
+        if (pown) {
+            const int b = max(pbeg, c0), en = min(pend, c1);
+            for (int e = b; e < en; ++e) {
+                const float s = s_alpha[(e - c0) * H + pk];
+                if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
+                else sm += __expf(s - mx);
+            }
+        }
+    }
+    if (pown) {
+        const int c = s_ph[pr];
         if (c > 0) lse_merge(mx, sm, 0.f, (float)c);
-        const bool any = end > beg;
+        const bool any = pend > pbeg;
         const float inv = any ? 1.f / sm : 0.f;
-        mout[(v0 + r) * H + k] = any ? mx : 0.f;
-        lout[(v0 + r) * H + k] = any ? sm : 1.f;
-        s_m[p] = mx;
-        s_inv[p] = inv;
-        for (int e = beg; e < end && e - E0 < ecap; ++e) s_alpha[(e - E0) * H + k] = __expf(s_alpha[(e - E0) * H + k] - mx) * inv;
+        mout[(v0 + pr) * H + pk] = any ? mx : 0.f;
+        lout[(v0 + pr) * H + pk] = any ? sm : 1.f;
+        if (single) {
+            for (int e = pbeg; e < pend; ++e) s_alpha[(e - E0) * H + pk] = __expf(s_alpha[(e - E0) * H + pk] - mx) * inv;
+        } else {
+            s_m[t] = mx;
+            s_inv[t] = inv;
+        }
     }
     __syncthreads();
     f32x4_t acc[NQ];
@@ -455,22 +505,25 @@ __global__ __launch_bounds__(kRowsThreads) void k_gat_fwd_rows(RelPtrs R, int H,
     for (int i = 0; i < NQ; ++i) acc[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     for (int c0 = E0; c0 < E1; c0 += ecap) {
         const int c1 = min(E1, c0 + ecap);
-        if (c0 > E0) {                                   // later chunks: recompute alphas
-            __syncthreads();                             // the previous chunk is consumed
-            for (int p = t; p < rows * H; p += kRowsThreads) {
-                const int r = p / H, k = p - (p / H) * H;
-                const int beg = max(s_ptr[r], c0), end = min(s_ptr[r + 1], c1);
-                for (int e = beg; e < end; ++e) {
-                    const int u = R.src[e];
-                    const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
-                    s_alpha[(e - c0) * H + k] = __expf(s - s_m[p]) * s_inv[p];
-                    if (k == 0) s_src[e - c0] = u;
+        if (!single) {                                   // recompute this chunk's alphas
+            if (c0 > E0) __syncthreads();                // the previous chunk is gathered
+            for (int p = t; p < (c1 - c0) * H; p += kRowsThreads) {
+                const int j = div_small(p, inv_h), k = p - j * H;
+                const int e = c0 + j;
+                int lo = 0, hi = rows - 1;               // row: last r with s_ptr[r] <= e
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_ptr[mid] <= e) lo = mid; else hi = mid - 1;
                 }
+                const int u = R.src[e];
+                const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                s_alpha[p] = __expf(s - s_m[lo * H + k]) * s_inv[lo * H + k];
+                if (k == 0) s_src[j] = u;
             }
             __syncthreads();
         }
-        // edge jj of every slot's row in one step, so a thread's NQ gathers are in
-        // flight together; per slot the sum still runs in CSR edge order
+        // phase B: edge jj of every slot's row in one step, so a thread's NQ gathers
+        // are in flight together; per slot the sum still runs in CSR edge order
         int sb[NQ], sn[NQ], nmax = 0;
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
@@ -619,7 +672,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 // GIN (with NOH): the G rows are given (hsg_gemm_f32_psw_elug produced them in the
 // FFN backward's epilogue): read instead of dOut / x / origin, and not written.
 constexpr int kCh = 16;
-template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false, bool GIN = false>
+// PF (GIN only): the next destination's indptr and softmax state are requested one
+// iteration ahead (vector loads, consumed by readfirstlane / directly).
+template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false, bool GIN = false, bool PF = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
                                                     const float *__restrict__ Z,
@@ -648,12 +703,40 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
         wave_lds_sync();
     }
 
-    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += gridDim.x * HSG_WAVES) {
+    static_assert(!PF || GIN, "prefetch: the G-input pass");
+    const int vstride = gridDim.x * HSG_WAVES;
+    int pf_beg = 0, pf_end = 0;
+    float pf_m = 0.f, pf_l = 1.f;
+    if constexpr (PF) {
+        const int v0 = blockIdx.x * HSG_WAVES + wid;
+        if (v0 < R.n_dst) {
+            pf_beg = R.indptr[v0];
+            pf_end = R.indptr[v0 + 1];
+            if (kact) { pf_m = mv[v0 * H + k]; pf_l = lv[v0 * H + k]; }
+        }
+    }
+    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += vstride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);
-        const int beg = R.indptr[v], end = R.indptr[v + 1];
-        // softmax state of v: independent of everything below, issued first
-        const float M = kact ? mv[v * H + k] : 0.f;
-        const float lvv = kact ? lv[v * H + k] : 1.f;
+        int beg, end;
+        float M, lvv;
+        if constexpr (PF) {
+            beg = __builtin_amdgcn_readfirstlane(pf_beg);
+            end = __builtin_amdgcn_readfirstlane(pf_end);
+            M = kact ? pf_m : 0.f;
+            lvv = kact ? pf_l : 1.f;
+            const int vn = v_ + vstride;
+            if (vn < R.n_dst) {
+                pf_beg = R.indptr[vn];
+                pf_end = R.indptr[vn + 1];
+                if (kact) { pf_m = mv[vn * H + k]; pf_l = lv[vn * H + k]; }
+            }
+        } else {
+            beg = R.indptr[v];
+            end = R.indptr[v + 1];
+            // softmax state of v: independent of everything below, issued first
+            M = kact ? mv[v * H + k] : 0.f;
+            lvv = kact ? lv[v * H + k] : 1.f;
+        }
         // prefetch edge j = l of this head: source rank, tau row and pre-activation
         int u0 = 0, t0 = 0;
         float pre0 = 0.f;
@@ -1134,13 +1217,13 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
         }                                                                                                   \
     } while (0)
 
-template <int TAU, int WPN, int OCC = 1>
+template <int TAU, int WPN, int OCC = 1, bool PF = false>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
                  float *out, float *m, float *l) {
 #define HSG_FWD(NF_)                                                                                     \
     case NF_:                                                                                            \
-        HSG_KLAUNCH(true, true, (k_gat_fwd<NF_, TAU, WPN, OCC>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
+        HSG_KLAUNCH(true, true, (k_gat_fwd<NF_, TAU, WPN, OCC, PF>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
                     sg, tau, org, h, out, m, l);                                                         \
         break;
     switch (nf) {
@@ -1217,9 +1300,12 @@ RowsPlan rows_plan(int H, int D, bool aligned) {
     const int hd4 = HD / 4;
     static const int nqs[] = {1, 2, 3, 4, 5, 6, 8};
     double best_u = 0.0;
+    int rt_force = 0;                                   // dev sweep: rows per block
+    if (const char *e = getenv("HSG_GAT_ROWS_RT")) rt_force = atoi(e);
     for (int nq : nqs) {
         if (force > 0 && nq != force) continue;
         int rt = kRowsThreads * nq / hd4;
+        if (rt_force > 0 && rt_force < rt) rt = rt_force;
         if (rt > kRowsMaxPairs / H) rt = kRowsMaxPairs / H;
         if (rt < 1) continue;
         const double u = (double)rt * hd4 / (kRowsThreads * nq);
@@ -1235,8 +1321,8 @@ int fwd_rows_dispatch(RowsPlan pl, hipStream_t st, RelPtrs R, int H, int D, floa
     const dim3 grid((unsigned)((R.n_dst + pl.rt - 1) / pl.rt));
 #define HSG_FR(NQ_)                                                                                     \
     case NQ_:                                                                                           \
-        hipLaunchKernelGGL((k_gat_fwd_rows<NQ_, TAU>), grid, dim3(kRowsThreads), 0, st, R, H, D, pl.rt, \
-                           slope, Z, sg, tau, org, h, out, m, l);                                        \
+        HSG_KLAUNCH(true, true, (k_gat_fwd_rows<NQ_, TAU>), grid, dim3(kRowsThreads), st, R, H, D, pl.rt, \
+                    slope, Z, sg, tau, org, h, out, m, l);                                               \
         break;
     switch (pl.nq) {
         HSG_FR(1) HSG_FR(2) HSG_FR(3) HSG_FR(4) HSG_FR(5) HSG_FR(6) HSG_FR(8)
@@ -1253,6 +1339,20 @@ bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
 // drops them.  cfg2 S2W backward 61.2 -> 56.1 us per step in one A/B.
 bool bwd_occ() {
     const char *e = getenv("HSG_GAT_BWD_OCC");
+    return !(e && atoi(e) == 0);
+}
+
+// next-destination prefetch in the G-input dst pass (dev knob, HSG_GAT_DST_PF=1)
+bool dst_pf() {
+    const char *e = getenv("HSG_GAT_DST_PF");
+    return e && atoi(e) == 1;
+}
+
+// next-destination prefetch in the one-destination-per-wave forward: cfg2 S2W
+// forward 17.8 -> 17.2 us in-step, step 1.3084 -> 1.3049 ms in one A/B (round 3);
+// HSG_GAT_FWD_PF=0 drops it
+bool fwd_pf() {
+    const char *e = getenv("HSG_GAT_FWD_PF");
     return !(e && atoi(e) == 0);
 }
 
@@ -1278,14 +1378,14 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
     return launch_status();
 }
 
-template <int TAU, int OCC = 1, bool NOH = false, bool GIN = false>
+template <int TAU, int OCC = 1, bool NOH = false, bool GIN = false, bool PF = false>
 int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, int om,
                      float slope, const float *Z, const float *sg, const float *tau, const float *h,
                      const float *m, const float *l, const float *dout, float *G, float *dpre,
                      float *dtp, const float *x = nullptr, const float *org = nullptr) {
 #define HSG_BD(NE_)                                                                                        \
     case NE_:                                                                                              \
-        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH, GIN>), grid, dim3(256), st, R, H, D, lph, \
+        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH, GIN, PF>), grid, dim3(256), st, R, H, D, lph, \
                     om, slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp, x, org);                           \
         break;
     if constexpr (NOH) {                 // the shapes the fused stack's S2W pass uses
@@ -1375,6 +1475,13 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     const int lph = lanes_per_head(H);
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
+        if (fwd_pf()) {
+            if (tau_mode == HSG_TAU_TABLE)
+                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, true>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                               origin, h, out, m, l);
+            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, true>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                              origin, h, out, m, l);
+        }
 #define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
         if (tau_mode == HSG_TAU_TABLE) return occ == 8 ? HSG_FO(HSG_TAU_TABLE, 8) : HSG_FO(HSG_TAU_TABLE, 7);
         return occ == 8 ? HSG_FO(HSG_TAU_PER_EDGE, 8) : HSG_FO(HSG_TAU_PER_EDGE, 7);
@@ -1483,6 +1590,13 @@ int hsg_gat_bwd_dst_g(const hsg_rel *rel, int H, int D, int tau_mode, float slop
     }
     const int ne = ne_bucket((D + lph - 1) / lph);
     float *Gw = const_cast<float *>(G);                 // read only (GIN)
+    if (dst_pf()) {
+        if (tau_mode == HSG_TAU_TABLE)
+            return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma,
+                                                                        tau, nullptr, m, l, nullptr, Gw, dpre, dtau_part);
+        return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6, true, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma,
+                                                                       tau, nullptr, m, l, nullptr, Gw, dpre, dtau_part);
+    }
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
                                                               nullptr, m, l, nullptr, Gw, dpre, dtau_part);

@@ -60,17 +60,19 @@ def test_gat_aggregate_matches_op_restatement(H, D, max_deg, origin, per_edge):
         assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
 
 
-@pytest.mark.parametrize("lpn", ["16", "32", "64"])
+@pytest.mark.parametrize("lpn", ["16", "32", "64", "64-nopf"])
 @pytest.mark.parametrize("H,D,skew,per_edge", [(6, 50, False, False), (6, 50, True, False), (8, 16, True, True),
                                                (1, 300, True, False), (16, 8, False, False)])
 def test_forward_lanes_per_node_variants(monkeypatch, lpn, H, D, skew, per_edge):
-    """Every forward work split (one destination per wave, or 2 / 4 per wave in
-    LPN-lane groups, HSG_GAT_LPN) against the fp64 restatement, on short
+    """Every forward work split (one destination per wave -- with the next
+    destination's indptr prefetched (default) or not (HSG_GAT_FWD_PF=0) -- or 2 / 4
+    per wave in LPN-lane groups, HSG_GAT_LPN) against the fp64 restatement, on short
     segments with a few long ones (skew: > 32 edges -> multi-chunk groups)."""
     from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
     from hetersumgraph_amd.relation import Relation
     from oracle.fused import gat_aggregate_ref
-    monkeypatch.setenv("HSG_GAT_LPN", lpn)
+    monkeypatch.setenv("HSG_GAT_LPN", lpn.split("-")[0])
+    monkeypatch.setenv("HSG_GAT_FWD_PF", "0" if lpn.endswith("nopf") else "1")
     rng = np.random.default_rng(H * 31 + D + skew)
     n_src, n_dst = 150, 203
     deg = rng.integers(0, 4, size=n_dst)

@@ -15,6 +15,8 @@ BF16 = os.environ.get("BF16") == "1"
 # 34-38: k_gemm7 dev diagnostics (no C store / no MFMA / loads only / A only / B only)
 PLANS = {"27": "g7 64 lds RNE prefetch", "34": "dev: no C store", "35": "dev: no MFMA", "36": "dev: loads only",
          "37": "dev: A loads only", "38": "dev: B loads only"}
+if os.environ.get("PLANS"):                 # e.g. PLANS=27,40,41
+    PLANS = {k: f"plan {k}" for k in os.environ["PLANS"].split(",")}
 if BF16:
     PLANS = {"0": "default (128 | 64 by N)", "9": "64 S2", "3": "128 S2"}
 ENV = "HSG_GEMM7B" if BF16 else "HSG_GEMM5"
