@@ -108,7 +108,8 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
                                             const float *w, int H, const int (&fh)[NF], const int (&fo)[NF],
                                             float (&acc)[NF]) {
     // measured on the config-2 passes: grouping pays for narrow rows (NF <= 2);
-    // for wide rows the extra registers cost more occupancy than they buy
+    // for wide rows the extra registers cost more occupancy than they buy (two-row
+    // groups in the S2W forward: 20.9 vs 18.4 us in-step, round 3)
     constexpr int GR = NF <= 2 ? 4 : 1;
     for (int j0 = 0; j0 < n; j0 += GR) {
         float xv[GR][NF];
@@ -133,7 +134,7 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
 // PF (one destination per wave only): the next destination's indptr / phantom are
 // requested one iteration ahead (vector loads, consumed by readfirstlane), and the
 // residual row is requested before the score phase.
-template <int NF, int TAU_MODE, int WPN, int OCC = 1, bool PF = false>
+template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0>
 __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     float *sa = s_alpha[wid];
     int *sn = s_nb[wid];
 
-    static_assert(!PF || WPN == 1, "prefetch: one destination per wave");
+    static_assert(PF == 0 || WPN == 1, "prefetch: one destination per wave");
     const int vstride = gridDim.x * NPB;
     int pf_beg = 0, pf_end = 0, pf_c = 0;
     if constexpr (PF) {
@@ -180,6 +181,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             beg = __builtin_amdgcn_readfirstlane(pf_beg);
             end = __builtin_amdgcn_readfirstlane(pf_end);
             c = __builtin_amdgcn_readfirstlane(pf_c);
+            // the residual row first: measured 17.3 us against 18.5 us with the row
+            // requested after the score loads (cfg2 S2W, in-step), although vmcnt counts
+            // in issue order and the score chain then also waits for this HBM row
 #pragma unroll
             for (int i = 0; i < NF; ++i) org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
             const int vn = v_ + vstride;
@@ -226,7 +230,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         const bool any = end > beg;
         const float inv = any ? 1.f / sm : 0.f;
         // the residual row: independent of the gathers below
-        if constexpr (!PF) {
+        if constexpr (PF == 0) {
 #pragma unroll
             for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
         }
@@ -672,9 +676,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 // GIN (with NOH): the G rows are given (hsg_gemm_f32_psw_elug produced them in the
 // FFN backward's epilogue): read instead of dOut / x / origin, and not written.
 constexpr int kCh = 16;
-// PF (GIN only): the next destination's indptr and softmax state are requested one
-// iteration ahead (vector loads, consumed by readfirstlane / directly).
-template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false, bool GIN = false, bool PF = false>
+template <int NE, int TAU_MODE, int OCC = 1, bool NOH = false, bool GIN = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int D, int lph, int origin_mode,
                                                     float slope,
                                                     const float *__restrict__ Z,
@@ -703,40 +705,12 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
         wave_lds_sync();
     }
 
-    static_assert(!PF || GIN, "prefetch: the G-input pass");
-    const int vstride = gridDim.x * HSG_WAVES;
-    int pf_beg = 0, pf_end = 0;
-    float pf_m = 0.f, pf_l = 1.f;
-    if constexpr (PF) {
-        const int v0 = blockIdx.x * HSG_WAVES + wid;
-        if (v0 < R.n_dst) {
-            pf_beg = R.indptr[v0];
-            pf_end = R.indptr[v0 + 1];
-            if (kact) { pf_m = mv[v0 * H + k]; pf_l = lv[v0 * H + k]; }
-        }
-    }
-    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += vstride) {
+    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += gridDim.x * HSG_WAVES) {
         const int v = __builtin_amdgcn_readfirstlane(v_);
-        int beg, end;
-        float M, lvv;
-        if constexpr (PF) {
-            beg = __builtin_amdgcn_readfirstlane(pf_beg);
-            end = __builtin_amdgcn_readfirstlane(pf_end);
-            M = kact ? pf_m : 0.f;
-            lvv = kact ? pf_l : 1.f;
-            const int vn = v_ + vstride;
-            if (vn < R.n_dst) {
-                pf_beg = R.indptr[vn];
-                pf_end = R.indptr[vn + 1];
-                if (kact) { pf_m = mv[vn * H + k]; pf_l = lv[vn * H + k]; }
-            }
-        } else {
-            beg = R.indptr[v];
-            end = R.indptr[v + 1];
-            // softmax state of v: independent of everything below, issued first
-            M = kact ? mv[v * H + k] : 0.f;
-            lvv = kact ? lv[v * H + k] : 1.f;
-        }
+        const int beg = R.indptr[v], end = R.indptr[v + 1];
+        // softmax state of v: independent of everything below, issued first
+        const float M = kact ? mv[v * H + k] : 0.f;
+        const float lvv = kact ? lv[v * H + k] : 1.f;
         // prefetch edge j = l of this head: source rank, tau row and pre-activation
         int u0 = 0, t0 = 0;
         float pre0 = 0.f;
@@ -1217,7 +1191,7 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
         }                                                                                                   \
     } while (0)
 
-template <int TAU, int WPN, int OCC = 1, bool PF = false>
+template <int TAU, int WPN, int OCC = 1, int PF = 0>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
                  float *out, float *m, float *l) {
@@ -1342,18 +1316,12 @@ bool bwd_occ() {
     return !(e && atoi(e) == 0);
 }
 
-// next-destination prefetch in the G-input dst pass (dev knob, HSG_GAT_DST_PF=1)
-bool dst_pf() {
-    const char *e = getenv("HSG_GAT_DST_PF");
-    return e && atoi(e) == 1;
-}
-
 // next-destination prefetch in the one-destination-per-wave forward: cfg2 S2W
 // forward 17.8 -> 17.2 us in-step, step 1.3084 -> 1.3049 ms in one A/B (round 3);
 // HSG_GAT_FWD_PF=0 drops it
-bool fwd_pf() {
+int fwd_pf() {
     const char *e = getenv("HSG_GAT_FWD_PF");
-    return !(e && atoi(e) == 0);
+    return e && atoi(e) == 0 ? 0 : 1;
 }
 
 // occupancy hint of the one-destination-per-wave forward: 7 waves per SIMD (73 -> 64
@@ -1378,14 +1346,14 @@ int bwd_dst_ep_dispatch(int D, dim3 grid, hipStream_t st, RelPtrs R, int H, int 
     return launch_status();
 }
 
-template <int TAU, int OCC = 1, bool NOH = false, bool GIN = false, bool PF = false>
+template <int TAU, int OCC = 1, bool NOH = false, bool GIN = false>
 int bwd_dst_dispatch(int ne, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, int om,
                      float slope, const float *Z, const float *sg, const float *tau, const float *h,
                      const float *m, const float *l, const float *dout, float *G, float *dpre,
                      float *dtp, const float *x = nullptr, const float *org = nullptr) {
 #define HSG_BD(NE_)                                                                                        \
     case NE_:                                                                                              \
-        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH, GIN, PF>), grid, dim3(256), st, R, H, D, lph, \
+        HSG_KLAUNCH(true, false, (k_gat_bwd_dst<NE_, TAU, OCC, NOH, GIN>), grid, dim3(256), st, R, H, D, lph, \
                     om, slope, Z, sg, tau, h, m, l, dout, G, dpre, dtp, x, org);                           \
         break;
     if constexpr (NOH) {                 // the shapes the fused stack's S2W pass uses
@@ -1475,12 +1443,13 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     const int lph = lanes_per_head(H);
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
-        if (fwd_pf()) {
+        const int pf = fwd_pf();
+        if (pf == 1) {
             if (tau_mode == HSG_TAU_TABLE)
-                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, true>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                               origin, h, out, m, l);
-            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, true>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                              origin, h, out, m, l);
+                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                            origin, h, out, m, l);
+            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                           origin, h, out, m, l);
         }
 #define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
         if (tau_mode == HSG_TAU_TABLE) return occ == 8 ? HSG_FO(HSG_TAU_TABLE, 8) : HSG_FO(HSG_TAU_TABLE, 7);
@@ -1590,13 +1559,6 @@ int hsg_gat_bwd_dst_g(const hsg_rel *rel, int H, int D, int tau_mode, float slop
     }
     const int ne = ne_bucket((D + lph - 1) / lph);
     float *Gw = const_cast<float *>(G);                 // read only (GIN)
-    if (dst_pf()) {
-        if (tau_mode == HSG_TAU_TABLE)
-            return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma,
-                                                                        tau, nullptr, m, l, nullptr, Gw, dpre, dtau_part);
-        return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6, true, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma,
-                                                                       tau, nullptr, m, l, nullptr, Gw, dpre, dtau_part);
-    }
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
                                                               nullptr, m, l, nullptr, Gw, dpre, dtau_part);

@@ -1386,230 +1386,6 @@ int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------
-// k_gemm10: k_gemm7's contract (fp32 A split in-kernel, pre-split weight planes) with
-// the block's whole weight panel RESIDENT in LDS and A fed straight to registers, so
-// the K loop has no block barrier and no LDS write at all.
-//   * One 512-thread block per CU (8 waves, 2 per SIMD).  At start the block copies its
-//     BN-column panel of the limb planes, all Kp rows, into LDS ([limb][BN][Kp + 8]
-//     bf16: the 16-B row skew makes every 16-lane ds_read_b128 phase conflict-free) --
-//     126 KB for BN = 64, Kp = 320; 100 KB for BN = 32, Kp = 512.
-//   * Every wave owns a contiguous range of 16-row subtiles (the column block's rows
-//     balanced over its ngrp * 8 waves to +-1 subtile) and walks it RS subtiles at a
-//     time: the fp32 A fragments (lane = row li, k-group kb: two 16-B loads per
-//     subtile per 32-deep step) come from global memory one step ahead into registers,
-//     are split into limbs there and meet the panel's fragments in 6 MFMAs each.
-//     Waves never wait for each other, so one wave's load latency hides under the
-//     other waves' MFMAs.
-//   * The ncb column blocks of one row group are consecutive logical tiles, and
-//     xcd_tile puts them on one XCD: the A rows they all read are fetched from HBM once
-//     and shared through that XCD's L2.
-//   * Epilogue per subtile through a per-wave LDS scratch (16 x BN): float4 bias / aux
-//     loads (the next subtile's requested before this one's stores) and C stores; the
-//     column partials (colpart) are per 16-row subtile: ceil(M / 16) rows.
-// ---------------------------------------------------------------------------------
-template <int BN>
-struct Epi16 {
-    static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR, STEPS = 16 / RPS;
-    f32x4 aux[STEPS], ex[STEPS];
-    __device__ __forceinline__ void load(const GemmArgs &p, int row0, int n0, int lane) {
-        const int q = lane % QPR, rs = lane / QPR;
-        const int nc = min(n0 + 4 * q, p.N - 4);
-        if (p.epi != HSG_EPI_STORE) {
-#pragma unroll
-            for (int t = 0; t < STEPS; ++t) {
-                const int m = min(row0 + t * RPS + rs, p.M - 1);
-                aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + nc);
-            }
-        }
-        if (p.epi == HSG_EPI_ADD_ELUG) {
-#pragma unroll
-            for (int t = 0; t < STEPS; ++t) {
-                const int m = min(row0 + t * RPS + rs, p.M - 1);
-                const size_t o = (size_t)m * p.ldaux + nc;
-                ex[t] = *reinterpret_cast<const f32x4 *>(p.aux2 + o) - *reinterpret_cast<const f32x4 *>(p.aux3 + o);
-            }
-        }
-    }
-    __device__ __forceinline__ void finish(const float *wl, int row0, int n0, int lane, const GemmArgs &p,
-                                           const f32x4 bn, int sub) const {
-        __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS writes
-        __builtin_amdgcn_wave_barrier();
-        const int q = lane % QPR, rs = lane / QPR;
-        const int n = n0 + 4 * q;
-        const bool qok = n < p.N;
-        f32x4 csum = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < STEPS; ++t) {
-            const int r = t * RPS + rs, m = row0 + r;
-            if (!qok || m >= p.M) continue;
-            f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
-            if (p.epi == HSG_EPI_RELU_BWD) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
-            } else {
-                v += bn;
-                if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
-                if (p.relu) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-                }
-            }
-            *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
-            if (p.epi == HSG_EPI_ADD_ELUG) {
-                f32x4 g;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
-                *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
-            }
-            csum += v;
-        }
-        if (p.colpart) {                                    // 16-row column partials, butterfly over rs
-#pragma unroll
-            for (int o = QPR; o < 64; o <<= 1)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) csum[e] += __shfl_xor(csum[e], o);
-            if (rs == 0 && qok) *reinterpret_cast<f32x4 *>(p.colpart + (size_t)sub * p.N + n) = csum;
-        }
-    }
-};
-
-template <int BN, int RS, int PM = 0>
-__global__ __launch_bounds__(512, 1) void k_gemm10(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp,
-                                                   int ncb, int ngrp) {
-    constexpr int NW = 8, TN = BN / 16, NL = PM == 2 ? 1 : 3;
-    constexpr int LDW = BN + 4;
-    extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
-    const int KP8 = Kp + 8;
-    __bf16 *panel = reinterpret_cast<__bf16 *>(dyn_lds);
-    float *scratch = dyn_lds + (NL * BN * KP8) / 2;
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lt = xcd_tile(blockIdx.x, ncb * ngrp);
-    const int cb = lt % ncb, grp = lt / ncb;
-    const int n0 = cb * BN;
-    // the panel: NL * BN rows of Kp bf16 in 16-B pieces
-    {
-        const int pcs = Kp / 8;
-        for (int q = threadIdx.x; q < NL * BN * pcs; q += NW * 64) {
-            const int row = q / pcs, c = q - row * pcs;
-            const int limb = row / BN, n = row - limb * BN;
-            const u32x4 v = *reinterpret_cast<const u32x4 *>(planes + ((size_t)(limb * Np + n0 + n) * Kp + 8 * c));
-            *reinterpret_cast<u32x4 *>(panel + (size_t)row * KP8 + 8 * c) = v;
-        }
-    }
-    // this wave's subtile range
-    const int MS = (p.M + 15) / 16, G = ngrp * NW, gw = grp * NW + wid;
-    const int s0 = (int)((long)MS * gw / G), s1 = (int)((long)MS * (gw + 1) / G);
-    const int li = lane & 15, kb = lane >> 4;
-    const int nt = Kp / 32;
-    float *wl = scratch + wid * 16 * LDW;
-    const int c = lane & 15, rq = 4 * (lane >> 4);
-    f32x4 bn = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (p.bias) bn = *reinterpret_cast<const f32x4 *>(p.bias + min(n0 + 4 * (lane % Epi16<BN>::QPR), p.N - 4));
-    __syncthreads();                                        // the panel is in place
-    for (int sc = s0; sc < s1; sc += RS) {
-        const int ns = min(RS, s1 - sc);
-        f32x4 acc[RS][TN];
-#pragma unroll
-        for (int i = 0; i < RS; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float *arow[RS];
-#pragma unroll
-        for (int i = 0; i < RS; ++i) arow[i] = p.A + (size_t)min((sc + i) * 16 + li, p.M - 1) * p.lda + 8 * kb;
-        f32x4 ax[RS], ay[RS];
-        auto loadA = [&](int kt, f32x4 (&x)[RS], f32x4 (&y)[RS]) {
-            const int k = 32 * kt + 8 * kb;
-#pragma unroll
-            for (int i = 0; i < RS; ++i) {
-                const float *sx = k < p.K ? arow[i] + 32 * kt : g_zero16;
-                const float *sy = k + 4 < p.K ? arow[i] + 32 * kt + 4 : g_zero16;
-                x[i] = *reinterpret_cast<const f32x4 *>(sx);
-                y[i] = *reinterpret_cast<const f32x4 *>(sy);
-            }
-        };
-        loadA(0, ax, ay);
-        Epi16<BN> ep;
-        for (int kt = 0; kt < nt; ++kt) {
-            bf16x8 a[RS][3];
-#pragma unroll
-            for (int i = 0; i < RS; ++i) {
-                if constexpr (PM == 2) {
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) a[i][0][e] = (__bf16)(e < 4 ? ax[i][e] : ay[i][e - 4]);
-                } else {
-                    split_rne8(ax[i], ay[i], a[i][0], a[i][1], a[i][2]);
-                }
-            }
-            // the next step's A fragments land under this step's MFMAs (the raw
-            // registers are free once split)
-            if (kt + 1 < nt) loadA(kt + 1, ax, ay);
-            else ep.load(p, sc * 16, n0, lane);             // the first subtile's epilogue operands
-            // all TN x NL weight fragments, then the products one limb pair at a time over
-            // every (subtile, column tile) accumulator: consecutive MFMAs are independent
-            bf16x8 b[NL][TN];
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int l = 0; l < NL; ++l)
-                    b[l][j] = *reinterpret_cast<const bf16x8 *>(panel + (size_t)(l * BN + 16 * j + li) * KP8 + 32 * kt + 8 * kb);
-            constexpr int NP = PM == 2 ? 1 : 6;
-            constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};   // small products first
-#pragma unroll
-            for (int pp = 0; pp < NP; ++pp)
-#pragma unroll
-                for (int i = 0; i < RS; ++i) {
-                    if (i >= ns) continue;                  // wave-uniform: the short last chunk
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][PM == 2 ? 0 : PA[pp]],
-                                                                            b[PM == 2 ? 0 : PB[pp]][j], acc[i][j], 0, 0, 0);
-                }
-        }
-        // epilogue, subtile by subtile through the wave's scratch
-#pragma unroll
-        for (int i = 0; i < RS; ++i) {
-            if (i >= ns) continue;
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) wl[(rq + e) * LDW + 16 * j + c] = acc[i][j][e];
-            Epi16<BN> cur = ep;
-            if (i + 1 < ns) ep.load(p, (sc + i + 1) * 16, n0, lane);
-            cur.finish(wl, (sc + i) * 16, n0, lane, p, bn, sc + i);
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();                // the scratch is read before it is rewritten
-        }
-    }
-}
-
-template <int BN, int RS, int PM = 0>
-int launch10(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
-    constexpr int NL = PM == 2 ? 1 : 3;
-    p.splits = 1;
-    p.k_tiles_per_split = Kp / 32;
-    const int ncb = (p.N + BN - 1) / BN;
-    if (ncb * BN > Np) return HSG_EINVAL;                  // panel rows must exist in the planes
-    if (!epi_rows_ok(p)) return HSG_EINVAL;
-    const size_t lds = (size_t)NL * BN * (Kp + 8) * 2 + (size_t)8 * 16 * (BN + 4) * 4;
-    if (lds > 160 * 1024) return HSG_EINVAL;
-    static bool attr = false;
-    if (!attr) {
-        hipFuncSetAttribute(reinterpret_cast<const void *>(&k_gemm10<BN, RS, PM>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr = true;
-    }
-    int ngrp = 256 / ncb;
-    const int ms = (p.M + 15) / 16;
-    if (ngrp * 8 > ms) ngrp = (ms + 7) / 8;
-    if (ngrp < 1) ngrp = 1;
-    hipLaunchKernelGGL((k_gemm10<BN, RS, PM>), dim3((unsigned)(ncb * ngrp)), dim3(512), lds, st, p, planes, Np, Kp,
-                       ncb, ngrp);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
-}
-
-// ---------------------------------------------------------------------------------
 // k_gemm6: k_gemm5's contract (fp32 A, pre-split weight planes) with A never staged
 // through LDS: each wave owns 32 A rows that no other wave reads, so every lane loads
 // its own fragment (row li, 8 consecutive k per 16-k step: 2 x dwordx4) straight
@@ -2108,24 +1884,19 @@ __device__ __forceinline__ void slab_reduce_job(const RedJobs &j, int q, int blk
             const float *P = j.seg[q][sg] + coff + c;
             const int rows = j.rows[q][sg], per = (rows + orows - 1) / orows;
             const int r1 = min(rows, (ob + 1) * per);
-            int r = ob * per + g;
-            // 16 rows in flight per thread (long segments: the hproj dW slabs are ~300
-            // rows deep), added into the four partial sums in row order
-            for (; r + 120 < r1; r += 128) {
+            // up to 16 rows in flight per thread, ALL requested before any is added: rows
+            // past the range load a clamped (valid) row and add 0, so a segment of <= 128
+            // rows is one round trip (the ragged 4-row / 1-row tail loops made the 100-row
+            // head-projection segments ~4 dependent round trips each); rows go into the
+            // four partial sums in row order
+            for (int r = ob * per + g; r < r1; r += 128) {
                 vec_t v[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)(r + 8 * u) * pitch);
+                for (int u = 0; u < 16; ++u)
+                    v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)min(r + 8 * u, r1 - 1) * pitch);
 #pragma unroll
-                for (int u = 0; u < 16; ++u) s[u & 3] += v[u];
+                for (int u = 0; u < 16; ++u) s[u & 3] += r + 8 * u < r1 ? v[u] : vec_t(0.f);
             }
-            for (; r + 24 < r1; r += 32) {
-                vec_t v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)(r + 8 * u) * pitch);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) s[u] += v[u];
-            }
-            for (; r < r1; r += 8) s[0] += *reinterpret_cast<const vec_t *>(P + (size_t)r * pitch);
         }
     }
     const vec_t t = (s[0] + s[1]) + (s[2] + s[3]);
@@ -2263,9 +2034,6 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 36 && epi_rows_ok(p)) return launch7<64, 2, 6>(p, pl, Np, Kp, st);   // dev: loads only
     if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
     if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
-    if (plan == 40 && epi_rows_ok(p)) return N > 320 ? launch10<64, 4>(p, pl, Np, Kp, st) : launch10<32, 4>(p, pl, Np, Kp, st);
-    if (plan == 42 && epi_rows_ok(p)) return N > 320 ? launch10<64, 3>(p, pl, Np, Kp, st) : launch10<32, 4>(p, pl, Np, Kp, st);
-    if (plan == 43 && epi_rows_ok(p)) return N > 320 ? launch10<64, 2>(p, pl, Np, Kp, st) : launch10<32, 4>(p, pl, Np, Kp, st);
     return launch5<64, 2>(p, pl, Np, Kp, st);
 }
 

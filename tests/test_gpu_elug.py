@@ -42,13 +42,10 @@ def test_psw_elug_declines_unaligned():
     assert not gemm_psw_elug(torch.randn(50, 64, device="cuda"), S, t.clone(), t, t, torch.empty_like(t))
 
 
-@pytest.mark.parametrize("pf", ["0", "1"])
-def test_dst_pass_with_given_G_equals_noh_pass(monkeypatch, pf):
+def test_dst_pass_with_given_G_equals_noh_pass():
     """hsg_gat_bwd_dst_g with the G rows hsg_gat_bwd_dst_noh wrote: bitwise the same
-    dpre and d tau partials (the same kernel body, G read instead of made), with and
-    without the next-destination prefetch (HSG_GAT_DST_PF)."""
+    dpre and d tau partials (the same kernel body, G read instead of made)."""
     import ctypes
-    monkeypatch.setenv("HSG_GAT_DST_PF", pf)
     from hetersumgraph_amd import graph as hg
     from hetersumgraph_amd import synth
     from hetersumgraph_amd._lib import HSG_TAU_TABLE, load, ptr
