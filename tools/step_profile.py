@@ -98,6 +98,13 @@ def parse(path, replays=REPLAYS):
           f"gaps {span - busy:.1f} us/step")
     for k in sorted(tot, key=lambda k: -tot[k]):
         print(f"{tot[k] / replays:9.1f} us  {cnt[k] / replays:5.1f}x  {tot[k] / cnt[k]:8.2f} us/launch  {k}")
+    # the step in launch order: mean time of each position (tells the W2S and S2W
+    # launches of one kernel apart) and its grid size
+    print("\nlaunch order (mean us per position, grid):")
+    for i in range(per):
+        ds = [(int(tail[j]["End_Timestamp"]) - int(tail[j]["Start_Timestamp"])) / 1e3 for j in range(i, len(tail), per)]
+        g = tail[i].get("Grid_Size", tail[i].get("Grid_Size_X", "?"))
+        print(f"  {i:3d} {sum(ds) / len(ds):8.2f} us  grid {g:>8}  {short(tail[i]['Kernel_Name'])}")
 
 
 if __name__ == "__main__":
