@@ -509,9 +509,7 @@ struct Stage3 {
 // grid (2,560 blocks at cfg2) runs in exactly two rounds of resident blocks instead of
 // 2.5 at 4 per CU
 template <int BM, int BN, bool AK, bool BKC, int BK, int PF, int NL, int IGLP = -1, int NT = 256>
-__global__ __launch_bounds__(NT, NT == 256   ? (BM * BN == 64 * 64 && !AK && !BKC ? 5 : 2)
-                                 : NT == 128 ? (BM * BN == 64 * 64 ? 8 : 4)
-                                             : 1) void k_gemm3(GemmArgs p) {
+__global__ __launch_bounds__(NT, NT == 256 ? (BM * BN == 64 * 64 && !AK && !BKC ? 5 : 2) : 1) void k_gemm3(GemmArgs p) {
     constexpr int WGN = NT / 128;                          // waves along N (2 along M)
     constexpr int WM = BM / 2, WN = BN / WGN;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -1775,10 +1773,6 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
             if (t3 == 1) rc = launch3<128, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
             else if (t3 == 3) rc = launch3<128, 128, 32, 1, 3, 0>(p, ak, bk, splits, st);
             else rc = launch3<64, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
-        } else if (var == 7) {                              // 2 waves along M: 32 x 64 wave tiles
-            rc = launch3<64, 64, 32, 1, 3, 0, 128>(p, ak, bk, splits, st);
-        } else if (var == 8) {                              // 2 waves along M: 64 x 64 wave tiles
-            rc = launch3<128, 64, 32, 1, 3, 0, 128>(p, ak, bk, splits, st);
         } else if (var == 6) {                              // 8 waves (2 x 4), iglp_opt(0)
             if (t3 == 1) rc = launch3<64, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
             else if (t3 == 3) rc = launch3<128, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
