@@ -169,3 +169,50 @@ def test_flat_gradients_detects_one_buffer():
     assert torch.equal(p.grad, torch.tensor([0.0, 2.0, 4.0])) and q.grad[1, 1].item() == 12.0
     q.grad = q.grad.clone()                          # another buffer: no single flat view
     assert flat_gradients([p, q]) is None
+
+
+def test_cfg3_global_batch_shards_over_eight_ranks():
+    """BASELINE configs[2] (cfg3: 256 CNN/DM-shaped docs data-parallel over 8 GPUs,
+    train.py:130-135 batching): bench.make_shard's document split gives every rank 32
+    whole documents, each document exactly once, edge loads within one document of
+    each other, and doc-weight fractions that sum to 1."""
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.parallel import shard_fraction, shard_owners
+    world = 8
+    docs = synth.make_batch_docs("cfg3", seed=0, n_docs=synth.CONFIGS["cfg3"][1] * world)
+    owner = shard_owners(docs, world)
+    counts = [owner.count(r) for r in range(world)]
+    assert counts == [32] * world
+    loads = [sum(len(d.src) for d, o in zip(docs, owner) if o == r) for r in range(world)]
+    assert max(loads) - min(loads) <= max(len(d.src) for d in docs)
+    fr = [shard_fraction(docs, r, world) for r in range(world)]
+    assert abs(sum(fr) - 1.0) < 1e-12 and all(abs(f - 1 / 8) < 1e-12 for f in fr)
+
+
+def _flat_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from hetersumgraph_amd.parallel import allreduce_gradients
+        # two parameters whose gradients are views of ONE flat buffer (the fused
+        # stack's layout), rank-dependent values, uneven doc weights
+        p, q = torch.nn.Parameter(torch.zeros(5, dtype=torch.float64)), torch.nn.Parameter(
+            torch.zeros(2, 3, dtype=torch.float64))
+        flat = torch.arange(11, dtype=torch.float64) * (rank + 1)
+        p.grad, q.grad = flat[:5], flat[5:].view(2, 3)
+        w = [(r + 1) / sum(range(1, world + 1)) for r in range(world)]
+        allreduce_gradients([p, q], scale=w[rank], bucket_bytes=1 << 30)
+        want = torch.arange(11, dtype=torch.float64) * sum(wr * (r + 1) for r, wr in enumerate(w))
+        assert torch.allclose(torch.cat([p.grad, q.grad.reshape(-1)]), want, rtol=0, atol=1e-12)
+        assert p.grad.untyped_storage().data_ptr() == flat.untyped_storage().data_ptr()   # reduced in place
+    finally:
+        dist.destroy_process_group()
+
+
+def test_flat_doc_weighted_allreduce_world8():
+    """The bench's DP exchange (one in-place doc-weighted all-reduce of the flat
+    gradient buffer, bench.py allreduce) at world size 8 -- the rank count of the
+    cfg3 / SCALE runs -- rehearsed on gloo: sum_r w_r g_r on every rank."""
+    world = 8
+    mp.spawn(_flat_worker, args=(world, _free_port()), nprocs=world, join=True)
