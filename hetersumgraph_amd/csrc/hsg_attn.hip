@@ -56,17 +56,15 @@ __device__ void head_v(int k, int D, int F, const float *__restrict__ attn, cons
 
 // one workgroup per head k: v_k (W_f,k staged in LDS), then tau[:, k]; block 0
 // also writes the contiguous a1 copy
-__global__ __launch_bounds__(256) void k_attn_params_fwd(int H, int D, int F, const float *__restrict__ attn,
-                                                         const float *__restrict__ wf,
-                                                         const float *__restrict__ bf,
-                                                         const float *__restrict__ T, float *__restrict__ a1,
-                                                         float *__restrict__ tau) {
+__device__ __forceinline__ void attn_fwd_head(int k, int H, int D, int F, const float *__restrict__ attn,
+                                              const float *__restrict__ wf, const float *__restrict__ bf,
+                                              const float *__restrict__ T, float *__restrict__ a1,
+                                              float *__restrict__ tau) {
     __shared__ float wlds[kWfLds];
     __shared__ float a3s[kDMax];
     __shared__ float v[kFMax];
     __shared__ float part[kNT][33];
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int k = blockIdx.x;
     if (k == 0)
         for (int i = tid; i < H * D; i += nt) {
             const int kk = i / D, d = i - (i / D) * D;
@@ -89,6 +87,28 @@ __global__ __launch_bounds__(256) void k_attn_params_fwd(int H, int D, int F, co
         for (int q = 0; q < 32; ++q) s += part[tid][q];
         tau[tid * H + k] = s;
     }
+}
+
+__global__ __launch_bounds__(256) void k_attn_params_fwd(int H, int D, int F, const float *__restrict__ attn,
+                                                         const float *__restrict__ wf,
+                                                         const float *__restrict__ bf,
+                                                         const float *__restrict__ T, float *__restrict__ a1,
+                                                         float *__restrict__ tau) {
+    attn_fwd_head(blockIdx.x, H, D, F, attn, wf, bf, T, a1, tau);
+}
+
+// the tables of two layers (the stack's W2S and S2W, sharing T) in one launch:
+// blocks [0, H0) are layer 0's heads, [H0, H0 + H1) layer 1's
+struct AttnFwdPair {
+    int H[2], D[2];
+    const float *attn[2], *wf[2], *bf[2];
+    float *a1[2], *tau[2];
+};
+
+__global__ __launch_bounds__(256) void k_attn_params_fwd_pair(AttnFwdPair j, int F, const float *__restrict__ T) {
+    const int q = (int)blockIdx.x >= j.H[0] ? 1 : 0;
+    const int k = (int)blockIdx.x - (q ? j.H[0] : 0);
+    attn_fwd_head(k, j.H[q], j.D[q], F, j.attn[q], j.wf[q], j.bf[q], T, j.a1[q], j.tau[q]);
 }
 
 // Stage 1 of the partial-slab reduction: blockIdx.y picks the slab (0: d tau
@@ -222,6 +242,17 @@ int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf,
     if (!dims_ok(H, D, F) || !attn || !wf || !T || !a1 || !tau) return HSG_EINVAL;
     hipLaunchKernelGGL(k_attn_params_fwd, dim3(H), dim3(256), 0, (hipStream_t)stream, H, D, F, attn, wf, bf, T,
                        a1, tau);
+    return status();
+}
+
+int hsg_attn_params_fwd_pair(int H0, int D0, const float *attn0, const float *wf0, const float *bf0, float *a1_0,
+                             float *tau0, int H1, int D1, const float *attn1, const float *wf1, const float *bf1,
+                             float *a1_1, float *tau1, int F, const float *T, void *stream) {
+    if (!dims_ok(H0, D0, F) || !dims_ok(H1, D1, F) || !attn0 || !wf0 || !a1_0 || !tau0 || !attn1 || !wf1 || !a1_1 ||
+        !tau1 || !T)
+        return HSG_EINVAL;
+    AttnFwdPair j{{H0, H1}, {D0, D1}, {attn0, attn1}, {wf0, wf1}, {bf0, bf1}, {a1_0, a1_1}, {tau0, tau1}};
+    hipLaunchKernelGGL(k_attn_params_fwd_pair, dim3(H0 + H1), dim3(256), 0, (hipStream_t)stream, j, F, T);
     return status();
 }
 

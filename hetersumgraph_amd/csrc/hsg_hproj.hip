@@ -142,6 +142,11 @@ struct DropJobs {
     uint32_t *bits[8];
     int start[9];
     int njobs;
+    // optional: the narrow-head projection's weight transpose (hsg_hproj_wt) in the
+    // blocks after the masks' (W == nullptr: none)
+    const float *W;
+    float *Wt;
+    int wH, wD, wIn;
 };
 
 // The step's dropout seed: seed += 1 and the backward-stable snapshot of the new value
@@ -154,7 +159,20 @@ __global__ __launch_bounds__(64) void k_seed_advance(int64_t *seed, int64_t *sna
     }
 }
 
+__device__ __forceinline__ void hproj_wt_block(int k, int c0, int D, int in, const float *__restrict__ W,
+                                               float *__restrict__ Wt) {
+    for (int e = threadIdx.x; e < 64 * D; e += 256) {
+        const int d = e >> 6, c = c0 + (e & 63);
+        if (c < in) Wt[((size_t)k * in + c) * D + d] = W[((size_t)k * D + d) * in + c];
+    }
+}
+
 __global__ __launch_bounds__(256) void k_dropmask_multi(DropJobs j, const int64_t *seedp) {
+    if ((int)blockIdx.x >= j.start[j.njobs]) {          // the weight-transpose blocks
+        const int b = (int)blockIdx.x - j.start[j.njobs], nct = (j.wIn + 63) / 64;
+        hproj_wt_block(b / nct, (b % nct) * 64, j.wD, j.wIn, j.W, j.Wt);
+        return;
+    }
     int q = 0;
     while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
     const long t = (long)((int)blockIdx.x - j.start[q]) * 256 + threadIdx.x;
@@ -327,11 +345,7 @@ __global__ __launch_bounds__(256) void k_hproj_fwd(int n, int in, int H, int D, 
 // coalesced along c, 32-bit index arithmetic only.
 __global__ __launch_bounds__(256) void k_hproj_wt(int H, int D, int in, const float *__restrict__ W,
                                                   float *__restrict__ Wt) {
-    const int k = blockIdx.y, c0 = blockIdx.x * 64;
-    for (int e = threadIdx.x; e < 64 * D; e += 256) {
-        const int d = e >> 6, c = c0 + (e & 63);
-        if (c < in) Wt[((size_t)k * in + c) * D + d] = W[((size_t)k * D + d) * in + c];
-    }
+    hproj_wt_block(blockIdx.y, blockIdx.x * 64, D, in, W, Wt);
 }
 
 template <int HB, int KS>
@@ -955,8 +969,20 @@ int hsg_seed_advance(int64_t *seed, int64_t *snap, void *stream) {
 
 int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
                        const uint32_t *offset, uint32_t *const *bits, void *stream) {
+    return hsg_dropmask_multi_wt(njobs, n, in, H, p, seed, offset, bits, 0, 0, 0, nullptr, nullptr, stream);
+}
+
+int hsg_dropmask_multi_wt(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
+                          const uint32_t *offset, uint32_t *const *bits, int wH, int wD, int wIn, const float *W,
+                          float *Wt, void *stream) {
     if (njobs < 1 || njobs > 8 || !seed) return HSG_EINVAL;
+    if (W && (wH < 1 || wD < 1 || wIn < 1 || !Wt)) return HSG_EINVAL;
     DropJobs j{};
+    j.W = W;
+    j.Wt = Wt;
+    j.wH = wH;
+    j.wD = wD;
+    j.wIn = wIn;
     j.njobs = njobs;
     j.start[0] = 0;
     for (int q = 0; q < njobs; ++q) {
@@ -966,8 +992,9 @@ int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, con
         const long total = (long)((H[q] + 1) / 2) * ((n[q] + 31) / 32) * mask_ldc(in[q]);
         j.start[q + 1] = j.start[q] + (int)((total + 255) / 256);
     }
-    if (j.start[njobs] == 0) return 0;
-    hipLaunchKernelGGL(k_dropmask_multi, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j, seed);
+    const int wblocks = W ? (wIn + 63) / 64 * wH : 0;
+    if (j.start[njobs] + wblocks == 0) return 0;
+    hipLaunchKernelGGL(k_dropmask_multi, dim3(j.start[njobs] + wblocks), dim3(256), 0, (hipStream_t)stream, j, seed);
     return status();
 }
 

@@ -22,13 +22,15 @@ import ctypes
 from ._lib import check, load, ptr, stream_of
 
 
-def dropmasks(jobs, device, stream_of_t):
+def dropmasks(jobs, device, stream_of_t, wt=None):
     """Keep-mask bits of several head projections in ONE launch
     (hsg_dropmask_multi): ``jobs`` = [(n, d_in, H, p, seed_t, offset)] with one
-    shared seed tensor; returns the bit tensors, each as hsg_dropmask would draw it."""
+    shared seed tensor; returns the bit tensors, each as hsg_dropmask would draw it.
+    ``wt`` = (W, H, D): the same launch also writes :func:`transposed_weight` of W
+    (hsg_dropmask_multi_wt), returned as ``(masks, Wt)``."""
     lib = load()
     if not jobs:
-        return []
+        return ([], transposed_weight(*wt)) if wt is not None else []
     if len({id(j[4]) for j in jobs}) != 1:
         raise ValueError("dropmasks: one seed tensor per batch")
     out = []
@@ -39,15 +41,22 @@ def dropmasks(jobs, device, stream_of_t):
         b = torch.empty(lib.hsg_dropmask_words(n, d_in, H), dtype=torch.int32, device=device)
         out.append(b)
         ns[q], ins[q], hs[q], ps[q], offs[q], bp[q] = n, d_in, H, float(p), off, b.data_ptr()
+    Wt = None
+    if wt is not None:
+        W, H, D = wt
+        W = W.contiguous()
+        Wt = torch.empty(H * W.shape[1] * D, dtype=W.dtype, device=W.device)
     for q0 in range(0, k, 8):
         q1 = min(k, q0 + 8)
         sl = slice(q0, q1)
         m = q1 - q0
-        check(lib.hsg_dropmask_multi(m, (ctypes.c_int * m)(*ns[sl]), (ctypes.c_int * m)(*ins[sl]),
-                                     (ctypes.c_int * m)(*hs[sl]), (ctypes.c_float * m)(*ps[sl]),
-                                     ptr(jobs[0][4]), (ctypes.c_uint32 * m)(*offs[sl]),
-                                     (ctypes.c_void_p * m)(*bp[sl]), stream_of_t), "hsg_dropmask_multi")
-    return out
+        w_args = (H, D, W.shape[1], ptr(W), ptr(Wt)) if (wt is not None and q0 == 0) else (0, 0, 0, None, None)
+        check(lib.hsg_dropmask_multi_wt(m, (ctypes.c_int * m)(*ns[sl]), (ctypes.c_int * m)(*ins[sl]),
+                                        (ctypes.c_int * m)(*hs[sl]), (ctypes.c_float * m)(*ps[sl]),
+                                        ptr(jobs[0][4]), (ctypes.c_uint32 * m)(*offs[sl]),
+                                        (ctypes.c_void_p * m)(*bp[sl]), *w_args, stream_of_t),
+              "hsg_dropmask_multi_wt")
+    return (out, Wt) if wt is not None else out
 
 
 def narrow_heads(d_in, H, D):

@@ -124,6 +124,21 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
+def attn_tables_pair(lay0, lay1, T):
+    """:func:`attn_tables` of two layers sharing T in ONE launch
+    (hsg_attn_params_fwd_pair): [(a1, tau) of lay0, (a1, tau) of lay1]; a layer is any
+    object with attn / wf / bf / H / D."""
+    lib = load()
+    outs = []
+    for lay in (lay0, lay1):
+        outs.append((lay.attn.new_empty(lay.H, lay.D), lay.attn.new_empty(N_BOX + 1, lay.H)))
+    (a0, t0), (a1, t1) = outs
+    check(lib.hsg_attn_params_fwd_pair(lay0.H, lay0.D, ptr(lay0.attn), ptr(lay0.wf), ptr(lay0.bf), ptr(a0), ptr(t0),
+                                       lay1.H, lay1.D, ptr(lay1.attn), ptr(lay1.wf), ptr(lay1.bf), ptr(a1), ptr(t1),
+                                       T.shape[1], ptr(T), stream_of(T)), "hsg_attn_params_fwd_pair")
+    return outs
+
+
 def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out=None, sigma=None, keep_h=True,
                   no_h=False):
     """Forward of one multi-head application with the TF-IDF-table edge term:

@@ -40,8 +40,8 @@ from .dense import gemm, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
-from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, gat_table_bwd,
-                  gat_table_fwd)
+from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, attn_tables_pair,
+                  gat_table_bwd, gat_table_fwd)
 
 
 class _Grads:
@@ -239,7 +239,15 @@ class _GatStack(torch.autograd.Function):
             draws.append([hm, fr])
         jobs = [(rel.n_src, lay.W.shape[1], lay.H, lay.p_attn, d[0][0], d[0][1])
                 for (lay, rel), d in zip(seq, draws) if d[0] is not None]
-        masks = iter(dropmasks(jobs, w0.device, stream_of(w0)))
+        # the narrow-head (VALU) projection's transposed weight comes out of the same
+        # launch as the masks (hsg_dropmask_multi_wt; HSG_WT_FOLD=0: its own launch)
+        narrow = [lay for lay in (w2s, s2w) if lay.p_attn > 0 and narrow_heads(lay.W.shape[1], lay.H, lay.D)]
+        fold = narrow[0] if narrow and jobs and os.environ.get("HSG_WT_FOLD", "1") != "0" else None
+        if fold is not None:
+            mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0), wt=(fold.W, fold.H, fold.D))
+        else:
+            mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0)), None
+        masks = iter(mlist)
         for d in draws:
             if d[0] is not None:
                 d[0] = next(masks)
@@ -264,10 +272,13 @@ class _GatStack(torch.autograd.Function):
             apps.append((lay, saved, nb, org, a))
 
         # the attention tables depend on the parameters only: once per layer
-        tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
+        if os.environ.get("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
+            tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T)))
+        else:
+            tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
         # likewise the transposed head weights of a narrow-head (VALU) projection
-        wts = {id(lay): (transposed_weight(lay.W, lay.H, lay.D)
-                         if lay.p_attn > 0 and narrow_heads(lay.W.shape[1], lay.H, lay.D) else None)
+        wts = {id(lay): ((wt_fold if lay is fold else transposed_weight(lay.W, lay.H, lay.D))
+                         if any(lay is q for q in narrow) else None)
                for lay in (w2s, s2w)}
         run(w2s, rw, ("w", 0), ("s", 0), ("s", 1))
         for i in range(n_iter):

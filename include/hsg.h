@@ -145,6 +145,14 @@ int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, fl
  *      H <= 16, H*D <= 512, F <= 256. */
 int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf, const float *bf,
                         const float *T, float *a1, float *tau, void *stream);
+
+/* The attention tables of TWO layers sharing the TF-IDF table T (the fused stack's
+ * W2S and S2W, once per forward) in one launch: for each layer exactly what
+ * hsg_attn_params_fwd writes (a1 [H, D], tau [11, H]).  Replaces the two per-layer
+ * launches of the same GATLayer.py:84-93 / 123-131 edge-type term. */
+int hsg_attn_params_fwd_pair(int H0, int D0, const float *attn0, const float *wf0, const float *bf0, float *a1_0,
+                             float *tau0, int H1, int D1, const float *attn1, const float *wf1, const float *bf1,
+                             float *a1_1, float *tau1, int F, const float *T, void *stream);
 int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_part, int n_da1_part,
                         const float *da1_part, const float *attn, const float *wf, const float *bf,
                         const float *T, float *dattn, float *dwf, float *dbf, float *dT, float *workspace,
@@ -340,6 +348,15 @@ int hsg_seed_advance(int64_t *seed, int64_t *snap, void *stream);
  * the masks of all its head projections up front. */
 int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, const float *p,
                        const int64_t *seed, const uint32_t *offset, uint32_t *const *bits, void *stream);
+
+/* hsg_dropmask_multi plus, in the same launch, the narrow-head projection's weight
+ * transpose Wt[k][c][d] = W[k*wD+d][c] of hsg_hproj_wt (H = wH, D = wD, in = wIn;
+ * W == NULL: masks only).  Both depend on the step's seed / the parameters only,
+ * so the fused stack draws its keep-masks and transposes W2S's weight in one
+ * launch (GATStackLayer.py:56 dropout, GATLayer.py:110 fc). */
+int hsg_dropmask_multi_wt(int njobs, const int *n, const int *in, const int *H, const float *p,
+                          const int64_t *seed, const uint32_t *offset, uint32_t *const *bits, int wH, int wD,
+                          int wIn, const float *W, float *Wt, void *stream);
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                   const uint32_t *bits, float p, float *Z, int ldz, void *stream);
 /* hsg_hproj_fwd plus the attention's source logits sigma[i][k] = <Z[i, kD:(k+1)D], a1[k]>

@@ -245,3 +245,36 @@ def test_src_pass_head_lane_variant(monkeypatch, hl, H, n_src, max_deg, per_edge
     for name, got, want in zip(("Z", "a1", "tau", "origin"), dl, leaves):
         scale = want.grad.abs().max().item() + 1e-6
         assert err(got.grad, want.grad) <= 2e-5 * max(1.0, scale), (name, err(got.grad, want.grad), scale)
+
+
+def test_attn_tables_pair_equals_per_layer():
+    """hsg_attn_params_fwd_pair (both layers' tables in one launch, the fused stack's
+    forward) writes bitwise what two hsg_attn_params_fwd launches write (W2S-like
+    layer without feat_fc bias, S2W-like layer with it)."""
+    from types import SimpleNamespace
+    from hetersumgraph_amd.ops import attn_tables, attn_tables_pair
+    torch.manual_seed(5)
+    dev = "cuda"
+    T = torch.randn(10, 50, device=dev)
+    l0 = SimpleNamespace(H=8, D=8, attn=torch.randn(8, 24, device=dev), wf=torch.randn(8, 8, 50, device=dev), bf=None)
+    l1 = SimpleNamespace(H=6, D=50, attn=torch.randn(6, 150, device=dev), wf=torch.randn(6, 50, 50, device=dev),
+                         bf=torch.randn(6, 50, device=dev))
+    got = attn_tables_pair(l0, l1, T)
+    for lay, (a1, tau) in zip((l0, l1), got):
+        ra1, rtau = attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D)
+        assert torch.equal(a1, ra1) and torch.equal(tau, rtau)
+
+
+def test_dropmasks_with_weight_transpose():
+    """hsg_dropmask_multi_wt: the masks are bitwise those of hsg_dropmask_multi and the
+    folded weight transpose equals hsg_hproj_wt's."""
+    from hetersumgraph_amd.hproj import dropmasks, transposed_weight
+    dev = torch.device("cuda")
+    seed = torch.tensor([1234], dtype=torch.int64, device=dev)
+    jobs = [(19200, 300, 8, 0.1, seed, 3), (1120, 64, 6, 0.1, seed, 7), (777, 300, 8, 0.1, seed, 11)]
+    W = torch.randn(64, 300, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ref = dropmasks(jobs, dev, st)
+    got, Wt = dropmasks(jobs, dev, st, wt=(W, 8, 8))
+    assert all(torch.equal(a, b) for a, b in zip(ref, got))
+    assert torch.equal(Wt, transposed_weight(W, 8, 8))
