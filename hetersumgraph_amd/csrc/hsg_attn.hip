@@ -141,50 +141,49 @@ __global__ __launch_bounds__(256) void k_colsum_stage(int rows0, int cols0, cons
 }
 
 // blocks 0..H-1: one head each (d attn row, dW_f,k, db_f,k); block H: dT
-__global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
-                                                         const float *__restrict__ dtau_st,   // [kStage][11*H]
-                                                         const float *__restrict__ da1_st,    // [kStage][H*D]
-                                                         const float *__restrict__ attn,
-                                                         const float *__restrict__ wf,
-                                                         const float *__restrict__ bf,
-                                                         const float *__restrict__ T, float *__restrict__ dattn,
-                                                         float *__restrict__ dwf, float *__restrict__ dbf,
-                                                         float *__restrict__ dT, int accumulate, int srows) {
-    __shared__ float wlds[kWfLds];
-    __shared__ float a3s[kDMax];
-    __shared__ float dv[kFMax];
-    __shared__ float dtau[kNT * kHMax];
-    const int tid = threadIdx.x, nt = blockDim.x;
+// d tau [11][H] of one layer, summed over the stage rows in order, into LDS
+__device__ __forceinline__ void attn_bwd_dtau(int H, const float *__restrict__ dtau_st, int srows, float *dtau) {
     const int NTH = kNT * H;
-    // d tau [11][H], summed over the stage rows in order
-    for (int i = tid; i < NTH; i += nt) {
+    for (int i = threadIdx.x; i < NTH; i += blockDim.x) {
         float s = 0.f;
 #pragma unroll 16
         for (int r = 0; r < srows; ++r) s += dtau_st[r * NTH + i];
         dtau[i] = s;
     }
-    __syncthreads();
-    const int k = blockIdx.x;
-    if (k == H) {                                  // dT[t][f] = sum_k dtau[t][k] v_k[f]
-        float *vall = wlds;                        // [H][F] (H*F <= 16*256 <= kWfLds)
-        for (int i = tid; i < H * F; i += nt) {
-            const int kk = i / F, f = i - (i / F) * F;
-            const float *wk = wf + (size_t)kk * D * F;
-            float s = 0.f;
+}
+
+// the dT block's contribution of one layer: dT[t][f] (+)= sum_k dtau[t][k] v_k[f]
+// (vall: LDS scratch [H][F])
+__device__ __forceinline__ void attn_bwd_dT(int H, int D, int F, const float *dtau, const float *__restrict__ attn,
+                                            const float *__restrict__ wf, float *vall, float *__restrict__ dT,
+                                            bool acc) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    __syncthreads();                               // vall may hold the previous layer's v
+    for (int i = tid; i < H * F; i += nt) {
+        const int kk = i / F, f = i - (i / F) * F;
+        const float *wk = wf + (size_t)kk * D * F;
+        float s = 0.f;
 #pragma unroll 8
-            for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
-            vall[i] = s;
-        }
-        __syncthreads();
-        for (int i = tid; i < (kNT - 1) * F; i += nt) {
-            const int t = i / F, f = i - (i / F) * F;
-            float s = 0.f;
-            for (int kk = 0; kk < H; ++kk) s = fmaf(dtau[t * H + kk], vall[kk * F + f], s);
-            dT[i] = (accumulate & 2) ? dT[i] + s : s;
-        }
-        return;
+        for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
+        vall[i] = s;
     }
-    // head k
+    __syncthreads();
+    for (int i = tid; i < (kNT - 1) * F; i += nt) {
+        const int t = i / F, f = i - (i / F) * F;
+        float s = 0.f;
+        for (int kk = 0; kk < H; ++kk) s = fmaf(dtau[t * H + kk], vall[kk * F + f], s);
+        dT[i] = acc ? dT[i] + s : s;
+    }
+}
+
+// head k of one layer: da1 (stage rows), da3, dWf, dbf
+__device__ __forceinline__ void attn_bwd_head(int k, int H, int D, int F, const float *dtau,
+                                              const float *__restrict__ da1_st, const float *__restrict__ attn,
+                                              const float *__restrict__ wf, const float *__restrict__ bf,
+                                              const float *__restrict__ T, float *__restrict__ dattn,
+                                              float *__restrict__ dwf, float *__restrict__ dbf, int accumulate,
+                                              int srows, float *wlds, float *a3s, float *dv) {
+    const int tid = threadIdx.x, nt = blockDim.x;
     const float *wk = wf + (size_t)k * D * F;
     const bool staged = D * F <= kWfLds;
     if (staged)
@@ -224,6 +223,62 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
         const float g = a3s[d] * dv[f];
         dwf[(size_t)k * D * F + i] = (accumulate & 1) ? dwf[(size_t)k * D * F + i] + g : g;
     }
+}
+
+__global__ __launch_bounds__(256) void k_attn_params_bwd(int H, int D, int F,
+                                                         const float *__restrict__ dtau_st,   // [kStage][11*H]
+                                                         const float *__restrict__ da1_st,    // [kStage][H*D]
+                                                         const float *__restrict__ attn,
+                                                         const float *__restrict__ wf,
+                                                         const float *__restrict__ bf,
+                                                         const float *__restrict__ T, float *__restrict__ dattn,
+                                                         float *__restrict__ dwf, float *__restrict__ dbf,
+                                                         float *__restrict__ dT, int accumulate, int srows) {
+    __shared__ float wlds[kWfLds];
+    __shared__ float a3s[kDMax];
+    __shared__ float dv[kFMax];
+    __shared__ float dtau[kNT * kHMax];
+    attn_bwd_dtau(H, dtau_st, srows, dtau);
+    __syncthreads();
+    const int k = blockIdx.x;
+    if (k == H) {                                  // dT[t][f] = sum_k dtau[t][k] v_k[f]
+        attn_bwd_dT(H, D, F, dtau, attn, wf, wlds, dT, (accumulate & 2) != 0);
+        return;
+    }
+    attn_bwd_head(k, H, D, F, dtau, da1_st, attn, wf, bf, T, dattn, dwf, dbf, accumulate, srows, wlds, a3s, dv);
+}
+
+// hsg_attn_params_finish of two layers sharing T in one launch: blocks [0, H0) and
+// [H0, H0 + H1) are the layers' heads, the last block adds both layers' dT terms in
+// layer order (layer 0's update of each element, then layer 1's: the same result as
+// the two launches in that order, also when both write the same dT)
+struct AttnBwdPair {
+    int H[2], D[2], acc[2];
+    const float *ws[2], *attn[2], *wf[2], *bf[2];
+    float *dattn[2], *dwf[2], *dbf[2], *dT[2];
+};
+
+__global__ __launch_bounds__(256) void k_attn_params_bwd_pair(AttnBwdPair j, int F, const float *__restrict__ T,
+                                                              int srows) {
+    __shared__ float wlds[kWfLds];
+    __shared__ float a3s[kDMax];
+    __shared__ float dv[kFMax];
+    __shared__ float dtau[2][kNT * kHMax];
+    const int b = blockIdx.x;
+    if (b == j.H[0] + j.H[1]) {                    // dT
+        attn_bwd_dtau(j.H[0], j.ws[0], srows, dtau[0]);
+        attn_bwd_dtau(j.H[1], j.ws[1], srows, dtau[1]);
+        __syncthreads();
+        for (int q = 0; q < 2; ++q)
+            attn_bwd_dT(j.H[q], j.D[q], F, dtau[q], j.attn[q], j.wf[q], wlds, j.dT[q], (j.acc[q] & 2) != 0);
+        return;
+    }
+    const int q = b >= j.H[0] ? 1 : 0, k = b - (q ? j.H[0] : 0);
+    attn_bwd_dtau(j.H[q], j.ws[q], srows, dtau[0]);
+    __syncthreads();
+    const float *da1 = j.ws[q] + (size_t)kStage * kNT * j.H[q];
+    attn_bwd_head(k, j.H[q], j.D[q], F, dtau[0], da1, j.attn[q], j.wf[q], j.bf[q], T, j.dattn[q], j.dwf[q], j.dbf[q],
+                  j.acc[q], srows, wlds, a3s, dv);
 }
 
 int status() {
@@ -291,5 +346,20 @@ int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const fl
     return status();
 }
 
+
+int hsg_attn_params_finish_pair(int H0, int D0, const float *ws0, const float *attn0, const float *wf0,
+                                const float *bf0, float *dattn0, float *dwf0, float *dbf0, float *dT0, int acc0,
+                                int H1, int D1, const float *ws1, const float *attn1, const float *wf1,
+                                const float *bf1, float *dattn1, float *dwf1, float *dbf1, float *dT1, int acc1,
+                                int F, const float *T, void *stream) {
+    if (!dims_ok(H0, D0, F) || !dims_ok(H1, D1, F) || !ws0 || !ws1 || !attn0 || !attn1 || !wf0 || !wf1 || !dattn0 ||
+        !dattn1 || !dwf0 || !dwf1 || !dT0 || !dT1 || !T)
+        return HSG_EINVAL;
+    AttnBwdPair j{{H0, H1}, {D0, D1}, {acc0, acc1}, {ws0, ws1}, {attn0, attn1}, {wf0, wf1}, {bf0, bf1},
+                  {dattn0, dattn1}, {dwf0, dwf1}, {dbf0, dbf1}, {dT0, dT1}};
+    hipLaunchKernelGGL(k_attn_params_bwd_pair, dim3(H0 + H1 + 1), dim3(256), 0, (hipStream_t)stream, j, F, T,
+                       kStage);
+    return status();
+}
 
 }  // extern "C"

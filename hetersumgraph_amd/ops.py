@@ -267,6 +267,18 @@ def attn_params_finish(ws, attn, T, wf, bf, H, D, dst):
                                         stream_of(ws)), "hsg_attn_params_finish")
 
 
+def attn_params_finish_pair(job0, job1, T):
+    """:func:`attn_params_finish` of two layers sharing T in ONE launch
+    (hsg_attn_params_finish_pair); ``job`` = (ws, layer, dst) with ``dst`` as in
+    :func:`gat_table_bwd`, in the order the two separate calls would run."""
+    args = []
+    for ws, lay, dst in (job0, job1):
+        dattn, dwf, dbf, dT, acc_head, acc_T = dst
+        args += [lay.H, lay.D, ptr(ws), ptr(lay.attn), ptr(lay.wf), ptr(lay.bf), ptr(dattn), ptr(dwf), ptr(dbf),
+                 ptr(dT), int(bool(acc_head)) | (2 if acc_T else 0)]
+    check(load().hsg_attn_params_finish_pair(*args, T.shape[1], ptr(T), stream_of(T)), "hsg_attn_params_finish_pair")
+
+
 class _GatHeadsTable(torch.autograd.Function):
     """One multi-head application whose edge-type term comes from the TF-IDF table.
 

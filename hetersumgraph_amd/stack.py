@@ -40,8 +40,8 @@ from .dense import gemm, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
-from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_workspace, attn_tables, attn_tables_pair,
-                  gat_table_bwd, gat_table_fwd)
+from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_finish_pair, attn_params_workspace, attn_tables,
+                  attn_tables_pair, gat_table_bwd, gat_table_fwd)
 
 
 class _Grads:
@@ -346,9 +346,12 @@ class _GatStack(torch.autograd.Function):
                 else:
                     gemm(A, B, a_t=True, out=dw.view(m, n), add=dw.view(m, n) if a_w else None)
         batch.flush()
-        for lay, ws in stages.values():
-            dst = _attn_dst(pgrads, lay, T)
-            if dst is not None:
+        fin = [(ws, lay, _attn_dst(pgrads, lay, T)) for lay, ws in stages.values()]   # in order (dT flags)
+        fin = [f for f in fin if f[2] is not None]
+        if len(fin) == 2 and os.environ.get("HSG_ATTN_PAIR", "1") != "0":
+            attn_params_finish_pair(fin[0], fin[1], T)                # both layers in one launch
+        else:
+            for ws, lay, dst in fin:
                 attn_params_finish(ws, lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, dst)
         ctx.apps = ctx.bufs = None
         dw0 = grads.get(("w", 0)) if need_w0 else None

@@ -170,6 +170,16 @@ int hsg_attn_params_stage(int H, int D, int n_dtau_part, const float *dtau_part,
 int hsg_attn_params_finish(int H, int D, int F, const float *workspace, const float *attn, const float *wf,
                            const float *bf, const float *T, float *dattn, float *dwf, float *dbf, float *dT,
                            int accumulate, void *stream);
+
+/* hsg_attn_params_finish of two layers sharing T (the fused stack's W2S and S2W) in
+ * one launch: the same gradients, and when both layers name the same dT, layer 0's
+ * update of each element is applied before layer 1's, exactly as two launches in
+ * that order (acc0 / acc1: the accumulate flags of the two calls). */
+int hsg_attn_params_finish_pair(int H0, int D0, const float *ws0, const float *attn0, const float *wf0,
+                                const float *bf0, float *dattn0, float *dwf0, float *dbf0, float *dT0, int acc0,
+                                int H1, int D1, const float *ws1, const float *attn1, const float *wf1,
+                                const float *bf1, float *dattn1, float *dwf1, float *dbf1, float *dT1, int acc1,
+                                int F, const float *T, void *stream);
 size_t hsg_attn_params_bwd_workspace_floats(int H, int D);
 
 /* ---- dense fp32 GEMM on the matrix cores ---------------------------------------

@@ -278,3 +278,46 @@ def test_dropmasks_with_weight_transpose():
     got, Wt = dropmasks(jobs, dev, st, wt=(W, 8, 8))
     assert all(torch.equal(a, b) for a, b in zip(ref, got))
     assert torch.equal(Wt, transposed_weight(W, 8, 8))
+
+
+@pytest.mark.parametrize("shared_dT,acc", [(True, (0, 2)), (False, (0, 0)), (True, (3, 3))])
+def test_attn_params_finish_pair_equals_two_launches(shared_dT, acc):
+    """hsg_attn_params_finish_pair (the stack backward's two layers in one launch)
+    against two hsg_attn_params_finish launches in order: bitwise equal gradients,
+    including the dT both layers write (layer 0's update first) and accumulation."""
+    from types import SimpleNamespace
+    from hetersumgraph_amd.ops import attn_params_finish, attn_params_finish_pair, attn_params_workspace
+    torch.manual_seed(9)
+    dev = "cuda"
+    T = torch.randn(10, 50, device=dev)
+    lays = [SimpleNamespace(H=8, D=8, attn=torch.randn(8, 24, device=dev), wf=torch.randn(8, 8, 50, device=dev),
+                            bf=None),
+            SimpleNamespace(H=6, D=50, attn=torch.randn(6, 150, device=dev), wf=torch.randn(6, 50, 50, device=dev),
+                            bf=torch.randn(6, 50, device=dev))]
+    wss = []
+    for lay in lays:
+        ws = attn_params_workspace(T, lay.H, lay.D)
+        ws.copy_(torch.randn_like(ws))
+        wss.append(ws)
+
+    def dsts(dT_shared):
+        out = []
+        for q, lay in enumerate(lays):
+            dT = dT_shared if dT_shared is not None else torch.randn_like(T)
+            acc_T = bool(acc[q] & 2) or (dT_shared is not None and q == 1)
+            out.append([torch.randn_like(lay.attn), torch.randn_like(lay.wf),
+                        torch.randn_like(lay.bf) if lay.bf is not None else None, dT, bool(acc[q] & 1), acc_T])
+        return out
+
+    torch.manual_seed(1)
+    d_ref = dsts(torch.randn_like(T) if shared_dT else None)
+    torch.manual_seed(1)
+    d_got = dsts(torch.randn_like(T) if shared_dT else None)
+    for q, lay in enumerate(lays):
+        attn_params_finish(wss[q], lay.attn, T, lay.wf, lay.bf, lay.H, lay.D, d_ref[q])
+    attn_params_finish_pair((wss[0], lays[0], d_got[0]), (wss[1], lays[1], d_got[1]), T)
+    torch.cuda.synchronize()
+    for a, b in zip(d_ref, d_got):
+        for x, y in zip(a[:4], b[:4]):
+            if x is not None:
+                assert torch.equal(x, y)
