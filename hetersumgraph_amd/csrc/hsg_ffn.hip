@@ -133,7 +133,7 @@ __global__ __launch_bounds__(512) void k_ffn_small_fwd(int n, const float *__res
     }
     __syncthreads();
     // ---- phase 3: y = sum of the K slices (wave order) + b2; out = LN(dropout(y) + x)
-    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     constexpr int NPL = (D + 63) / 64;
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(512) void k_ffn_small_fwd(int n, const float *__res
                 for (int q = 1; q < NW; ++q) v += ps[q][r * D + c];
                 v += b2[c];
                 yout[o] = v;
-                if (p_drop > 0.f) v = hsg_keep(seed, offset, o, thr) ? v * scale : 0.f;
+                if (p_drop > 0.f) v = hsg_keep32(dkey, (uint32_t)o, thr) ? v * scale : 0.f;
                 s[i] = v + xs[r * LX + c];
                 acc += s[i];
             }
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd(int n, const float *__res
             hv[t][e] = H[(size_t)r * HID + cb + 16 * t + li];
         }
     // ---- phase A: LayerNorm + dropout backward, rows w and w + 8
-    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     const float gam = gamma[lane];
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd(int n, const float *__res
         bool keep = true;
         float v = yv;
         if (p_drop > 0.f) {
-            keep = hsg_keep(seed, offset, o, thr);
+            keep = hsg_keep32(dkey, (uint32_t)o, thr);
             v = keep ? v * scale : 0.f;
         }
         const float xh = (v + xv - mu) * rs;
@@ -354,7 +354,7 @@ int hsg_ffn_small_fwd(int n, int d, int d_hid, const float *x, const float *w1, 
                       void *stream) {
     if (n < 0 || !hsg_ffn_small_supported(d, d_hid) || p_drop < 0.f || p_drop >= 1.f) return HSG_EINVAL;
     if (!x || !w1 || !b1 || !w2 || !b2 || !gamma || !beta || !H || !y || !out || !mean || !rstd) return HSG_EINVAL;
-    if (p_drop > 0.f && !seed) return HSG_EINVAL;
+    if (p_drop > 0.f && (!seed || (long)n * d >= (1L << 32))) return HSG_EINVAL;   // 32-bit mask index
     if (!aligned16(x) || !aligned16(w1) || !aligned16(w2)) return HSG_EINVAL;
     if (n == 0) return 0;
     hipLaunchKernelGGL((k_ffn_small_fwd<64, 512>), dim3((unsigned)((n + kRB - 1) / kRB)), dim3(512), 0,
@@ -373,7 +373,7 @@ int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x
     if (n < 0 || !hsg_ffn_small_supported(d, d_hid) || p_drop < 0.f || p_drop >= 1.f) return HSG_EINVAL;
     if (!dout || !x || !H || !y || !w1 || !w2 || !gamma || !mean || !rstd || !dy || !dH || !dx || !lnpart || !hpart)
         return HSG_EINVAL;
-    if (p_drop > 0.f && !seed) return HSG_EINVAL;
+    if (p_drop > 0.f && (!seed || (long)n * d >= (1L << 32))) return HSG_EINVAL;   // 32-bit mask index
     if (n == 0) return 0;
     hipLaunchKernelGGL((k_ffn_small_bwd<64, 512>), dim3((unsigned)hsg_ffn_small_bwd_blocks(n)), dim3(512), 0,
                        (hipStream_t)stream, n, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy, dH,

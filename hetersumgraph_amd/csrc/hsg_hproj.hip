@@ -27,14 +27,7 @@ namespace {
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
-    x ^= x >> 16;
-    x *= 0x7feb352du;
-    x ^= x >> 15;
-    x *= 0x846ca68bu;
-    x ^= x >> 16;
-    return x;
-}
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) { return hsg_lowbias32(x); }
 
 // 16-bit uniforms, two heads per hash: drop probability resolution 2^-16.
 __device__ __forceinline__ uint32_t thr16(float p) {
@@ -73,9 +66,7 @@ __device__ __forceinline__ u32x4v bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // heads' 32 uniforms, compared against the threshold with two or three logic ops
 // per plane instead of a compare and a shift per row.
 __device__ __forceinline__ uint32_t drop_key(const int64_t *seedp, uint32_t offset) {
-    const uint64_t key64 = hsg_mix64((uint64_t)seedp[0] * 0x9E3779B97F4A7C15ull +
-                                     (uint64_t)offset * 0xD1B54A32D192ED03ull);
-    return (uint32_t)key64 ^ (uint32_t)(key64 >> 32);
+    return hsg_drop_key((uint64_t)seedp[0], offset);
 }
 
 // thread unit t of one mask: (head pair kp, 32-row word iw, column c), c fastest

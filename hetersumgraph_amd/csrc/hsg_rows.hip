@@ -7,7 +7,8 @@
 // the matching backward (LayerNorm backward, dropout backward, residual split,
 // per-block dgamma/dbeta partials -- no atomics, deterministic).
 //
-// Dropout masks come from a counter-based hash of (seed, offset, element): seed is
+// Dropout masks come from a counter-based hash of (seed, offset, element) (hsg_rng.h:
+// a per-call 32-bit key, then lowbias32 per element): seed is
 // read from device memory (so a HIP-graph replay can advance it), offset is a
 // per-call-site constant.  Forward and backward regenerate the same mask, so no
 // mask tensor is stored.  One wave per row; lane owns columns lane + 64*i.
@@ -35,7 +36,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
                                                 float *__restrict__ out, float *__restrict__ mean,
                                                 float *__restrict__ rstd) {
     const int lane = threadIdx.x & 63;
-    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += gridDim.x * 4) {
@@ -48,7 +49,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
             if (c < d) {
                 const size_t o = (size_t)r * d + c;
                 float v = y[o];
-                if (p_drop > 0.f) v = hsg_keep(seed, offset, o, thr) ? v * scale : 0.f;
+                if (p_drop > 0.f) v = hsg_keep32(dkey, (uint32_t)o, thr) ? v * scale : 0.f;
                 s[i] = v + x[o];
                 acc += s[i];
             }
@@ -82,7 +83,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__re
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
     if (row0 >= n) return;
-    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     f32x4r s[RPW][NV];
@@ -100,7 +101,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__re
                 f32x4r v = *reinterpret_cast<const f32x4r *>(y + o);
                 if (p_drop > 0.f) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = hsg_keep(seed, offset, o + e, thr) ? v[e] * scale : 0.f;
+                    for (int e = 0; e < 4; ++e) v[e] = hsg_keep32(dkey, (uint32_t)(o + e), thr) ? v[e] * scale : 0.f;
                 }
                 s[q][i] = v + *reinterpret_cast<const f32x4r *>(x + o);
                 acc[q] += (s[q][i][0] + s[q][i][1]) + (s[q][i][2] + s[q][i][3]);
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
                                                 float *__restrict__ part) {
     __shared__ float s_red[4][kMaxPerLane * 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t seed = p_drop > 0.f ? (uint64_t)seedp[0] : 0;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     float dg[NPL], db[NPL], dyb[NPL];
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
                 if (c < d) {
                     float v = yv[q][i];
                     if (p_drop > 0.f) {
-                        keep[i] = hsg_keep(seed, offset, rb + c, thr);
+                        keep[i] = hsg_keep32(dkey, (uint32_t)(rb + c), thr);
                         v = keep[i] ? v * scale : 0.f;
                     }
                     xh[i] = (v + xv[q][i] - mu[q]) * rs[q];
@@ -288,7 +289,8 @@ int hsg_ln_bwd_blocks(int n) { return grid_rows(n, kLnBwdGridCap); }
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta, float eps,
                float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
                void *stream) {
-    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed))
+    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) ||
+        (p_drop > 0.f && (long)n * d >= (1L << 32)))                      // 32-bit mask index
         return HSG_EINVAL;
     if (n == 0) return 0;
     const int npl = (d + 63) / 64;
@@ -328,7 +330,8 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
 int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                float *dy, float *dx, float *part, void *stream) {
-    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) || !part)
+    if (d < 1 || d > 64 * kMaxPerLane || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) || !part ||
+        (p_drop > 0.f && (long)n * d >= (1L << 32)))
         return HSG_EINVAL;
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(grid_rows(n, kLnBwdGridCap)), block(256);

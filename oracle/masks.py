@@ -24,7 +24,6 @@ import numpy as np
 _M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
 K_SEED = np.uint64(0x9E3779B97F4A7C15)
 K_OFF = np.uint64(0xD1B54A32D192ED03)
-K_IDX = np.uint64(0xA24BAED4963EE407)
 
 
 def _u64(x):
@@ -57,14 +56,16 @@ def ffn_scale(p):
 
 
 def ffn_keep(seed, offset, n, d, p):
-    """bool [n, d]: the FFN dropout keep-mask of one call (hsg_keep over the
-    row-major element index r * d + c) -- csrc/hsg_rows.hip k_ln_fwd*, csrc/hsg_ffn.hip."""
+    """bool [n, d]: the FFN dropout keep-mask of one call (hsg_keep32 over the
+    row-major element index r * d + c with the call's key hsg_drop_key(seed, offset))
+    -- csrc/hsg_rng.h, used by csrc/hsg_rows.hip k_ln_fwd* / k_ln_bwd and
+    csrc/hsg_ffn.hip."""
     thr = ffn_threshold(p)
-    idx = np.arange(n * d, dtype=np.uint64)
+    key = _drop_key(seed, offset)
+    idx = np.arange(n * d, dtype=np.uint32)
     with np.errstate(over="ignore"):
-        base = _u64(np.int64(seed).astype(np.uint64)) * K_SEED + np.uint64(offset & 0xFFFFFFFF) * K_OFF
-        z = mix64(base + idx * K_IDX)
-    return ((z >> np.uint64(32)) >= np.uint64(thr)).reshape(n, d)
+        h = _lowbias32((idx * np.uint32(0x85EBCA6B)) ^ key)
+    return (h >= np.uint32(thr)).reshape(n, d)
 
 
 # ------------------------------------------------------- head-projection masks
