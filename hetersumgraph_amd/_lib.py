@@ -28,7 +28,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
-           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_dropmask_multi_wt", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
+           "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_dropmask_multi_wt", "hsg_step_prologue", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
            "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
@@ -113,6 +113,7 @@ _SIGS = {
     "hsg_wsplit_dims": [_I, _I, _P, _P],
     "hsg_dropmask_multi": [_I, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_dropmask_multi_wt": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P],
+    "hsg_step_prologue": [_I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
     "hsg_gemm_bf16_slabs": [_I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P, _P],
     "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],

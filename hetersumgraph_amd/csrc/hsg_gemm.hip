@@ -44,6 +44,7 @@
 #include <atomic>
 
 #include "../../include/hsg.h"
+#include "hsg_wsplit.h"
 
 namespace {
 
@@ -396,12 +397,7 @@ typedef short v4s16 __attribute__((ext_vector_type(4)));
 // ds_read_b128 groups hit 64 distinct banks)
 template <int BK> struct Ldh { static constexpr int v = BK + 8; };
 
-__device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &x2) {
-    x0 = (__bf16)x;                       // v_cvt_pk_bf16_f32, RNE
-    const float r = x - (float)x0;        // exact
-    x1 = (__bf16)r;
-    x2 = (__bf16)(r - (float)x1);         // exact difference, then RNE
-}
+__device__ __forceinline__ void split3(float x, __bf16 &x0, __bf16 &x1, __bf16 &x2) { hsg_split3(x, x0, x1, x2); }
 
 // One operand tile for k_gemm3: ROWS (M or N) x BK (K) from global into registers,
 // then into NL bf16 limb planes in LDS, in the operand's own global orientation:
@@ -865,42 +861,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm4(GemmArgs p) {
 // tile rows are 64 B; chunk c (16 B) of row r sits at c ^ ((r >> 2) & 3), which
 // makes the ds_read_b128 fragment reads conflict-free.
 // ---------------------------------------------------------------------------------
-struct WSplitJobs {
-    const float *W[4];
-    __bf16 *out[4];
-    int N[4], K[4], ldw[4], trans[4], Np[4], Kp[4];
-    int start[5];
-    int n;
-};
-
-// One thread per (n, 8 consecutive k): three 16-B limb stores.  Job q owns blocks
-// [start[q], start[q+1]); for a transposed weight consecutive threads take consecutive
-// n, so each of the 8 reads W[k][n] is coalesced across the wave.
-__global__ __launch_bounds__(256) void k_wsplit(WSplitJobs j) {
-    int q = 0;
-    while (q + 1 < j.n && (int)blockIdx.x >= j.start[q + 1]) ++q;
-    const int u = ((int)blockIdx.x - j.start[q]) * 256 + threadIdx.x;
-    const int Kp = j.Kp[q], Np = j.Np[q], N = j.N[q], K = j.K[q], ldw = j.ldw[q];
-    const int kc8 = Kp / 8;
-    if (u >= Np * kc8) return;
-    const bool tr = j.trans[q] != 0;
-    const int n = tr ? u % Np : u / kc8, k0 = 8 * (tr ? u / Np : u % kc8);
-    const float *W = j.W[q];
-    bf16x8 x0, x1, x2;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const int k = k0 + e;
-        float v = 0.f;
-        if (n < N && k < K) v = tr ? W[(size_t)k * ldw + n] : W[(size_t)n * ldw + k];
-        __bf16 a, b, c;
-        split3(v, a, b, c);
-        x0[e] = a; x1[e] = b; x2[e] = c;
-    }
-    const size_t plane = (size_t)Np * Kp, o = (size_t)n * Kp + k0;
-    *reinterpret_cast<bf16x8 *>(j.out[q] + o) = x0;
-    *reinterpret_cast<bf16x8 *>(j.out[q] + plane + o) = x1;
-    *reinterpret_cast<bf16x8 *>(j.out[q] + 2 * plane + o) = x2;
-}
+// one launch splits up to four weights (hsg_wsplit.h)
+__global__ __launch_bounds__(256) void k_wsplit(HsgWSplitJobs j) { hsg_wsplit_block(j, (int)blockIdx.x); }
 
 // Epilogue of one wave's TN 32x32 accumulator tiles (lane: rows row0 + (r&3) + 8(r>>2)
 // + 4h, column col0 + 32j + li), epi_apply's semantics.  The aux operand (relu' mask
@@ -1976,18 +1938,8 @@ void hsg_wsplit_dims(int N, int K, int *Np, int *Kp) {
 int hsg_wsplit(int njobs, const float *const *W, const int *N, const int *K, const int *ldw, const int *trans,
                void *const *planes, void *stream) {
     if (njobs < 1 || njobs > 4) return HSG_EINVAL;
-    WSplitJobs j{};
-    j.n = njobs;
-    j.start[0] = 0;
-    for (int q = 0; q < njobs; ++q) {
-        if (!W[q] || !planes[q] || N[q] <= 0 || K[q] <= 0 || (((uintptr_t)planes[q]) & 15)) return HSG_EINVAL;
-        if (ldw[q] < (trans[q] ? N[q] : K[q])) return HSG_EINVAL;
-        j.W[q] = W[q];
-        j.out[q] = reinterpret_cast<__bf16 *>(planes[q]);
-        j.N[q] = N[q]; j.K[q] = K[q]; j.ldw[q] = ldw[q]; j.trans[q] = trans[q] != 0;
-        hsg_wsplit_dims(N[q], K[q], &j.Np[q], &j.Kp[q]);
-        j.start[q + 1] = j.start[q] + (j.Np[q] * (j.Kp[q] / 8) + 255) / 256;     // blocks
-    }
+    HsgWSplitJobs j{};
+    if (hsg_wsplit_setup(j, njobs, W, N, K, ldw, trans, planes)) return HSG_EINVAL;
     hipLaunchKernelGGL(k_wsplit, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;

@@ -21,6 +21,7 @@
 
 #include "../../include/hsg.h"
 #include "hsg_rng.h"
+#include "hsg_wsplit.h"
 
 namespace {
 
@@ -138,6 +139,9 @@ struct DropJobs {
     const float *W;
     float *Wt;
     int wH, wD, wIn;
+    // optional: the wide FFN's weight limb planes (hsg_wsplit) in the blocks after those
+    HsgWSplitJobs ws;
+    int ws_first;                                    // first block of the split
 };
 
 // The step's dropout seed: seed += 1 and the backward-stable snapshot of the new value
@@ -159,6 +163,10 @@ __device__ __forceinline__ void hproj_wt_block(int k, int c0, int D, int in, con
 }
 
 __global__ __launch_bounds__(256) void k_dropmask_multi(DropJobs j, const int64_t *seedp) {
+    if ((int)blockIdx.x >= j.ws_first) {                // the weight limb split blocks
+        hsg_wsplit_block(j.ws, (int)blockIdx.x - j.ws_first);
+        return;
+    }
     if ((int)blockIdx.x >= j.start[j.njobs]) {          // the weight-transpose blocks
         const int b = (int)blockIdx.x - j.start[j.njobs], nct = (j.wIn + 63) / 64;
         hproj_wt_block(b / nct, (b % nct) * 64, j.wD, j.wIn, j.W, j.Wt);
@@ -966,7 +974,17 @@ int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, con
 int hsg_dropmask_multi_wt(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
                           const uint32_t *offset, uint32_t *const *bits, int wH, int wD, int wIn, const float *W,
                           float *Wt, void *stream) {
+    return hsg_step_prologue(njobs, n, in, H, p, seed, offset, bits, wH, wD, wIn, W, Wt, 0, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int hsg_step_prologue(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
+                      const uint32_t *offset, uint32_t *const *bits, int wH, int wD, int wIn, const float *W,
+                      float *Wt, int nsplit, const float *const *sW, const int *sN, const int *sK, const int *sldw,
+                      const int *strans, void *const *splanes, void *stream) {
     if (njobs < 1 || njobs > 8 || !seed) return HSG_EINVAL;
+    if (nsplit < 0 || nsplit > 4 || (nsplit > 0 && (!sW || !sN || !sK || !sldw || !strans || !splanes)))
+        return HSG_EINVAL;
     if (W && (wH < 1 || wD < 1 || wIn < 1 || !Wt)) return HSG_EINVAL;
     DropJobs j{};
     j.W = W;
@@ -984,8 +1002,11 @@ int hsg_dropmask_multi_wt(int njobs, const int *n, const int *in, const int *H, 
         j.start[q + 1] = j.start[q] + (int)((total + 255) / 256);
     }
     const int wblocks = W ? (wIn + 63) / 64 * wH : 0;
-    if (j.start[njobs] + wblocks == 0) return 0;
-    hipLaunchKernelGGL(k_dropmask_multi, dim3(j.start[njobs] + wblocks), dim3(256), 0, (hipStream_t)stream, j, seed);
+    j.ws_first = j.start[njobs] + wblocks;
+    if (nsplit > 0 && hsg_wsplit_setup(j.ws, nsplit, sW, sN, sK, sldw, strans, splanes)) return HSG_EINVAL;
+    const int total = j.ws_first + (nsplit > 0 ? j.ws.start[nsplit] : 0);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(k_dropmask_multi, dim3(total), dim3(256), 0, (hipStream_t)stream, j, seed);
     return status();
 }
 

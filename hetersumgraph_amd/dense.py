@@ -117,9 +117,11 @@ def split_dims(N, K):
     return np_.value, kp.value
 
 
-def split_weights(*specs):
+def split_weights(*specs, launch=True):
     """[(W, trans), ...] (1..4) -> [SplitWeight]: B = W^T if trans else W, split in
-    one launch."""
+    one launch.  ``launch=False``: the planes are allocated but not written; returns
+    (weights, job) with ``job`` = (n, W, N, K, ldw, trans, planes) ctypes arrays for a
+    caller that runs the split inside another launch (hsg_step_prologue)."""
     lib = load()
     if not 1 <= len(specs) <= 4:
         raise ValueError("split_weights: 1..4 weights per launch")
@@ -136,8 +138,10 @@ def split_weights(*specs):
     n = len(specs)
     arr_i = ctypes.c_int * n
     arr_p = ctypes.c_void_p * n
-    check(lib.hsg_wsplit(n, arr_p(*Ws), arr_i(*Ns), arr_i(*Ks), arr_i(*lds), arr_i(*trs), arr_p(*Ps),
-                         stream_of(specs[0][0])), "hsg_wsplit")
+    job = (n, arr_p(*Ws), arr_i(*Ns), arr_i(*Ks), arr_i(*lds), arr_i(*trs), arr_p(*Ps))
+    if not launch:
+        return out, job
+    check(lib.hsg_wsplit(*job, stream_of(specs[0][0])), "hsg_wsplit")
     return out
 
 

@@ -49,13 +49,14 @@ def _draw(x, p_drop, rng):
     return rng if rng is not None else hsg_rng.get(x.device).take()
 
 
-def ffn_wsplit(x, w1, b1, w2, b2):
+def ffn_wsplit(x, w1, b1, w2, b2, launch=True):
     """The pre-split weight operands (hsg_wsplit: W1, W2 for the forward GEMMs, W2^T,
     W1^T for dH = dy W2 and dx += dH W1) of an FFN that runs on the GEMM path, or
     None: the narrow fused FFN, the 'f32mfma' GEMM mode, shapes hsg_gemm_f32_psw
     does not take, or HSG_GEMM_PSW=0 (A/B).  In the 'bf16' mode the GEMMs on these
     planes run hsg_gemm_bf16_psw (plane 0 = RNE(W), one product).  Made once per forward of the fused stack and
-    shared by all applications of the layer and their backward."""
+    shared by all applications of the layer and their backward.  ``launch=False``:
+    (weights, job) with the split left to the caller's launch (hsg_step_prologue)."""
     lib = load()
     if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
         return None
@@ -64,6 +65,9 @@ def ffn_wsplit(x, w1, b1, w2, b2):
     d_hid, d = w1.shape
     if d % 4 or d_hid % 4 or not (w1.is_contiguous() and w2.is_contiguous()):
         return None
+    if not launch:                       # (planes, job) for hsg_step_prologue
+        out, job = split_weights((w1, False), (w2, False), (w2, True), (w1, True), launch=False)
+        return tuple(out), job
     return tuple(split_weights((w1, False), (w2, False), (w2, True), (w1, True)))
 
 

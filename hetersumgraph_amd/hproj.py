@@ -22,14 +22,18 @@ import ctypes
 from ._lib import check, load, ptr, stream_of
 
 
-def dropmasks(jobs, device, stream_of_t, wt=None):
+def dropmasks(jobs, device, stream_of_t, wt=None, wsplit_job=None):
     """Keep-mask bits of several head projections in ONE launch
     (hsg_dropmask_multi): ``jobs`` = [(n, d_in, H, p, seed_t, offset)] with one
     shared seed tensor; returns the bit tensors, each as hsg_dropmask would draw it.
     ``wt`` = (W, H, D): the same launch also writes :func:`transposed_weight` of W
-    (hsg_dropmask_multi_wt), returned as ``(masks, Wt)``."""
+    (hsg_dropmask_multi_wt), returned as ``(masks, Wt)``.  ``wsplit_job``: a
+    dense.split_weights(..., launch=False) job whose limb planes the same launch
+    writes (hsg_step_prologue)."""
     lib = load()
     if not jobs:
+        if wsplit_job is not None:
+            check(lib.hsg_wsplit(*wsplit_job, stream_of_t), "hsg_wsplit")
         return ([], transposed_weight(*wt)) if wt is not None else []
     if len({id(j[4]) for j in jobs}) != 1:
         raise ValueError("dropmasks: one seed tensor per batch")
@@ -51,11 +55,12 @@ def dropmasks(jobs, device, stream_of_t, wt=None):
         sl = slice(q0, q1)
         m = q1 - q0
         w_args = (H, D, W.shape[1], ptr(W), ptr(Wt)) if (wt is not None and q0 == 0) else (0, 0, 0, None, None)
-        check(lib.hsg_dropmask_multi_wt(m, (ctypes.c_int * m)(*ns[sl]), (ctypes.c_int * m)(*ins[sl]),
-                                        (ctypes.c_int * m)(*hs[sl]), (ctypes.c_float * m)(*ps[sl]),
-                                        ptr(jobs[0][4]), (ctypes.c_uint32 * m)(*offs[sl]),
-                                        (ctypes.c_void_p * m)(*bp[sl]), *w_args, stream_of_t),
-              "hsg_dropmask_multi_wt")
+        s_args = wsplit_job if (wsplit_job is not None and q0 == 0) else (0, None, None, None, None, None, None)
+        check(lib.hsg_step_prologue(m, (ctypes.c_int * m)(*ns[sl]), (ctypes.c_int * m)(*ins[sl]),
+                                    (ctypes.c_int * m)(*hs[sl]), (ctypes.c_float * m)(*ps[sl]),
+                                    ptr(jobs[0][4]), (ctypes.c_uint32 * m)(*offs[sl]),
+                                    (ctypes.c_void_p * m)(*bp[sl]), *w_args, *s_args, stream_of_t),
+              "hsg_step_prologue")
     return (out, Wt) if wt is not None else out
 
 

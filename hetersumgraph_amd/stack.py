@@ -225,7 +225,7 @@ class _GatStack(torch.autograd.Function):
         # into one [applications, rows, width] buffer per layer, so the backward runs
         # each FFN weight gradient as ONE GEMM over all applications' rows
         n_app = {id(w2s): n_iter + 1, id(s2w): n_iter}
-        bufs, slot, wsplits = {}, {id(w2s): 0, id(s2w): 0}, {}
+        bufs, slot = {}, {id(w2s): 0, id(s2w): 0}
 
         # every dropout draw of the forward, in the order the layer-by-layer path takes
         # them (per application: head projection, then FFN), so both paths see the
@@ -243,8 +243,22 @@ class _GatStack(torch.autograd.Function):
         # launch as the masks (hsg_dropmask_multi_wt; HSG_WT_FOLD=0: its own launch)
         narrow = [lay for lay in (w2s, s2w) if lay.p_attn > 0 and narrow_heads(lay.W.shape[1], lay.H, lay.D)]
         fold = narrow[0] if narrow and jobs and os.environ.get("HSG_WT_FOLD", "1") != "0" else None
+        # ... and so are the wide FFN's weight limb planes (hsg_step_prologue: one launch
+        # for masks, transpose and split; HSG_WT_FOLD=0: separate launches)
+        wsplits, split_job = {}, None
         if fold is not None:
-            mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0), wt=(fold.W, fold.H, fold.D))
+            for lay in (w2s, s2w):
+                d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+                r = ffn_wsplit(w0.new_empty(1, d), lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2,
+                               launch=False)
+                wsplits[id(lay)] = r[0] if r is not None else None
+                if r is not None and split_job is None:
+                    split_job = r[1]
+                elif r is not None:                  # a second wide FFN: its own launch
+                    wsplits[id(lay)] = ffn_wsplit(w0.new_empty(1, d), lay.w1.view(d_hid, d), lay.b1,
+                                                  lay.w2.view(d, d_hid), lay.b2)
+            mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0), wt=(fold.W, fold.H, fold.D),
+                                       wsplit_job=split_job)
         else:
             mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0)), None
         masks = iter(mlist)
@@ -259,9 +273,11 @@ class _GatStack(torch.autograd.Function):
                 d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
                 bufs[key] = (states[org].new_empty(n_app[key], rel.n_dst, d),
                              states[org].new_empty(n_app[key], rel.n_dst, d_hid))
-                # the FFN weights split into limb planes once per forward (hsg_wsplit)
-                wsplits[key] = ffn_wsplit(bufs[key][0][0], lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid),
-                                          lay.b2)
+                # the FFN weights split into limb planes once per forward (hsg_wsplit),
+                # unless the prologue launch already did
+                if key not in wsplits:
+                    wsplits[key] = ffn_wsplit(bufs[key][0][0], lay.w1.view(d_hid, d), lay.b1,
+                                              lay.w2.view(d, d_hid), lay.b2)
             a = slot[key]
             slot[key] += 1
             out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],

@@ -367,6 +367,17 @@ int hsg_dropmask_multi(int njobs, const int *n, const int *in, const int *H, con
 int hsg_dropmask_multi_wt(int njobs, const int *n, const int *in, const int *H, const float *p,
                           const int64_t *seed, const uint32_t *offset, uint32_t *const *bits, int wH, int wD,
                           int wIn, const float *W, float *Wt, void *stream);
+
+/* The step's parameter-only prologue in ONE launch: hsg_dropmask_multi_wt's masks and
+ * weight transpose, plus hsg_wsplit's limb planes of nsplit (0..4) weights (sW, sN,
+ * sK, sldw, strans, splanes as hsg_wsplit's W, N, K, ldw, trans, planes): the fused
+ * stack's dropout masks (GATStackLayer.py:56), W2S fc weight (GATLayer.py:110) and
+ * the S2W FFN's w_1 / w_2 views (GATLayer.py:39), all independent of the step's
+ * activations. */
+int hsg_step_prologue(int njobs, const int *n, const int *in, const int *H, const float *p, const int64_t *seed,
+                      const uint32_t *offset, uint32_t *const *bits, int wH, int wD, int wIn, const float *W,
+                      float *Wt, int nsplit, const float *const *sW, const int *sN, const int *sK, const int *sldw,
+                      const int *strans, void *const *splanes, void *stream);
 int hsg_hproj_fwd(int n, int in, int H, int D, const float *X, int ldx, const float *W,
                   const uint32_t *bits, float p, float *Z, int ldz, void *stream);
 /* hsg_hproj_fwd plus the attention's source logits sigma[i][k] = <Z[i, kD:(k+1)D], a1[k]>

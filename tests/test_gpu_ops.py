@@ -321,3 +321,26 @@ def test_attn_params_finish_pair_equals_two_launches(shared_dT, acc):
         for x, y in zip(a[:4], b[:4]):
             if x is not None:
                 assert torch.equal(x, y)
+
+
+def test_step_prologue_weight_split_equals_hsg_wsplit():
+    """hsg_step_prologue: the masks, the folded weight transpose AND the wide FFN's
+    limb planes in one launch equal hsg_dropmask_multi / hsg_hproj_wt / hsg_wsplit."""
+    from hetersumgraph_amd.dense import split_weights
+    from hetersumgraph_amd.hproj import dropmasks, transposed_weight
+    dev = torch.device("cuda")
+    seed = torch.tensor([77], dtype=torch.int64, device=dev)
+    jobs = [(19200, 300, 8, 0.1, seed, 3), (1120, 64, 6, 0.1, seed, 7)]
+    W = torch.randn(64, 300, device=dev)
+    w1, w2 = torch.randn(512, 300, device=dev), torch.randn(300, 512, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    specs = ((w1, False), (w2, False), (w2, True), (w1, True))
+    ref_masks = dropmasks(jobs, dev, st)
+    ref_split = split_weights(*specs)
+    pre, job = split_weights(*specs, launch=False)
+    got_masks, Wt = dropmasks(jobs, dev, st, wt=(W, 8, 8), wsplit_job=job)
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(ref_masks, got_masks))
+    assert torch.equal(Wt, transposed_weight(W, 8, 8))
+    for a, b in zip(ref_split, pre):
+        assert torch.equal(a.planes, b.planes)
