@@ -142,14 +142,23 @@ __global__ __launch_bounds__(256) void k_colsum_stage(int rows0, int cols0, cons
 
 // blocks 0..H-1: one head each (d attn row, dW_f,k, db_f,k); block H: dT
 // d tau [11][H] of one layer, summed over the stage rows in order, into LDS
+// (rows requested 32 at a time before any is added: the sum still runs in row order)
+__device__ __forceinline__ float attn_bwd_dtau_col(int NTH, const float *__restrict__ dtau_st, int srows, int i) {
+    float s = 0.f;
+    for (int r0 = 0; r0 < srows; r0 += 32) {
+        float v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) v[q] = dtau_st[min(r0 + q, srows - 1) * NTH + i];
+#pragma unroll
+        for (int q = 0; q < 32; ++q)
+            if (r0 + q < srows) s += v[q];
+    }
+    return s;
+}
+
 __device__ __forceinline__ void attn_bwd_dtau(int H, const float *__restrict__ dtau_st, int srows, float *dtau) {
     const int NTH = kNT * H;
-    for (int i = threadIdx.x; i < NTH; i += blockDim.x) {
-        float s = 0.f;
-#pragma unroll 16
-        for (int r = 0; r < srows; ++r) s += dtau_st[r * NTH + i];
-        dtau[i] = s;
-    }
+    for (int i = threadIdx.x; i < NTH; i += blockDim.x) dtau[i] = attn_bwd_dtau_col(NTH, dtau_st, srows, i);
 }
 
 // the dT block's contribution of one layer: dT[t][f] (+)= sum_k dtau[t][k] v_k[f]
@@ -162,9 +171,21 @@ __device__ __forceinline__ void attn_bwd_dT(int H, int D, int F, const float *dt
     for (int i = tid; i < H * F; i += nt) {
         const int kk = i / F, f = i - (i / F) * F;
         const float *wk = wf + (size_t)kk * D * F;
+        const float *a3 = attn + kk * 3 * D + 2 * D;
         float s = 0.f;
-#pragma unroll 8
-        for (int d = 0; d < D; ++d) s = fmaf(attn[kk * 3 * D + 2 * D + d], wk[d * F + f], s);
+        // 32 weights requested at a time (coalesced across f), then added in d order
+        for (int d0 = 0; d0 < D; d0 += 32) {
+            float w[32], a[32];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const int d = min(d0 + q, D - 1);
+                w[q] = wk[d * F + f];
+                a[q] = a3[d];
+            }
+#pragma unroll
+            for (int q = 0; q < 32; ++q)
+                if (d0 + q < D) s = fmaf(a[q], w[q], s);
+        }
         vall[i] = s;
     }
     __syncthreads();
@@ -207,8 +228,14 @@ __device__ __forceinline__ void attn_bwd_head(int k, int H, int D, int F, const 
             if (dbf) dbf[k * D + d] = (accumulate & 1) ? dbf[k * D + d] + a3s[d] * dc : a3s[d] * dc;
         }
         float g = 0.f;                             // d a1: stage rows in order
-#pragma unroll 16
-        for (int r = 0; r < srows; ++r) g += da1_st[(size_t)r * H * D + k * D + d];
+        for (int r0 = 0; r0 < srows; r0 += 32) {
+            float v[32];
+#pragma unroll
+            for (int q = 0; q < 32; ++q) v[q] = da1_st[(size_t)min(r0 + q, srows - 1) * H * D + k * D + d];
+#pragma unroll
+            for (int q = 0; q < 32; ++q)
+                if (r0 + q < srows) g += v[q];
+        }
         if (accumulate & 1) {
             dattn[k * D3 + d] += g;
             dattn[k * D3 + 2 * D + d] += s;
@@ -266,8 +293,11 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd_pair(AttnBwdPair j, int
     __shared__ float dtau[2][kNT * kHMax];
     const int b = blockIdx.x;
     if (b == j.H[0] + j.H[1]) {                    // dT
-        attn_bwd_dtau(j.H[0], j.ws[0], srows, dtau[0]);
-        attn_bwd_dtau(j.H[1], j.ws[1], srows, dtau[1]);
+        const int n0 = kNT * j.H[0], n1 = kNT * j.H[1];
+        for (int i = threadIdx.x; i < n0 + n1; i += blockDim.x) {      // both layers' columns in one pass
+            const int q = i >= n0 ? 1 : 0, c = i - (q ? n0 : 0);
+            dtau[q][c] = attn_bwd_dtau_col(q ? n1 : n0, j.ws[q], srows, c);
+        }
         __syncthreads();
         for (int q = 0; q < 2; ++q)
             attn_bwd_dT(j.H[q], j.D[q], F, dtau[q], j.attn[q], j.wf[q], wlds, j.dT[q], (j.acc[q] & 2) != 0);
