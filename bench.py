@@ -202,12 +202,18 @@ def epilogue_bytes_fwd(rel, H, D):
     return 4 * rel.n_dst * H * D
 
 
-def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False):
+def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False, issued=False):
     """Per-step work items (name, bytes, flops, peak TFLOP/s) of the timed stack
     (W2S + n_iter x (S2W, W2S), fwd + bwd) for the full-stack floor
     sum_k max(B_k / BW, F_k / peak_k).  Dense bytes are the GEMM
-    operands and results (fp32); the FFN and head-projection flops are exact."""
-    dense_peak = BF16_MFMA_PEAK_TFLOPS if gemm_dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
+    operands and results (fp32); the FFN and head-projection flops are exact.
+    ``issued``: price the wide (S2W) FFN GEMMs at the rate the path ISSUES them --
+    in 'f32' mode six bf16 limb products per fp32-accurate product on the bf16 MFMA
+    (2.5 PF/s / 6 = 417 TF/s fp32-equivalent) -- instead of the exact-f32 MFMA peak."""
+    if gemm_dtype == "bf16":
+        dense_peak = BF16_MFMA_PEAK_TFLOPS
+    else:
+        dense_peak = BF16_MFMA_PEAK_TFLOPS / 6 if issued else FP32_MFMA_PEAK_TFLOPS
     items = []
     layers = {"W2S": (rel_w, 300, 8, 8, 64), "S2W": (rel_s, 64, 6, 50, 300)}
     apps = ["W2S"] + ["S2W", "W2S"] * n_iter
@@ -409,13 +415,24 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     torch.cuda.set_device(local % ndev)
     dev = torch.device("cuda", local % ndev)
-    if world > 1:
+    # the data-parallel exchange runs whenever there is more than one rank; at one rank
+    # HSG_DP_REHEARSAL=1 runs it anyway over a world-size-1 group (the driver's N-GPU
+    # code path -- RCCL communicator, doc-weighted in-place all-reduce captured in the
+    # step graph -- exercised on one GPU; tests/test_gpu_rccl.py)
+    dp = world > 1 or os.environ.get("HSG_DP_REHEARSAL", "0") == "1"
+    backend = None
+    if dp:
         import torch.distributed as dist
         backend = os.environ.get("HSG_DIST_BACKEND", "nccl")       # nccl = RCCL over xGMI
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        if world > 1:
+            dist.init_process_group(backend, **kw)
         else:
-            dist.init_process_group(backend)
+            import tempfile
+            fd, rdv = tempfile.mkstemp(prefix="hsg_rdv_")
+            os.close(fd)
+            os.unlink(rdv)
+            dist.init_process_group(backend, init_method=f"file://{rdv}", rank=0, world_size=1, **kw)
     from hetersumgraph_amd import _lib
     _lib.load()
     from hetersumgraph_amd.dense import set_gemm_dtype
@@ -442,14 +459,19 @@ def main():
 
     def allreduce():
         # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL.
-        # After a graph replay every gradient is final at once, so there is nothing to
+        # After the backward every gradient is final at once, so there is nothing to
         # overlap with: ONE flat bucket (7 MB at cfg2) pays one collective latency
         # instead of one per 2 MiB bucket (the eager train step overlaps its buckets
         # with the backward instead: parallel.GradientReducer).  The fused stack writes
         # every gradient into one flat buffer (stack._Grads), which is reduced in place:
-        # one scale pass + one all-reduce, no concatenation or copy-back
-        from hetersumgraph_amd.parallel import allreduce_gradients
-        allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
+        # one scale pass + one all-reduce, no concatenation or copy-back -- and no host
+        # sync, so on RCCL it is captured into the step's graph
+        from hetersumgraph_amd.parallel import allreduce_gradients, flat_gradients, reduce_flat
+        flat = flat_gradients(params)
+        if flat is not None:
+            reduce_flat(flat, scale=frac)
+        else:
+            allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
 
     def zero():
         # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
@@ -461,65 +483,95 @@ def main():
     for _ in range(max(args.warmup, 2)):
         zero()
         step()
-        if world > 1:
-            allreduce()
+        if dp:
+            allreduce()                # also the communicator's first collective, before any capture
     torch.cuda.synchronize()
 
     use_graph = not args.no_graph
     graph = None
-    if use_graph:
-        try:
-            s_side = torch.cuda.Stream(dev)
-            s_side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(s_side):
-                for _ in range(2):
-                    zero()
-                    step()
-            torch.cuda.current_stream(dev).wait_stream(s_side)
-            zero()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
+    # RCCL collectives are capturable: the exchange joins the step's graph (one replay
+    # = step + exchange); gloo's are not, so a gloo rehearsal runs it eagerly after it
+    capture_exchange = dp and backend == "nccl" and os.environ.get("HSG_CAPTURE_EXCHANGE", "1") != "0"
+
+    def capture(with_exchange):
+        s_side = torch.cuda.Stream(dev)
+        s_side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s_side):
+            for _ in range(2):
+                zero()
                 step()
-            torch.cuda.synchronize()
-        except Exception as exc:  # pragma: no cover - reported in the JSON
-            print(f"hip graph capture failed, running eager: {exc!r}", file=sys.stderr)
-            graph = None
-            use_graph = False
+                if with_exchange:
+                    allreduce()
+        torch.cuda.current_stream(dev).wait_stream(s_side)
+        zero()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+            if with_exchange:
+                allreduce()
+        torch.cuda.synchronize()
+        return g
+
+    if use_graph:
+        for attempt in ((True, False) if capture_exchange else (False,)):
+            try:
+                graph = capture(attempt)
+                capture_exchange = attempt
+                break
+            except Exception as exc:  # pragma: no cover - reported on stderr and in the JSON
+                print(f"hip graph capture (exchange inside: {attempt}) failed: {exc!r}", file=sys.stderr)
+                graph = None
+        if graph is None:
+            use_graph = capture_exchange = False
+    else:
+        capture_exchange = False
 
     def run_one():
-        # replay == zero_grad(set_to_none) + forward + backward: the captured backward
-        # writes (does not accumulate into) the graph-owned .grad tensors
+        # replay == zero_grad(set_to_none) + forward + backward (+ the captured exchange):
+        # the captured backward writes (does not accumulate into) the graph-owned .grad
+        # tensors, and the captured all-reduce reduces them in place
         if graph is not None:
             graph.replay()
         else:
             zero()
             step()
-        if world > 1:
+        if dp and not capture_exchange:
             allreduce()
 
     for _ in range(args.warmup):
         run_one()
-    if world > 1:
+    if dp:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
+    # one HIP event after every step on the launching stream: the per-step times give
+    # the median (t_step is the median); the contract's value stays the
+    # timed region's mean (K steps between barrier + synchronize)
+    st_main = torch.cuda.current_stream(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record(st_main)
+    for i in range(args.steps):
         run_one()
+        evs[i + 1].record(st_main)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    med_ms = float(np.median(step_ms))
+    if dp:
+        t = torch.tensor([dt, med_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt, med_ms = float(t[0].item()), float(t[1].item())
     ms_per_step = dt / args.steps * 1e3
     value = E_global / (dt / args.steps)
     from hetersumgraph_amd.parallel import flat_gradients
-    dp_exchange = ("none (one rank)" if world == 1 else
-                   "one in-place all-reduce of the flat gradient buffer" if flat_gradients(params) is not None
-                   else "bucketed all-reduce (concatenated copies)")
+    dp_exchange = ("none (one rank)" if not dp else
+                   ("one in-place all-reduce of the flat gradient buffer" if flat_gradients(params) is not None
+                    else "bucketed all-reduce (concatenated copies)")
+                   + (", captured in the step's HIP graph" if capture_exchange else ", eager after each step")
+                   + f" ({backend}, world {world})")
 
     # edge kernels timed inside eager steps (HIP events of their dispatches), after the
     # timed region so they cannot perturb it
@@ -542,6 +594,7 @@ def main():
     traffic, traffic_src, traffic_rec = pmc_traffic() if args.config == "cfg2" else (None, None, None)
     items = step_work(rel_w, rel_s, args.n_iter, args.dtype)
     floor_s, edge_floor_s, dense_floor_s, gflop = full_stack_floor(items)
+    floor_i, _, dense_floor_i, _ = full_stack_floor(step_work(rel_w, rel_s, args.n_iter, args.dtype, issued=True))
     d_ms, d_flops, d_name = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
     d_tf = d_flops / (d_ms * 1e-3) / 1e12
 
@@ -553,6 +606,11 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        "median_ms_per_step": med_ms,
+        "value_at_median": E_global / (med_ms * 1e-3),
+        "step_timing": "value / ms_per_step: the timed region (K steps between barrier + synchronize) / K; "
+                       "median_ms_per_step: median of the K per-step HIP-event intervals of the same steps "
+                       "(BASELINE.md t_step), max over ranks",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -585,7 +643,13 @@ def main():
                        "dense_floor_us": dense_floor_s * 1e6, "dense_gflop_per_step": gflop,
                        "frac": floor_s / (ms_per_step * 1e-3),
                        "formula": "sum_k max(B_k/8 TB/s, F_k/peak_k) / t_step over the step's edge, head-"
-                                  "projection and FFN work (bench.step_work)"},
+                                  "projection and FFN work (bench.step_work)",
+                       "floor_issued_us": floor_i * 1e6, "dense_floor_issued_us": dense_floor_i * 1e6,
+                       "frac_issued": floor_i / (ms_per_step * 1e-3),
+                       "frac_issued_is": "the same floor with the dense work priced at the rate the path issues "
+                                         "it: the fp32-accurate GEMMs as 6 bf16 limb products each at the bf16 "
+                                         "MFMA peak (2.5 PF/s), i.e. 417 TF/s fp32-equivalent, the exact-f32 "
+                                         "kernels (head projection, narrow FFN) at 157 TF/s"},
         "roofline_dense": dense_roofline(d_name, rel_s.n_dst, d_tf, d_flops, d_ms, args.dtype),
     }
     if traffic_rec is not None:
@@ -607,7 +671,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

@@ -120,6 +120,26 @@ def flat_gradients(params):
     return torch.empty(0, dtype=grads[0].dtype, device=grads[0].device).set_(st, 0, (total,))
 
 
+def reduce_flat(flat, group=None, scale=None):
+    """All-reduce ONE flat gradient buffer in place: sum_r scale_r * g_r when
+    ``scale`` (this rank's :func:`shard_fraction`) is given, else the mean.  No
+    world-size-1 short cut, no host synchronisation and no allocation, so on the
+    nccl (RCCL) backend it can be captured into the step's HIP graph after the
+    backward (bench.py replays step + exchange as one graph; the communicator must
+    have run one collective before the capture)."""
+    if scale is not None:
+        if scale != 1.0:
+            flat.mul_(scale)                    # weighted sum = global-batch mean
+        op = dist.ReduceOp.SUM
+    elif dist.get_backend(group) == "nccl":
+        op = dist.ReduceOp.AVG                  # RCCL averages natively
+    else:
+        op = dist.ReduceOp.SUM
+    dist.all_reduce(flat, op=op, group=group)
+    if scale is None and op == dist.ReduceOp.SUM:
+        flat.div_(dist.get_world_size(group))
+
+
 def allreduce_gradients(params, group=None, bucket_bytes=2 << 20, scale=None):
     """Reduce ``p.grad`` over the process group in flat buckets of at most
     ``bucket_bytes`` (all issued asynchronously, then waited): the mean when
@@ -135,16 +155,7 @@ def allreduce_gradients(params, group=None, bucket_bytes=2 << 20, scale=None):
     if flat is not None:
         # the gradients already form one flat buffer: reduce it in place (no cat /
         # copy-back); the doc-weighted sum scales it first (one elementwise pass)
-        if scale is not None:
-            flat.mul_(scale)
-            op = dist.ReduceOp.SUM
-        elif dist.get_backend(group) == "nccl":
-            op = dist.ReduceOp.AVG
-        else:
-            op = dist.ReduceOp.SUM
-        dist.all_reduce(flat, op=op, group=group)
-        if scale is None and op == dist.ReduceOp.SUM:
-            flat.div_(world)
+        reduce_flat(flat, group, scale)
         return
     grads = [p.grad for p in params if p.grad is not None]
     pending = [_launch(b, scale, world, group) for b in _buckets(grads, bucket_bytes)]
@@ -188,6 +199,7 @@ class GradientReducer:
             for p in b:
                 self.where[id(p)] = bi
         self.ready = [0] * len(self.buckets)
+        self.seen = set()                    # parameters whose hook fired since the last finish()
         self.next = 0                        # next bucket to launch
         self.pending = []
         self._sync = True
@@ -215,9 +227,12 @@ class GradientReducer:
         if not self._sync:
             return
         bi = self.where[id(p)]
-        if self.next == len(self.buckets) or self.ready[bi] >= len(self.buckets[bi]):
+        # a parameter's hook firing twice before finish() is a second backward, even
+        # when the first one left its bucket incomplete (a parameter without gradient)
+        if id(p) in self.seen or self.next == len(self.buckets) or self.ready[bi] >= len(self.buckets[bi]):
             raise RuntimeError("GradientReducer: a second backward before finish() -- its gradients would not "
                                "be reduced; run the earlier micro-batches under no_sync()")
+        self.seen.add(id(p))
         self.ready[bi] += 1
         while self.next < len(self.buckets) and self.ready[self.next] == len(self.buckets[self.next]):
             self._launch_next()
@@ -232,6 +247,7 @@ class GradientReducer:
         self.pending = []
         self.next = 0
         self.ready = [0] * len(self.buckets)
+        self.seen = set()
         return self.params
 
     def remove(self):

@@ -249,14 +249,14 @@ class _GatStack(torch.autograd.Function):
         if fold is not None:
             for lay in (w2s, s2w):
                 d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
-                r = ffn_wsplit(w0.new_empty(1, d), lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2,
-                               launch=False)
+                args = (w0.new_empty(1, d), lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2)
+                if split_job is not None:           # a second wide FFN: its own launch
+                    wsplits[id(lay)] = ffn_wsplit(*args)
+                    continue
+                r = ffn_wsplit(*args, launch=False)
                 wsplits[id(lay)] = r[0] if r is not None else None
-                if r is not None and split_job is None:
+                if r is not None:
                     split_job = r[1]
-                elif r is not None:                  # a second wide FFN: its own launch
-                    wsplits[id(lay)] = ffn_wsplit(w0.new_empty(1, d), lay.w1.view(d_hid, d), lay.b1,
-                                                  lay.w2.view(d, d_hid), lay.b2)
             mlist, wt_fold = dropmasks(jobs, w0.device, stream_of(w0), wt=(fold.W, fold.H, fold.D),
                                        wsplit_job=split_job)
         else:

@@ -223,6 +223,18 @@ def main():
                  "vocab_size": np.array(2000)}
         np.savez_compressed(os.path.join(HERE, "model_hsg_cfg1.npz"), **graph_arrays(cdocs), **compact(res),
                             **extra, **meta)
+    if want("model_hsg_cfg1_n1"):
+        # the same 4 config-1-shaped documents through HSumGraph at train.py's own
+        # default n_iter = 1 (train.py:282): W2S, then ONE (S2W, W2S) round
+        rng = np.random.default_rng(15)
+        cdocs = sort_by_sentences([synth.make_hsg_doc(rng, N=30, W=400, k=20, vocab_size=2000)
+                                   for _ in range(4)])
+        res = model_case(HiGraph, cdocs, 7, "HSumGraph", vocab_size=2000, n_iter=1)
+        extra = {"sent_words": np.concatenate([d.words for d in cdocs]).astype(np.int32),
+                 "sent_label": np.concatenate([d.label for d in cdocs]).astype(np.int8),
+                 "vocab_size": np.array(2000), "n_iter": np.array(1)}
+        np.savez_compressed(os.path.join(HERE, "model_hsg_cfg1_n1.npz"), **graph_arrays(cdocs), **compact(res),
+                            **extra, **meta)
     if args.only is not None:
         return
 

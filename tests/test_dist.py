@@ -92,6 +92,18 @@ def _worker(rank, world, port, bucket_bytes, skewed, hooks, accum=False):
                 _loss(mine, extra, T).backward()
             red2.finish()
             red2.remove()
+            # the same when the first backward left a bucket incomplete (a
+            # parameter that got no gradient): the repeated hook still raises
+            extra3 = _params()
+            unused = torch.zeros(3, dtype=torch.float64, requires_grad=True)
+            red3 = GradientReducer([unused] + list(extra3.values()), bucket_bytes=1 << 30, scale=scale)
+            assert len(red3.buckets) == 1
+            _loss(mine, extra3, T).backward()
+            assert red3.next == 0                    # the bucket waits for `unused`
+            with pytest.raises(RuntimeError, match="second backward"):
+                _loss(mine, extra3, T).backward()
+            red3.finish()
+            red3.remove()
             red.remove()
         elif hooks:
             red = GradientReducer(list(local.values()), bucket_bytes=bucket_bytes, scale=scale)

@@ -34,6 +34,50 @@ def test_psw_elug_matches_fp64(M, N, K):
     assert (G.double() - gexact).abs().max().item() <= 2e-4 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_psw_elug_gate_from_large_origin(mode):
+    """the gate elu'(h) = exp(h) (h <= 0) comes from e = x - origin, so
+    its absolute error is ~ulp(origin) whatever exp(h) is: relative accuracy of
+    exp(h) is lost for strongly negative h beside a large residual.  Pinned here on
+    rows with |origin| >> |elu(h)| (|origin| up to ~200, h down to -14) against
+    fp64 dOut * elu'(h) from the TRUE h, in both GEMM modes.  Bound: the gate's
+    error stays within 4 ulp(|x| + |origin|) (the fp32 rounding of x and of the
+    subtraction), i.e. |G - G_exact| <= |dOut| * 4 * 2^-23 * (|x| + |origin|) +
+    the dx GEMM's own error (fp32-class, or bf16-operand in 'bf16' mode)."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    M, N, K = 4096, 300, 512
+    torch.manual_seed(7)
+    dH = torch.randn(M, K, device="cuda")
+    W1 = torch.randn(K, N, device="cuda") / K ** 0.5
+    with gemm_dtype(mode):
+        (S,) = split_weights((W1, True))
+    assert S.mode == mode
+    ds = torch.randn(M, N, device="cuda")
+    origin = 50 * torch.randn(M, N, device="cuda")
+    h = torch.empty(M, N, device="cuda").uniform_(-14.0, 2.0)
+    x = torch.nn.functional.elu(h) + origin
+    out = ds.clone()
+    G = torch.empty_like(ds)
+    assert gemm_psw_elug(dH, S, out, x, origin, G)
+    if mode == "bf16":      # the GEMM itself on bf16-rounded operands (hsg_gemm_bf16 semantics)
+        ref = ds.double() + dH.bfloat16().double() @ W1.bfloat16().double()
+    else:
+        ref = ds.double() + dH.double() @ W1.double()
+    scale = max(1.0, ref.abs().max().item())
+    tol_gemm = 1e-4 * scale if mode == "f32" else 2e-2 * scale
+    assert (out.double() - ref).abs().max().item() <= tol_gemm
+    gate = torch.where(h.double() > 0, torch.ones_like(ref), torch.exp(h.double()))
+    gexact = out.double() * gate                 # the exact gate on the dx the kernel produced
+    gate_err = 4 * 2.0 ** -23 * (x.double().abs() + origin.double().abs())
+    bound = out.double().abs() * gate_err + 1e-12
+    excess = ((G.double() - gexact).abs() - bound).max().item()
+    neg = h < -8
+    rel_neg = ((G.double() - gexact).abs() / gexact.abs().clamp_min(1e-30))[neg].max().item()
+    print(f"{mode}: worst |G - G_exact| beyond bound {excess:.3e}; relative error of the gate at h < -8: "
+          f"{rel_neg:.2e} (absolute, not relative, accuracy is the contract)")
+    assert excess <= 0.0
+
+
 def test_psw_elug_declines_unaligned():
     from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
     W1 = torch.randn(64, 30, device="cuda")

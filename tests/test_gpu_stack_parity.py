@@ -39,7 +39,7 @@ from helpers import build_graph, concat_arrays, gat_inputs, seeded_gat_params, s
 
 pytestmark = pytest.mark.gpu
 
-N_ITER = 2
+N_ITER = 2          # the bench's n_iter; train.py's own default is 1 (train.py:282), pinned below too
 
 
 def _f64(t):
@@ -71,14 +71,14 @@ def check_grad(fails, name, got, ref, fro_tol, bad_frac, worst_tol, scale_ref=No
         fails.append((name, s))
 
 
-def train_masks(drop_seed, off0, n_w, n_s, p=0.1):
+def train_masks(drop_seed, off0, n_w, n_s, p=0.1, n_iter=N_ITER):
     """The keep-masks of the fused stack's forward, application by application
     (W2S, then n_iter x (S2W, W2S)), in the order stack._GatStack draws them: per
     application one head-projection call (offset +1) then one FFN call (+1)."""
     from oracle import masks
     hs, fs = masks.hproj_scale(p), masks.ffn_scale(p)
     out, off = [], off0
-    for kind in ["W2S"] + ["S2W", "W2S"] * N_ITER:
+    for kind in ["W2S"] + ["S2W", "W2S"] * n_iter:
         n_src, d_in, H, n_dst, d = (n_w, 300, 8, n_s, 64) if kind == "W2S" else (n_s, 64, 6, n_w, 300)
         hk = masks.hproj_keep(drop_seed, off + 1, n_src, d_in, H, p)
         fk = masks.ffn_keep(drop_seed, off + 2, n_dst, d, p)
@@ -87,7 +87,7 @@ def train_masks(drop_seed, off0, n_w, n_s, p=0.1):
     return out
 
 
-def oracle_stack(z, seed, masks=None):
+def oracle_stack(z, seed, masks=None, n_iter=N_ITER):
     """fp64 oracle: s1 = W2S(w0, s0); then n_iter x (w = S2W(w, s); s = W2S(w, s)).
     ``masks``: train mode, one (head keep, scale, FFN keep, scale) per application."""
     from oracle import fused
@@ -101,7 +101,7 @@ def oracle_stack(z, seed, masks=None):
     m = iter(masks) if masks is not None else None
     nxt = (lambda: next(m)) if m is not None else (lambda: None)
     w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T, masks=nxt())
-    for _ in range(N_ITER):
+    for _ in range(n_iter):
         w = fused.wswgat_layer("S2W", rsw, w, s, p2, T, masks=nxt())
         s = fused.wswgat_layer("W2S", rws, w, s, p1, T, masks=nxt())
     R = torch.from_numpy(np.random.default_rng(seed).standard_normal(tuple(s.shape)))
@@ -109,7 +109,7 @@ def oracle_stack(z, seed, masks=None):
     return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, p1=p1, p2=p2, R=R)
 
 
-def gpu_stack(z, seed, R, train_seed=None):
+def gpu_stack(z, seed, R, train_seed=None, n_iter=N_ITER):
     """The fused stack on the GPU; ``train_seed``: train mode (dropout 0.1) with the
     dropout stream reseeded to it (returns the offset the stack's draws start at)."""
     from hetersumgraph_amd.HiGraph import register_tfidf_table
@@ -131,16 +131,18 @@ def gpu_stack(z, seed, R, train_seed=None):
         rng.manual_seed(train_seed)
         off0 = rng.get(dev).offset
     assert fused_stack_ok(G, w2s, s2w, T, Xw, Xs)
-    s = gat_stack(G, w2s, s2w, T, Xw, Xs, N_ITER)
+    s = gat_stack(G, w2s, s2w, T, Xw, Xs, n_iter)
     if train_seed is not None:
-        assert rng.get(dev).offset == off0 + 2 * (2 * N_ITER + 1)     # one head + one FFN draw per application
+        assert rng.get(dev).offset == off0 + 2 * (2 * n_iter + 1)     # one head + one FFN draw per application
     assert type(s.grad_fn).__name__.startswith("_GatStack")        # the timed node, not the layer path
     s.backward(R.to(dev, torch.float32))
     torch.cuda.synchronize()
     return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w, off0=off0)
 
 
-CASES = [("cfg2", "f32", 31), ("cfg4", "f32", 32), ("cfg5", "f32", 33), ("cfg5", "bf16", 33)]
+# (config, GEMM dtype, seed, n_iter): n_iter 2 is the bench's, 1 train.py's default
+CASES = [("cfg2", "f32", 31, 2), ("cfg4", "f32", 32, 2), ("cfg5", "f32", 33, 2), ("cfg5", "bf16", 33, 2),
+         ("cfg2", "f32", 35, 1)]
 
 
 def compare(config, dtype, r, o, n_docs, n_edges):
@@ -179,24 +181,25 @@ def compare(config, dtype, r, o, n_docs, n_edges):
     assert not fails, fails
 
 
-@pytest.mark.parametrize("config,dtype,seed", CASES)
-def test_stack_vs_oracle_full_size(config, dtype, seed):
+@pytest.mark.parametrize("config,dtype,seed,n_iter", CASES)
+def test_stack_vs_oracle_full_size(config, dtype, seed, n_iter):
     from hetersumgraph_amd import synth
     from hetersumgraph_amd.dense import gemm_dtype
     docs = synth.make_batch_docs(config, seed=0)
     z = synth_fixture(docs)
     n_edges = int(z["g_n_edges"].sum())
-    o = oracle_stack(z, seed)
+    o = oracle_stack(z, seed, n_iter=n_iter)
     with gemm_dtype(dtype):
-        r = gpu_stack(z, seed, o["R"])
+        r = gpu_stack(z, seed, o["R"], n_iter=n_iter)
     compare(config, dtype, r, o, len(docs), n_edges)
 
 
-TRAIN_CASES = [("cfg2", "f32", 41), ("cfg4", "f32", 42), ("cfg5", "f32", 43), ("cfg5", "bf16", 44)]
+TRAIN_CASES = [("cfg2", "f32", 41, 2), ("cfg4", "f32", 42, 2), ("cfg5", "f32", 43, 2), ("cfg5", "bf16", 44, 2),
+               ("cfg2", "f32", 45, 1)]
 
 
-@pytest.mark.parametrize("config,dtype,seed", TRAIN_CASES)
-def test_train_stack_vs_oracle_full_size(config, dtype, seed):
+@pytest.mark.parametrize("config,dtype,seed,n_iter", TRAIN_CASES)
+def test_train_stack_vs_oracle_full_size(config, dtype, seed, n_iter):
     """The timed configuration: train mode, dropout 0.1 (head inputs and FFN outputs),
     the fused stack's kernels (hsg_dropmask_multi, the head-projection forward with
     the sigma epilogue, hsg_hproj_dx / _dw through the same bits, the masked LN /
@@ -210,8 +213,8 @@ def test_train_stack_vs_oracle_full_size(config, dtype, seed):
     drop_seed = 1000 + seed
     R = torch.from_numpy(np.random.default_rng(seed).standard_normal((int(z["n_s"]), 64)))
     with gemm_dtype(dtype):
-        r = gpu_stack(z, seed, R, train_seed=drop_seed)
-    ms = train_masks(drop_seed, r["off0"], int(z["n_w"]), int(z["n_s"]))
-    o = oracle_stack(z, seed, masks=ms)
+        r = gpu_stack(z, seed, R, train_seed=drop_seed, n_iter=n_iter)
+    ms = train_masks(drop_seed, r["off0"], int(z["n_w"]), int(z["n_s"]), n_iter=n_iter)
+    o = oracle_stack(z, seed, masks=ms, n_iter=n_iter)
     assert torch.equal(o["R"], R)
     compare(config, dtype, r, o, len(docs), n_edges)
