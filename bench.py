@@ -405,6 +405,11 @@ def cpu_baseline(docs, args, stack):
 
 def main():
     args = parse()
+    # stdout carries exactly ONE JSON line (rank 0): anything libraries print there
+    # (RCCL's version banner at communicator init, for one) goes to stderr instead
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -670,7 +675,8 @@ def main():
         except Exception as exc:  # pragma: no cover
             out["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dp:
         dist.destroy_process_group()
 

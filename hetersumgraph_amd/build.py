@@ -4,6 +4,11 @@ hipcc cross-compiles without a GPU; the .so lands next to this file so that it
 travels with the repository snapshot to the GPU box.  Each source compiles to its
 own object in parallel (no cross-file device symbols, so no -fgpu-rdc), then one
 link step.
+
+``--dev`` (or HSG_DEV_BUILD=1) builds ``libhsg_dev.so`` instead, with HSG_DEV
+defined (csrc/hsg_dev.h): the A/B switches read the environment and the rejected
+variants are compiled in.  The tools load it through ``HSG_LIB_PATH``; the product
+``libhsg.so`` carries the default kernels only.
 """
 import os
 import subprocess
@@ -15,8 +20,11 @@ ROOT = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip", "hsg_cnn.hip", "hsg_ffn.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
+DEV_OUT = os.path.join(HERE, "libhsg_dev.so")
+DEV_OBJDIR = os.path.join(ROOT, "build", "obj_dev")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
-HEADERS = [os.path.join(ROOT, "include", "hsg.h"), os.path.join(HERE, "csrc", "hsg_rng.h")]
+HEADERS = [os.path.join(ROOT, "include", "hsg.h")] + [os.path.join(HERE, "csrc", h) for h in
+                                                      ("hsg_rng.h", "hsg_wsplit.h", "hsg_dev.h")]
 # host-only graph builder (no HIP runtime: usable in DataLoader workers)
 HOST_SOURCES = [os.path.join(HERE, "csrc", "hsg_graphbuild.cpp")]
 HOST_HEADERS = [os.path.join(ROOT, "include", "hsg_graph.h")]
@@ -30,16 +38,17 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def needs_build():
-    if not os.path.exists(OUT):
+def needs_build(dev=False):
+    out = DEV_OUT if dev else OUT
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(s) > t for s in SOURCES + HEADERS)
 
 
-def _flags():
+def _flags(dev=False):
     return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
-            "-I", os.path.join(ROOT, "include")]
+            "-I", os.path.join(ROOT, "include")] + (["-DHSG_DEV"] if dev else [])
 
 
 # per-file extra flags: the narrow-head projection wants plain v_fmac_f32 (SGPR weight
@@ -47,17 +56,17 @@ def _flags():
 FILE_FLAGS = {"hsg_hproj.hip": ["-fno-slp-vectorize"]}
 
 
-def _obj(src):
-    return os.path.join(OBJDIR, os.path.basename(src).replace(".hip", ".o"))
+def _obj(src, dev=False):
+    return os.path.join(DEV_OBJDIR if dev else OBJDIR, os.path.basename(src).replace(".hip", ".o"))
 
 
-def _compile(src, force, verbose):
-    obj = _obj(src)
+def _compile(src, force, verbose, dev=False):
+    obj = _obj(src, dev)
     if not force and os.path.exists(obj):
         t = os.path.getmtime(obj)
         if os.path.getmtime(src) <= t and all(os.path.getmtime(h) <= t for h in HEADERS):
             return obj
-    cmd = [hipcc()] + _flags() + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj + ".tmp"]
+    cmd = [hipcc()] + _flags(dev) + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -80,21 +89,24 @@ def build_host(force=False, verbose=True):
     return HOST_OUT
 
 
-def build(force=False, verbose=True):
+def build(force=False, verbose=True, dev=None):
+    if dev is None:
+        dev = os.environ.get("HSG_DEV_BUILD", "0") == "1"
     build_host(force=force, verbose=verbose)
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(OBJDIR, exist_ok=True)
+    out = DEV_OUT if dev else OUT
+    if not force and not needs_build(dev):
+        return out
+    os.makedirs(DEV_OBJDIR if dev else OBJDIR, exist_ok=True)
     jobs = min(len(SOURCES), os.cpu_count() or 1, 8)
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force, verbose), SOURCES))
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
+        objs = list(ex.map(lambda s: _compile(s, force, verbose, dev), SOURCES))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, dev=True if "--dev" in sys.argv else None)

@@ -24,6 +24,7 @@
 #include <stdlib.h>
 
 #include "../../include/hsg.h"
+#include "hsg_dev.h"
 
 #define HSG_HMAX 16          // max heads (reference: 8 for W2S, 6 for S2W)
 #define HSG_NT 11            // tau table rows: 10 tf-idf boxes + zero row
@@ -74,11 +75,32 @@ struct RelPtrs {
     const int32_t *__restrict__ cindptr;
     const int32_t *__restrict__ cdst;
     const int32_t *__restrict__ cperm;
+    int xcd;                 // 1: XCD-local node order (work_range)
 };
 
+// XCD-local node order (round 4).  The batched graph is a disjoint union of documents
+// with node ids document by document (dataloader.py:480), so a node's neighbours --
+// the rows its segment gathers -- lie in its own document, near it in rank order.
+// Workgroup b is dispatched to XCD b % 8 (round robin; the map is not guaranteed, so
+// this is for locality only and any placement stays correct): with a grid that is a
+// multiple of 8, XCD x walks the contiguous eighth [s_x, e_x) of the n nodes, so each
+// XCD's 4 MB L2 fetches only its own documents' rows instead of every XCD fetching
+// all of them (S2W: the Z / sigma table 8 times over; W2S and the src passes: the
+// rows shared by a document's nodes once per XCD that touches them).
+struct WorkRange { int first, end, stride; };
+__device__ __forceinline__ WorkRange work_range(int n, int npb, int slot, int xcd) {
+    const int g = (int)gridDim.x, b = (int)blockIdx.x;
+    if (!xcd || (g & 7)) return WorkRange{b * npb + slot, n, g * npb};
+    const int x = b & 7, j = b >> 3, per = n >> 3, rem = n & 7;
+    const int s = x * per + min(x, rem);
+    return WorkRange{s + j * npb + slot, s + per + (x < rem ? 1 : 0), (g >> 3) * npb};
+}
+
 RelPtrs rel_ptrs(const hsg_rel *r) {
+    int xcd = 1;
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_XCD")) xcd = atoi(e);      // dev A/B
     return RelPtrs{r->n_src, r->n_dst, r->n_edges, r->indptr, r->src, r->tf, r->phantom,
-                   r->cindptr, r->cdst, r->cperm};
+                   r->cindptr, r->cdst, r->cperm, xcd};
 }
 
 template <int TAU_MODE>
@@ -167,13 +189,14 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     int *sn = s_nb[wid];
 
     static_assert(PF == 0 || WPN == 1, "prefetch: one destination per wave");
-    const int vstride = gridDim.x * NPB;
+    const WorkRange wr = work_range(R.n_dst, NPB, wid / WPN, R.xcd);
+    const int vstride = wr.stride;
     int pf_beg = 0, pf_end = 0, pf_c = 0;
     if constexpr (PF) {
-        const int v0 = blockIdx.x * NPB + wid / WPN;
-        if (v0 < R.n_dst) { pf_beg = R.indptr[v0]; pf_end = R.indptr[v0 + 1]; pf_c = R.phantom[v0]; }
+        const int v0 = wr.first;
+        if (v0 < wr.end) { pf_beg = R.indptr[v0]; pf_end = R.indptr[v0 + 1]; pf_c = R.phantom[v0]; }
     }
-    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += vstride) {
+    for (int v_ = wr.first; v_ < wr.end; v_ += vstride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
         int beg, end, c;
         float org[NF];
@@ -187,7 +210,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
 #pragma unroll
             for (int i = 0; i < NF; ++i) org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
             const int vn = v_ + vstride;
-            if (vn < R.n_dst) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
+            if (vn < wr.end) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
         } else {
             beg = R.indptr[v];
             end = R.indptr[v + 1];
@@ -601,7 +624,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_ep(RelPtrs R, int H, int D,
 #pragma unroll
     for (int t = 0; t < HSG_NT; ++t) dt[t] = 0.f;
 
-    for (int v_ = blockIdx.x * NPB + wid / WPN; v_ < R.n_dst; v_ += gridDim.x * NPB) {
+    const WorkRange wr = work_range(R.n_dst, NPB, wid / WPN, R.xcd);
+    for (int v_ = wr.first; v_ < wr.end; v_ += wr.stride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
         const int beg = R.indptr[v], end = R.indptr[v + 1];
         const float M = kact ? mv[v * H + k] : 0.f;             // issued early: independent
@@ -705,7 +729,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_dst(RelPtrs R, int H, int 
         wave_lds_sync();
     }
 
-    for (int v_ = blockIdx.x * HSG_WAVES + wid; v_ < R.n_dst; v_ += gridDim.x * HSG_WAVES) {
+    const WorkRange wr = work_range(R.n_dst, HSG_WAVES, wid, R.xcd);
+    for (int v_ = wr.first; v_ < wr.end; v_ += wr.stride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);
         const int beg = R.indptr[v], end = R.indptr[v + 1];
         // softmax state of v: independent of everything below, issued first
@@ -911,7 +936,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
 #pragma unroll
     for (int i = 0; i < NF; ++i) da1[i] = 0.f;
 
-    for (int u_ = blockIdx.x * NPB + wid / WPN; u_ < R.n_src; u_ += gridDim.x * NPB) {
+    const WorkRange wr = work_range(R.n_src, NPB, wid / WPN, R.xcd);
+    for (int u_ = wr.first; u_ < wr.end; u_ += wr.stride) {
         const int u = __builtin_amdgcn_readfirstlane(u_);
         const int beg = R.cindptr[u], end = R.cindptr[u + 1];
         int eb, ee;
@@ -1042,7 +1068,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
         a1v[q] = a1 ? *reinterpret_cast<const f4 *>(a1 + kc * D + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
         da1[q] = f4{0.f, 0.f, 0.f, 0.f};
     }
-    for (int u0 = (blockIdx.x * HSG_WAVES + wid) * wpw; u0 < R.n_src; u0 += gridDim.x * HSG_WAVES * wpw) {
+    const WorkRange wr = work_range((R.n_src + wpw - 1) / wpw, HSG_WAVES, wid, R.xcd);   // in wave groups
+    for (int q0 = wr.first; q0 < wr.end; q0 += wr.stride) {
+        const int u0 = q0 * wpw;
         const int u = u0 + sl;
         const bool act = kact && u < R.n_src;
         const int uc = act ? u : 0;
@@ -1148,7 +1176,7 @@ constexpr int kLongSegment = 16;       // mean segment length from which 4 waves
 // waves per node for a set of n nodes sharing n_edges edges
 int wpn_for(int n, int n_edges) { return n > 0 && n_edges >= kLongSegment * n ? 4 : 1; }
 int grid_nodes(int n, int wpn, int cap) {
-    if (const char *e = getenv("HSG_GAT_CAP")) cap = atoi(e) < cap ? atoi(e) : cap;   // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_CAP")) cap = atoi(e) < cap ? atoi(e) : cap;   // dev sweep
     int b = wpn == 4 ? n : (n + HSG_WAVES - 1) / HSG_WAVES;
     if (b < 1) b = 1;
     return b < cap ? b : cap;
@@ -1250,7 +1278,7 @@ int fwd_grp_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
 int fwd_lanes_per_node(const hsg_rel *r, int H, int D) {
     int lpn = 64;
     const int HD = H * D;
-    if (const char *e = getenv("HSG_GAT_LPN")) lpn = atoi(e);
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_LPN")) lpn = atoi(e);
     if (lpn != 16 && lpn != 32) lpn = 64;
     if (lpn < 64 && (grp_nf_bucket((HD + lpn - 1) / lpn, lpn) < 0 || next_pow2(H) > lpn)) lpn = 64;
     return lpn;
@@ -1266,7 +1294,7 @@ RowsPlan rows_plan(int H, int D, bool aligned) {
     // one destination per wave (tools/gat_fwd_lpn.py): the per-(row, head) index ->
     // score chain of phase A costs more latency than the float4 band saves.
     int force = 0;
-    if (const char *e = getenv("HSG_GAT_ROWS")) force = atoi(e);
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_ROWS")) force = atoi(e);
     if (force == 0) return best;
     const int HD = H * D;
     // a 4-column slot must not span more than two heads: D >= 2 (D = 2 slots are head-aligned)
@@ -1275,7 +1303,7 @@ RowsPlan rows_plan(int H, int D, bool aligned) {
     static const int nqs[] = {1, 2, 3, 4, 5, 6, 8};
     double best_u = 0.0;
     int rt_force = 0;                                   // dev sweep: rows per block
-    if (const char *e = getenv("HSG_GAT_ROWS_RT")) rt_force = atoi(e);
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_ROWS_RT")) rt_force = atoi(e);
     for (int nq : nqs) {
         if (force > 0 && nq != force) continue;
         int rt = kRowsThreads * nq / hd4;
@@ -1312,7 +1340,7 @@ bool aligned16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
 // no spill) and of the 4-waves-per-node src pass (5: 101 -> 90); HSG_GAT_BWD_OCC=0
 // drops them.  cfg2 S2W backward 61.2 -> 56.1 us per step in one A/B.
 bool bwd_occ() {
-    const char *e = getenv("HSG_GAT_BWD_OCC");
+    const char *e = HSG_DEV_ENV("HSG_GAT_BWD_OCC");
     return !(e && atoi(e) == 0);
 }
 
@@ -1320,7 +1348,7 @@ bool bwd_occ() {
 // forward 17.8 -> 17.2 us in-step, step 1.3084 -> 1.3049 ms in one A/B (round 3);
 // HSG_GAT_FWD_PF=0 drops it
 int fwd_pf() {
-    const char *e = getenv("HSG_GAT_FWD_PF");
+    const char *e = HSG_DEV_ENV("HSG_GAT_FWD_PF");
     return e && atoi(e) == 0 ? 0 : 1;
 }
 
@@ -1328,7 +1356,7 @@ int fwd_pf() {
 // VGPRs, no spill; the SGPR count admits 7 blocks per CU); HSG_GAT_FWD_OCC=1 drops it
 int fwd_occ() {
     int o = 7;
-    if (const char *e = getenv("HSG_GAT_FWD_OCC")) o = atoi(e);
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_FWD_OCC")) o = atoi(e);
     return o == 7 || o == 8 ? o : 1;
 }
 
@@ -1413,6 +1441,7 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     if (rel->n_dst == 0) return 0;
     const RelPtrs R = rel_ptrs(rel);
     hipStream_t st = (hipStream_t)stream;
+#ifdef HSG_DEV
     const int lpn = fwd_lanes_per_node(rel, H, D);
     if (lpn < 64) {
         const int ng = 256 / lpn;
@@ -1424,8 +1453,10 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
         return lpn == 32 ? HSG_G(HSG_TAU_PER_EDGE, 32) : HSG_G(HSG_TAU_PER_EDGE, 16);
 #undef HSG_G
     }
+#endif
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
+#ifdef HSG_DEV
     if (wpn == 1) {                      // short segments: row-tile float4 kernel
         const bool al = aligned16p(Z) && aligned16p(h) && (!origin || (aligned16p(origin) && aligned16p(out)));
         const RowsPlan pl = rows_plan(H, D, al);
@@ -1435,37 +1466,52 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
             return fwd_rows_dispatch<HSG_TAU_PER_EDGE>(pl, st, R, H, D, slope, Z, sigma, tau, origin, h, out, m, l);
         }
     }
+#endif
     // one destination per wave: one persistent wave of blocks (256 CUs x the 7 blocks
     // the w = 7 kernel keeps resident; cfg2 S2W forward 24.8 -> 22.4 us per step)
     int fcap = wpn == 1 && fwd_occ() == 7 ? kFwdPersistentCap : kFwdGridCap;
-    if (const char *e = getenv("HSG_GAT_FWD_CAP")) fcap = atoi(e) > 0 ? atoi(e) : fcap;   // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_FWD_CAP")) fcap = atoi(e) > 0 ? atoi(e) : fcap;   // dev sweep
     const dim3 grid(grid_nodes(rel->n_dst, wpn, fcap));
     const int lph = lanes_per_head(H);
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
         const int pf = fwd_pf();
-        if (pf == 1) {
+        if (pf == 1 || occ != 8) {
+#ifdef HSG_DEV
+            if (pf != 1) {
+                if (tau_mode == HSG_TAU_TABLE)
+                    return fwd_dispatch<HSG_TAU_TABLE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                             origin, h, out, m, l);
+                return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                            origin, h, out, m, l);
+            }
+#endif
             if (tau_mode == HSG_TAU_TABLE)
                 return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                             origin, h, out, m, l);
             return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                            origin, h, out, m, l);
         }
+#ifdef HSG_DEV
 #define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
-        if (tau_mode == HSG_TAU_TABLE) return occ == 8 ? HSG_FO(HSG_TAU_TABLE, 8) : HSG_FO(HSG_TAU_TABLE, 7);
-        return occ == 8 ? HSG_FO(HSG_TAU_PER_EDGE, 8) : HSG_FO(HSG_TAU_PER_EDGE, 7);
+        if (tau_mode == HSG_TAU_TABLE) return HSG_FO(HSG_TAU_TABLE, 8);
+        return HSG_FO(HSG_TAU_PER_EDGE, 8);
 #undef HSG_FO
+#endif
     }
 #define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
-    if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_F(HSG_TAU_TABLE, 4) : HSG_F(HSG_TAU_TABLE, 1);
-    return wpn == 4 ? HSG_F(HSG_TAU_PER_EDGE, 4) : HSG_F(HSG_TAU_PER_EDGE, 1);
+#ifdef HSG_DEV
+    if (wpn == 1) return tau_mode == HSG_TAU_TABLE ? HSG_F(HSG_TAU_TABLE, 1) : HSG_F(HSG_TAU_PER_EDGE, 1);
+#endif
+    if (tau_mode == HSG_TAU_TABLE) return HSG_F(HSG_TAU_TABLE, 4);         // wpn == 1 took the w = 7 kernel above
+    return HSG_F(HSG_TAU_PER_EDGE, 4);
 #undef HSG_F
 }
 
 int hsg_gat_bwd_blocks(const hsg_rel *rel) {
     if (!rel) return 0;
     int cap = kBwdDstGridCap;
-    if (const char *e = getenv("HSG_GAT_BWD_CAP")) cap = atoi(e) > 0 ? atoi(e) : cap;   // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_BWD_CAP")) cap = atoi(e) > 0 ? atoi(e) : cap;   // dev sweep
     return grid_nodes(rel->n_dst, dst_wpn(rel), cap);
 }
 
@@ -1496,18 +1542,20 @@ int hsg_gat_bwd_dst(const hsg_rel *rel, int H, int D, int tau_mode, int origin_m
     // the same grid as above, the d tau slab's row count, with some idle waves)
     const int ne = ne_bucket((D + lph - 1) / lph);
     if (ne < 0) return HSG_EINVAL;
-    if (bwd_occ()) {
+#ifdef HSG_DEV
+    if (!bwd_occ()) {
         if (tau_mode == HSG_TAU_TABLE)
-            return bwd_dst_dispatch<HSG_TAU_TABLE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
-                                                      tau, h, m, l, dout, G, dpre, dtau_part);
-        return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
-                                                     sigma, tau, h, m, l, dout, G, dpre, dtau_part);
+            return bwd_dst_dispatch<HSG_TAU_TABLE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
+                                                   tau, h, m, l, dout, G, dpre, dtau_part);
+        return bwd_dst_dispatch<HSG_TAU_PER_EDGE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
+                                                  sigma, tau, h, m, l, dout, G, dpre, dtau_part);
     }
+#endif
     if (tau_mode == HSG_TAU_TABLE)
-        return bwd_dst_dispatch<HSG_TAU_TABLE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
-                                               tau, h, m, l, dout, G, dpre, dtau_part);
-    return bwd_dst_dispatch<HSG_TAU_PER_EDGE>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
-                                              sigma, tau, h, m, l, dout, G, dpre, dtau_part);
+        return bwd_dst_dispatch<HSG_TAU_TABLE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z, sigma,
+                                                  tau, h, m, l, dout, G, dpre, dtau_part);
+    return bwd_dst_dispatch<HSG_TAU_PER_EDGE, 6>(ne, grid, st, R, H, D, lph, origin_mode, slope, Z,
+                                                 sigma, tau, h, m, l, dout, G, dpre, dtau_part);
 }
 
 int hsg_gat_bwd_dst_noh_supported(const hsg_rel *rel, int H, int D) {
@@ -1532,10 +1580,12 @@ int hsg_gat_bwd_dst_noh(const hsg_rel *rel, int H, int D, int tau_mode, float sl
         return 0;
     }
     const int ne = ne_bucket((D + lph - 1) / lph);
-    const char *oe = getenv("HSG_GAT_NOH_OCC");                           // dev A/B
+#ifdef HSG_DEV
+    const char *oe = HSG_DEV_ENV("HSG_GAT_NOH_OCC");                      // dev A/B
     if (oe && atoi(oe) == 5 && tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE, 5, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
                                                         nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
+#endif
     if (tau_mode == HSG_TAU_TABLE)
         return bwd_dst_dispatch<HSG_TAU_TABLE, 6, true>(ne, grid, st, R, H, D, lph, 1, slope, Z, sigma, tau,
                                                         nullptr, m, l, dout, G, dpre, dtau_part, x, origin);
@@ -1587,7 +1637,7 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
     }
     const int wpn = src_wpn(rel), lph = lanes_per_head(H);
     // narrow heads over short segments: the head-lane kernel (HSG_GAT_SRC_HL=0: off)
-    const char *hl = getenv("HSG_GAT_SRC_HL");
+    const char *hl = HSG_DEV_ENV("HSG_GAT_SRC_HL");
     if (wpn == 1 && D == 8 && H <= 8 && !(hl && atoi(hl) == 0) && (((uintptr_t)G | (uintptr_t)dZ | (uintptr_t)Z |
                                                                  (uintptr_t)a1) & 15) == 0) {
         const int hp = next_pow2(H);
@@ -1608,8 +1658,11 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
     }
 #define HSG_S(TAU, W) bwd_src_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, sigma, tau, m, l, G, dpre, a1, \
                                                Z, dZ, dsigma, da1_part)
-    if (tau_mode == HSG_TAU_TABLE) return wpn == 4 ? HSG_S(HSG_TAU_TABLE, 4) : HSG_S(HSG_TAU_TABLE, 1);
-    return wpn == 4 ? HSG_S(HSG_TAU_PER_EDGE, 4) : HSG_S(HSG_TAU_PER_EDGE, 1);
+#ifdef HSG_DEV
+    if (wpn == 4) return tau_mode == HSG_TAU_TABLE ? HSG_S(HSG_TAU_TABLE, 4) : HSG_S(HSG_TAU_PER_EDGE, 4);
+#endif
+    if (tau_mode == HSG_TAU_TABLE) return HSG_S(HSG_TAU_TABLE, 1);      // wpn == 4 took the w = 5 kernel above
+    return HSG_S(HSG_TAU_PER_EDGE, 1);
 #undef HSG_S
 }
 
@@ -1631,6 +1684,10 @@ int hsg_kclock_arm(void *stream, void *start_event, void *stop_event) {
 
 int hsg_kclock_pending(void) { return (t_kc.start ? 1 : 0) + (t_kc.stop ? 2 : 0); }
 
+#ifdef HSG_DEV
+const char *hsg_version(void) { return "hsg 0.1 gfx950 (fp32 WSWGAT edge kernels) dev"; }
+#else
 const char *hsg_version(void) { return "hsg 0.1 gfx950 (fp32 WSWGAT edge kernels)"; }
+#endif
 
 }  // extern "C"

@@ -44,6 +44,7 @@
 #include <atomic>
 
 #include "../../include/hsg.h"
+#include "hsg_dev.h"
 #include "hsg_wsplit.h"
 
 namespace {
@@ -1539,7 +1540,7 @@ int launch_tiles(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
         });
         if (cap > 0 && cap < g) g = cap;
     }
-    if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
     if (ak && bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, true, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
     else if (ak && !bk) hipLaunchKernelGGL((k_gemm<BM, BN, true, false, NBUF, BK, BF>), grid, dim3(256), 0, st, p);
@@ -1555,7 +1556,7 @@ int launch3(GemmArgs p, bool ak, bool bk, int splits, hipStream_t st) {
     p.k_tiles_per_split = (kt_total + splits - 1) / splits;
     p.splits = splits;
     long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM) * splits;
-    if (const char *e = getenv("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_GEMM_GRID")) g = atol(e) < g ? atol(e) : g;   // dev sweep
     dim3 grid((unsigned)g);
     if (ak && bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, true, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
     else if (ak && !bk) hipLaunchKernelGGL((k_gemm3<BM, BN, true, false, BK, PF, NL, IGLP, NT>), grid, dim3(NT), 0, st, p);
@@ -1671,26 +1672,26 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
     if (splits > 1 && colsum_part) return HSG_EINVAL;     // column partials need the unsplit epilogue
     GemmArgs p{M, N, K, A, lda, B, ldb, C, ldc, bias, aux, ldaux, epi, relu,
                (kt_total + splits - 1) / splits, workspace, colsum_part, splits, 1};
-    if (const char *x = getenv("HSG_GEMM_XCD")) p.xcd = atoi(x);        // dev A/B switch
+    if (const char *x = HSG_DEV_ENV("HSG_GEMM_XCD")) p.xcd = atoi(x);        // dev A/B switch
     const bool ak = a_kcontig != 0, bk = b_kcontig != 0;
     int best = colsum_part ? 5 : plan_tile(M, N, K, splits);     // column partials: 64-row tiles
-    if (const char *f = getenv("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM_TILE"))      // dev override (tools/gemm_tiles.py)
         if (!colsum_part) best = atoi(f);
     int rc;
     // both operands M/N-contiguous (the weight gradients dW = dY^T X): the split path
     // with transpose-read staging, 64x64 tiles and the iglp_opt(0) interleave
     // (tools/gemm_dw3.py: 108-114 us against 129-142 us for the exact-f32 MFMA on the
-    // cfg2 S2W shapes); HSG_GEMM3_DW=0 selects the exact-f32 MFMA (A/B)
+    // cfg2 S2W shapes); HSG_GEMM3_DW=0 selects the exact-f32 MFMA (dev A/B)
     bool dw3 = false;
-    if (mode == MODE_F32_SPLIT && !ak && !bk && !getenv("HSG_GEMM3_TILE")) {
-        const char *e = getenv("HSG_GEMM3_DW");
+    if (mode == MODE_F32_SPLIT && !ak && !bk && !HSG_DEV_ENV("HSG_GEMM3_TILE")) {
+        const char *e = HSG_DEV_ENV("HSG_GEMM3_DW");
         if (e && e[0] == '0') mode = MODE_F32_MFMA;
         else dw3 = true;
     }
     // bf16 mode: the split kernel's plans with ONE limb (the RNE bf16 rounding of each
     // operand, one product) -- the same staging, tiles and transpose reads as the f32
-    // mode; HSG_GEMM_BF16_OLD=1 keeps the register-staged k_gemm<..., BF> tiles (A/B)
-    if (mode == MODE_BF16 && !getenv("HSG_GEMM_BF16_OLD")) {
+    // mode; HSG_GEMM_BF16_OLD=1 keeps the register-staged k_gemm<..., BF> tiles (dev A/B)
+    if (mode == MODE_BF16 && !HSG_DEV_ENV("HSG_GEMM_BF16_OLD")) {
         int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
         if (!ak && !bk) rc = launch3<64, 64, 32, 1, 1, 0>(p, ak, bk, splits, st);
         else if (t3 == 1) rc = launch3<128, 64, 32, 1, 1>(p, ak, bk, splits, st);
@@ -1703,8 +1704,9 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : (int)e;
     }
+#ifdef HSG_DEV
     int g4 = 0;                                             // dev switch: k_gemm4 plans
-    if (const char *f = getenv("HSG_GEMM4")) g4 = atoi(f);
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM4")) g4 = atoi(f);
     if (mode == MODE_F32_SPLIT && ak && bk && (K & 3) == 0 && g4 > 0) {
         if (colsum_part || g4 == 1) rc = launch4<64, 64, 3>(p, splits, st);
         else if (g4 == 2) rc = launch4<128, 64, 3>(p, splits, st);
@@ -1712,14 +1714,24 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         else if (g4 == 4) rc = launch4<128, 64, 2>(p, splits, st);
         else if (g4 == 5) rc = launch4<64, 64, 2>(p, splits, st);
         else rc = launch4<128, 128, 2>(p, splits, st);
-    } else if (mode == MODE_F32_SPLIT) {
+    } else
+#endif
+    if (mode == MODE_F32_SPLIT) {
         int t3 = plan3(M, N, K, splits, colsum_part != nullptr, bk);
-        if (const char *f = getenv("HSG_GEMM3_TILE"))      // dev override
+        if (const char *f = HSG_DEV_ENV("HSG_GEMM3_TILE"))      // dev override
             if (!colsum_part) t3 = atoi(f);
         int var = dw3 ? 5 : 0;                              // dev variants (tools/gemm3_sweep.py)
         if (dw3) t3 = 0;
-        if (const char *f = getenv("HSG_GEMM3_VAR")) var = atoi(f);
-        if (var == 1) {                                     // 2-deep register prefetch
+        if (const char *f = HSG_DEV_ENV("HSG_GEMM3_VAR")) var = atoi(f);
+        if (var == 5) {                                     // iglp_opt(0) interleave (the dW default)
+            if (t3 == 1) rc = launch3<128, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
+#ifdef HSG_DEV
+            else if (t3 == 3) rc = launch3<128, 128, 32, 1, 3, 0>(p, ak, bk, splits, st);
+#endif
+            else rc = launch3<64, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
+        }
+#ifdef HSG_DEV
+        else if (var == 1) {                                // 2-deep register prefetch
             if (t3 == 1) rc = launch3<128, 64, 32, 2>(p, ak, bk, splits, st);
             else rc = launch3<64, 64, 32, 2>(p, ak, bk, splits, st);
         } else if (var == 2) {                              // BK = 64
@@ -1731,35 +1743,35 @@ int gemm_impl(int mode, int M, int N, int K, const float *A, int lda, int a_kcon
         } else if (var == 4) {                              // one limb, 2-deep prefetch
             if (t3 == 1) rc = launch3<128, 64, 32, 2, 1>(p, ak, bk, splits, st);
             else rc = launch3<64, 64, 32, 2, 1>(p, ak, bk, splits, st);
-        } else if (var == 5) {                              // iglp_opt(0) interleave
-            if (t3 == 1) rc = launch3<128, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
-            else if (t3 == 3) rc = launch3<128, 128, 32, 1, 3, 0>(p, ak, bk, splits, st);
-            else rc = launch3<64, 64, 32, 1, 3, 0>(p, ak, bk, splits, st);
         } else if (var == 6) {                              // 8 waves (2 x 4), iglp_opt(0)
             if (t3 == 1) rc = launch3<64, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
             else if (t3 == 3) rc = launch3<128, 256, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
             else rc = launch3<64, 128, 32, 1, 3, 0, 512>(p, ak, bk, splits, st);
         } else if (t3 == 3) rc = launch3<128, 128>(p, ak, bk, splits, st);
-        else if (t3 == 1) rc = launch3<128, 64>(p, ak, bk, splits, st);
         else if (t3 == 2) rc = launch3<64, 128>(p, ak, bk, splits, st);
+#endif
+        else if (t3 == 1) rc = launch3<128, 64>(p, ak, bk, splits, st);
         else rc = launch3<64, 64>(p, ak, bk, splits, st);
-    } else if (mode == MODE_BF16) {
-        // bf16 operands: the two single-buffer plans (the K loop is load-bound, so the
-        // deeper tiles of the f32 plan table do not pay)
+    }
+#ifdef HSG_DEV
+    else if (mode == MODE_BF16) {
+        // bf16 operands: the register-staged single-buffer plans (dev A/B)
         if (best == 4) rc = launch_tiles<128, 64, 1, kBK, true>(p, ak, bk, splits, st);
         else rc = launch_tiles<64, 64, 1, kBK, true>(p, ak, bk, splits, st);
     } else if (best == 0) rc = launch_tiles<128, 128>(p, ak, bk, splits, st);
     else if (best == 1) rc = launch_tiles<128, 64>(p, ak, bk, splits, st);
     else if (best == 2) rc = launch_tiles<64, 64>(p, ak, bk, splits, st);
     else if (best == 3) rc = launch_tiles<128, 128, 1>(p, ak, bk, splits, st);
-    else if (best == 4) rc = launch_tiles<128, 64, 1>(p, ak, bk, splits, st);
-    else if (best == 5) rc = launch_tiles<64, 64, 1>(p, ak, bk, splits, st);
     else if (best == 6) rc = launch_tiles<64, 64, 1, 64>(p, ak, bk, splits, st);
     else if (best == 7) rc = launch_tiles<128, 64, 1, 64>(p, ak, bk, splits, st);
     else if (best == 8) rc = launch_tiles<64, 64, 2, 64>(p, ak, bk, splits, st);
     else if (best == 10) rc = launch_tiles<64, 128, 1>(p, ak, bk, splits, st);
     else if (best == 11) rc = launch_tiles<64, 128, 2>(p, ak, bk, splits, st);
-    else rc = launch_tiles<128, 128, 1, 64>(p, ak, bk, splits, st);
+    else if (best == 12) rc = launch_tiles<128, 128, 1, 64>(p, ak, bk, splits, st);
+#endif
+    // the exact-f32 MFMA (hsg_gemm_f32_mfma): plan_tile's two single-buffer tiles
+    else if (best == 4) rc = launch_tiles<128, 64, 1>(p, ak, bk, splits, st);
+    else rc = launch_tiles<64, 64, 1>(p, ak, bk, splits, st);
     if (rc || splits == 1 || slabs_only) return rc;
     const size_t total = (size_t)M * N;
     int blocks = (int)((total + 255) / 256);
@@ -1777,7 +1789,7 @@ int hsg_gemm_f32(int M, int N, int K, const float *A, int lda, int a_kcontig, co
                  int b_kcontig, float *C, int ldc, const float *bias, const float *aux, int ldaux, int epi,
                  int relu, int splits, float *workspace, float *colsum_part, void *stream) {
     int mode = MODE_F32_SPLIT;
-    if (const char *e = getenv("HSG_GEMM_F32"))          // dev A/B: "mfma" = exact-f32 instruction
+    if (const char *e = HSG_DEV_ENV("HSG_GEMM_F32"))          // dev A/B: "mfma" = exact-f32 instruction
         if (e[0] == 'm') mode = MODE_F32_MFMA;
     return gemm_impl(mode, M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias, aux, ldaux, epi, relu,
                      splits, workspace, colsum_part, stream);
@@ -1906,7 +1918,7 @@ int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *ou
         // float4 columns when every segment, the output and the column geometry allow
         bool v4 = cols[q] % 4 == 0 && pitch[q] % 4 == 0 && coff[q] % 4 == 0 && ((uintptr_t)out[q] & 15) == 0;
         for (int sg = 0; sg < nseg[q]; ++sg) v4 = v4 && ((uintptr_t)j.seg[q][sg] & 15) == 0;
-        if (const char *e = getenv("HSG_SLAB_VEC")) v4 = v4 && atoi(e) != 1;                // dev A/B
+        if (const char *e = HSG_DEV_ENV("HSG_SLAB_VEC")) v4 = v4 && atoi(e) != 1;                // dev A/B
         j.vec[q] = v4 ? 4 : 1;
         j.start[q + 1] = j.start[q] + (cols[q] + 32 * j.vec[q] - 1) / (32 * j.vec[q]) * out_rows[q];
     }
@@ -1956,17 +1968,18 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
-    if (const char *x = getenv("HSG_GEMM_XCD")) p.xcd = atoi(x);
+    if (const char *x = HSG_DEV_ENV("HSG_GEMM_XCD")) p.xcd = atoi(x);
     // k_gemm7 64-wide, LDS-staged float4 epilogue, RNE split with scalar subtractions:
     // cfg2 S2W FFN GEMMs 51.0 / 44.0 / 48.5 / 44.7 us against 55.6 / 48.0 / 53.4 / 47.9
     // for k_gemm5 (plan 7), medians of 5 interleaved rounds in one process
     // (tools/gemm5_sweep.py).  The truncation split (plan 28) is 1-2 us faster but its
     // larger limbs (|a1| < 2^-7 |a|) double the dropped-product bound, and a reference
     // golden's gradient gate-flip row left its tolerance with it.
-    int plan = 27;
-    if (const char *f = getenv("HSG_GEMM5")) plan = atoi(f);
     const __bf16 *pl = reinterpret_cast<const __bf16 *>(planes);
     hipStream_t st = (hipStream_t)stream;
+#ifdef HSG_DEV
+    int plan = 27;
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM5")) plan = atoi(f);
     if (plan == 2) return launch5<128, 2>(p, pl, Np, Kp, st);
     if (plan == 3) return launch5<64, 3>(p, pl, Np, Kp, st);
     if (plan == 4) return launch5<128, 3>(p, pl, Np, Kp, st);
@@ -1977,8 +1990,7 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 24) return launch5<64, 2, 0, true>(p, pl, Np, Kp, st);
     if (plan == 25) return launch5<64, 2, 0, true, true>(p, pl, Np, Kp, st);
     if (plan == 26) return launch5<128, 2, 0, true, true>(p, pl, Np, Kp, st);
-    if (plan == 27 && epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
-    if (plan == 27 || plan == 28 || plan == 30) return launch5<64, 2, 0>(p, pl, Np, Kp, st);   // unaligned / ragged quads
+    // (the plan-specific lines come before the unaligned fallback)
     if (plan == 28 && epi_rows_ok(p)) return launch7<64, 2, 1>(p, pl, Np, Kp, st);   // truncation split
     if (plan == 30 && epi_rows_ok(p)) return N <= 320 ? launch7<80, 2>(p, pl, Np, Kp, st) : launch7<128, 2>(p, pl, Np, Kp, st);
     if (plan == 34 && epi_rows_ok(p)) return launch7<64, 2, 4>(p, pl, Np, Kp, st);   // dev: no C store
@@ -1986,14 +1998,20 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 36 && epi_rows_ok(p)) return launch7<64, 2, 6>(p, pl, Np, Kp, st);   // dev: loads only
     if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
     if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
-    return launch5<64, 2>(p, pl, Np, Kp, st);
+    if (plan != 27) return launch5<64, 2>(p, pl, Np, Kp, st);
+#endif
+    if (epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
+    return launch5<64, 2, 0>(p, pl, Np, Kp, st);             // unaligned / ragged quads
 }
 
 // bf16-mode k_gemm7 (one product per tile): dev plans for the tile / depth / occupancy sweep
 static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
     int plan = 0;
-    if (const char *f = getenv("HSG_GEMM7B")) plan = atoi(f);
+#ifdef HSG_DEV
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM7B")) plan = atoi(f);
+#endif
     switch (plan) {
+#ifdef HSG_DEV
     case 1: return launch7<64, 3, 2>(p, pl, Np, Kp, st);
     case 2: return launch7<64, 4, 2>(p, pl, Np, Kp, st);
     case 3: return launch7<128, 2, 2>(p, pl, Np, Kp, st);
@@ -2004,6 +2022,7 @@ static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st
     case 7: return launch7<64, 3, 2, 3>(p, pl, Np, Kp, st);
     case 8: return launch7<128, 2, 2, 3>(p, pl, Np, Kp, st);
     case 9: return launch7<64, 2, 2>(p, pl, Np, Kp, st);
+#endif
     default:
         // tools/gemm5_sweep.py BF16=1 at cfg5's 28800 word rows (3 interleaved rounds):
         // N = 512 runs 31.1 us on 128-wide tiles against 37.8 on 64 (half the A re-reads);

@@ -20,6 +20,13 @@
 #include <stdlib.h>
 
 #include "../../include/hsg.h"
+#include "hsg_dev.h"
+
+#ifdef HSG_DEV
+#define HSG_PF_DEV 1
+#else
+#define HSG_PF_DEV 0
+#endif
 #include "hsg_rng.h"
 #include "hsg_wsplit.h"
 
@@ -744,7 +751,7 @@ struct DwGeom {
 // 1,024-block target: cfg2 step 1.502 vs 1.526 ms (tools/ab.py; 1,536 / 2,048 blocks
 // and the 8-slot, 512-block plan are slower)
 int dw_slots() {
-    if (const char *e = getenv("HSG_HPROJ_DWS")) return atoi(e) == 8 ? 8 : 4;        // dev A/B
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_DWS")) return atoi(e) == 8 ? 8 : 4;        // dev A/B
     return 4;
 }
 
@@ -755,7 +762,7 @@ DwGeom dw_geom(int n, int in, int H, int D) {
     g.sgroups = (ns + dw_slots() - 1) / dw_slots();
     const int steps = (n + 31) / 32 > 0 ? (n + 31) / 32 : 1;
     int target = dw_slots() == 4 ? 1024 : 512;          // blocks to aim for
-    if (const char *e = getenv("HSG_HPROJ_DWB")) target = atoi(e);     // dev sweep
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_DWB")) target = atoi(e);     // dev sweep
     int want = target / (g.ctiles * g.sgroups);
     if (want < 1) want = 1;
     if (want > steps) want = steps;
@@ -1036,26 +1043,26 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
     // slot-group size: 2 when a head has at most 2 slots (W2S, D = 8: 28.6 us against
     // 32.1 us at SG = 4, rocprofv3 kernel trace), else 4 (whole heads per wave)
     int sg = sph <= 2 ? 2 : 4;
-    if (const char *e = getenv("HSG_HPROJ_SG")) {                     // dev A/B
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_SG")) {                     // dev A/B
         const int v = atoi(e);
         sg = (v == 1 && sph == 1) ? 1 : (v == 2 && sph <= 2) ? 2 : 4;
     }
     int pf = 1;                                                                       // register ring depth (2, 4: no gain, tools/ab.py)
-    if (const char *e = getenv("HSG_HPROJ_PF")) pf = atoi(e);                         // dev A/B (1, 2, 4)
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_PF")) pf = atoi(e);                         // dev A/B (1, 2, 4)
     // one wave per block: the small S2W grid (420 waves at cfg2) spreads over more CUs
     // (8.84 -> 8.34 us per launch in the trace; step -3 us and +-0 us in two A/Bs)
     int wpb = 1;
-    if (const char *e = getenv("HSG_HPROJ_WPB")) wpb = atoi(e) == 4 ? 4 : (atoi(e) == 2 ? 2 : 1);   // dev A/B
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_WPB")) wpb = atoi(e) == 4 ? 4 : (atoi(e) == 2 ? 2 : 1);   // dev A/B
 #define HSG_HF(SG_)                                                                                              \
     {                                                                                                            \
         const long tasks = (long)((n + 15) / 16) * ((ns + SG_ - 1) / SG_);                                       \
         const dim3 grid((unsigned)((tasks + wpb - 1) / wpb)), blk(64 * wpb);                                     \
-        if (vec && pf == 4)                                                                                      \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 4>), grid, blk, 0, (hipStream_t)stream, n, in, H, D,       \
-                               X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
-        else if (vec && pf == 2)                                                                                 \
-            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, 2>), grid, blk, 0, (hipStream_t)stream, n, in, H, D,       \
-                               X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                               \
+        if (HSG_PF_DEV && vec && pf == 4)                                                                        \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, HSG_PF_DEV ? 4 : 1>), grid, blk, 0, (hipStream_t)stream, n, \
+                               in, H, D, X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                     \
+        else if (HSG_PF_DEV && vec && pf == 2)                                                                   \
+            hipLaunchKernelGGL((k_hproj_fwd<SG_, true, HSG_PF_DEV ? 2 : 1>), grid, blk, 0, (hipStream_t)stream, n, \
+                               in, H, D, X, ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                     \
         else if (vec)                                                                                            \
             hipLaunchKernelGGL((k_hproj_fwd<SG_, true>), grid, blk, 0, (hipStream_t)stream, n, in, H, D, X,       \
                                ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
@@ -1063,7 +1070,10 @@ int hsg_hproj_fwd_logits(int n, int in, int H, int D, const float *X, int ldx, c
             hipLaunchKernelGGL((k_hproj_fwd<SG_, false>), grid, blk, 0, (hipStream_t)stream, n, in, H, D, X,      \
                                ldx, W, bits, drop_scale(p), Z, ldz, a1, sigma);                                  \
     }
-    if (sg == 1) HSG_HF(1) else if (sg == 2) HSG_HF(2) else HSG_HF(4)
+#ifdef HSG_DEV
+    if (sg == 1) HSG_HF(1) else
+#endif
+    if (sg == 2) HSG_HF(2) else HSG_HF(4)
 #undef HSG_HF
     return status();
 }
@@ -1087,11 +1097,12 @@ int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float 
     if ((a1 == nullptr) != (sigma == nullptr)) return HSG_EINVAL;
     if (n == 0) return 0;
     // block = HB heads x KS K parts (HSG_HPROJ_FWD_PLAN = HB*10 + KS for A/B)
-    int plan = 22;
-    if (const char *e = getenv("HSG_HPROJ_FWD_PLAN")) plan = atoi(e);
     hipStream_t st = (hipStream_t)stream;
     const float s = drop_scale(p);
     const int nrt = (n + 63) / 64;
+#ifdef HSG_DEV
+    int plan = 22;
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_FWD_PLAN")) plan = atoi(e);
 #define HSG_T8(HB_, KS_)                                                                                          \
     if (plan == HB_ * 10 + KS_) {                                                                                 \
         const int bpr = (H + HB_ - 1) / HB_;                                                                      \
@@ -1101,6 +1112,7 @@ int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float 
     }
     HSG_T8(4, 2) HSG_T8(8, 1) HSG_T8(4, 1) HSG_T8(2, 4) HSG_T8(1, 4)
 #undef HSG_T8
+#endif
     const int bpr = (H + 1) / 2;
     hipLaunchKernelGGL((k_hproj_fwd_v8<2, 2>), dim3((unsigned)((nrt + 7) / 8 * 8 * bpr)), dim3(256), 0, st, n, in, H,
                        X, ldx, Wt, bits, s, Z, ldz, a1, sigma);
@@ -1116,7 +1128,8 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const long rtiles = (n + 15) / 16;
     // wide wave tiles (16 x 64) when that still gives >= 2048 waves, else 16 x 16
     const long wide = rtiles * ((in + 63) / 64);
-    if (const char *e = getenv("HSG_HPROJ_DX")) {                     // dev sweep: CT*10 + HF
+#ifdef HSG_DEV
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_DX")) {                     // dev sweep: CT*10 + HF
         const int v = atoi(e), ct = v / 10, hf = v % 10;
         const long tiles = rtiles * ((in + 16 * ct - 1) / (16 * ct));
         const dim3 g((unsigned)((tiles + 3) / 4));
@@ -1129,11 +1142,12 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         HSG_DXV(4, 1) HSG_DXV(4, 4) HSG_DXV(2, 2)
 #undef HSG_DXV
     }
+#endif
     // dev A/B (HSG_HPROJ_DXPRE): 0 = the chained kernels only; 1 (default) = one wave
     // per head when the grid is small, k_hproj_dx_n8 for narrow heads; 2 = one wave per
     // head for every small-D shape that is not narrow
     // (an up-front-operand form of k_hproj_dx<4, 1> with dword loads: 35.7 us, slower)
-    const char *pe = getenv("HSG_HPROJ_DXPRE");
+    const char *pe = HSG_DEV_ENV("HSG_HPROJ_DXPRE");
     const int mode = pe ? atoi(pe) : 1;
     if (mode != 0 && wide >= 2048 && H <= 8 && D == 8 && in % 4 == 0 && ldx % 4 == 0 && ldz % 2 == 0 &&
         aligned16(dX) && ((uintptr_t)dZ & 7) == 0 && aligned16(W)) {
@@ -1180,18 +1194,20 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const DwGeom g = dw_geom(n, in, H, D);
     const long total = (long)H * D * in;
     if (n > 0) {
-        const char *ve = getenv("HSG_HPROJ_DWVEC");                   // dev A/B: 0 = dword staging
+        const char *ve = HSG_DEV_ENV("HSG_HPROJ_DWVEC");                   // dev A/B: 0 = dword staging
         const bool vec = (!ve || atoi(ve) != 0) && dw_slots() == 4 && D == 8 && in % 4 == 0 && ldx % 4 == 0 &&
                          ldz % 4 == 0 && aligned16(X) && aligned16(dZ);
         if (vec)
             hipLaunchKernelGGL((k_hproj_dw<4, true>), dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H,
                                D, g.rows, dZ, ldz, X, ldx, bits, part);
-        else if (dw_slots() == 4)
+#ifdef HSG_DEV
+        else if (dw_slots() == 8)
+            hipLaunchKernelGGL(k_hproj_dw<8>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D,
+                               g.rows, dZ, ldz, X, ldx, bits, part);
+#endif
+        else
             hipLaunchKernelGGL(k_hproj_dw<4>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D,
                                g.rows, dZ, ldz, X, ldx, bits, part);
-        else
-        hipLaunchKernelGGL(k_hproj_dw<8>, dim3(g.ctiles, g.sgroups, g.chunks), dim3(256), 0, st, n, in, H, D, g.rows,
-                           dZ, ldz, X, ldx, bits, part);
         int rc = status();
         if (rc) return rc;
     }

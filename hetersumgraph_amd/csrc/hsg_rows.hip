@@ -17,6 +17,7 @@
 #include <stdlib.h>
 
 #include "../../include/hsg.h"
+#include "hsg_dev.h"
 #include "hsg_rng.h"
 
 namespace {
@@ -301,7 +302,7 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
     // rows per wave: 3 for 257..512 columns (cfg2 S2W, d = 300: 6,400 waves = one round
     // of resident waves, against 9,600 at 2; step -4 us in one A/B, 4 rows: -3 us)
     int rpw = (d + 255) / 256 == 2 ? 3 : 2;
-    if (const char *e = getenv("HSG_LN_FWD")) {                   // dev A/B: 0 = scalar, 1-4 rows per wave
+    if (const char *e = HSG_DEV_ENV("HSG_LN_FWD")) {                   // dev A/B: 0 = scalar, 1-4 rows per wave
         rpw = atoi(e);
         vec = vec && rpw > 0;
     }
@@ -314,7 +315,10 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
                            offset, out, mean, rstd);                                                       \
         return status();                                                                                   \
     }
-        HSG_LNF4(1, 1) HSG_LNF4(1, 2) HSG_LNF4(1, 4) HSG_LNF4(2, 1) HSG_LNF4(2, 2) HSG_LNF4(2, 3) HSG_LNF4(2, 4)
+        HSG_LNF4(1, 2) HSG_LNF4(2, 3)
+#ifdef HSG_DEV
+        HSG_LNF4(1, 1) HSG_LNF4(1, 4) HSG_LNF4(2, 1) HSG_LNF4(2, 2) HSG_LNF4(2, 4)
+#endif
 #undef HSG_LNF4
     }
 #define HSG_LNF(K)                                                                                       \

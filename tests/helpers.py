@@ -107,3 +107,18 @@ def synth_fixture(docs):
     z["n_w"] = int((z["g_unit"] == 0).sum())
     z["n_s"] = int((z["g_unit"] == 1).sum())
     return z
+
+
+def dev_lib():
+    """True when the loaded library is the dev build (libhsg_dev.so via HSG_LIB_PATH):
+    only it reads the A/B switches of the rejected kernel variants (csrc/hsg_dev.h);
+    the product libhsg.so runs the defaults whatever the environment says."""
+    from hetersumgraph_amd._lib import version
+    return version().endswith(" dev")
+
+
+def skip_unless_dev(variant_is_default):
+    import pytest
+    if not variant_is_default and not dev_lib():
+        pytest.skip("dev kernel variant: runs against libhsg_dev.so (HSG_LIB_PATH); the product library "
+                    "carries the default kernels only")

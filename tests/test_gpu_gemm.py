@@ -6,6 +6,8 @@ the exact-f32 instruction's)."""
 import pytest
 import torch
 
+from helpers import skip_unless_dev
+
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(19200 // 8, 512, 300), (1000, 300, 512), (67, 45, 33), (1120, 64, 512), (300, 512, 2400),
@@ -172,6 +174,7 @@ def test_psw_layouts(M, N, K, trans, plan, monkeypatch):
     """Every tile plan, row/column/K tails, both weight orientations: fp32-class error
     against fp64 (the same bound as hsg_gemm_f32's test_layouts)."""
     from hetersumgraph_amd.dense import gemm_psw, split_weights
+    skip_unless_dev(plan == "27")
     monkeypatch.setenv("HSG_GEMM5", plan)
     torch.manual_seed(M + N + K)
     A = mk(M, K)
@@ -190,6 +193,7 @@ def test_psw_split_is_fp32_class(M, N, K, plan, monkeypatch):
     fp32-class: per element |C - C_fp64| / sum_k |a_k b_k| within 1.5x of the exact-f32
     instruction's and below 2e-6, on operands spread over many binades."""
     from hetersumgraph_amd.dense import gemm, gemm_psw, split_weights
+    skip_unless_dev(plan == "27")
     monkeypatch.setenv("HSG_GEMM5", plan)
     torch.manual_seed(K + 1)
     A = mk(M, K) * torch.exp(2 * torch.randn(1, device="cuda"))
@@ -314,7 +318,8 @@ def test_slab_batch_staged_rows():
 def test_slab_reduce_float4_columns_bitwise_equal_scalar(cols, pitch, coff, out_rows, monkeypatch):
     """hsg_slab_reduce reads 16-byte column pieces when the job's geometry is aligned
     (cols, pitch, offset multiples of 4); the per-column summation order is the scalar
-    form's, so the sums are bitwise equal (HSG_SLAB_VEC=1 forces the scalar form)."""
+    form's, so the sums are bitwise equal (HSG_SLAB_VEC=1 forces the scalar form: dev library)."""
+    skip_unless_dev(False)
     from hetersumgraph_amd.reduce import SlabBatch
     torch.manual_seed(7)
     segs = [torch.randn(r, pitch, device="cuda") for r in (4096, 301, 7, 64)]

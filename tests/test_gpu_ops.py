@@ -5,6 +5,8 @@ import numpy as np
 import pytest
 import torch
 
+from helpers import skip_unless_dev
+
 pytestmark = pytest.mark.gpu
 
 
@@ -71,6 +73,7 @@ def test_forward_lanes_per_node_variants(monkeypatch, lpn, H, D, skew, per_edge)
     from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
     from hetersumgraph_amd.relation import Relation
     from oracle.fused import gat_aggregate_ref
+    skip_unless_dev(lpn == "64")
     monkeypatch.setenv("HSG_GAT_LPN", lpn.split("-")[0])
     monkeypatch.setenv("HSG_GAT_FWD_PF", "0" if lpn.endswith("nopf") else "1")
     rng = np.random.default_rng(H * 31 + D + skew)
@@ -173,6 +176,7 @@ def test_forward_row_tile_variants(monkeypatch, nq, H, D, dense_band, per_edge):
     from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
     from hetersumgraph_amd.relation import Relation
     from oracle.fused import gat_aggregate_ref
+    skip_unless_dev(nq == "0")
     monkeypatch.setenv("HSG_GAT_ROWS", nq)
     rng = np.random.default_rng(H * 17 + D + dense_band)
     n_src, n_dst = 120, 700
@@ -221,6 +225,7 @@ def test_src_pass_head_lane_variant(monkeypatch, hl, H, n_src, max_deg, per_edge
     segment lengths (the unpaired last edge), both tau modes."""
     from hetersumgraph_amd.ops import gat_aggregate, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
     from oracle.fused import gat_aggregate_ref
+    skip_unless_dev(hl == "1")
     monkeypatch.setenv("HSG_GAT_SRC_HL", hl)
     D = 8
     rng = np.random.default_rng(n_src + H + max_deg)
