@@ -17,7 +17,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip", "hsg_cnn.hip", "hsg_ffn.hip")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("hsg_gat.hip", "hsg_attn.hip", "hsg_gemm.hip", "hsg_rows.hip", "hsg_hproj.hip", "hsg_relbuild.hip", "hsg_cnn.hip", "hsg_ffn.hip", "hsg_dw.hip")]
 OUT = os.path.join(HERE, "libhsg.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 DEV_OUT = os.path.join(HERE, "libhsg_dev.so")

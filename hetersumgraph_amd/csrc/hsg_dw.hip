@@ -1,0 +1,289 @@
+// hsg_dw.hip -- the FFN weight gradients of one WSWGAT layer, BOTH in ONE launch (gfx950).
+//
+// Replaces the two deferred split-K GEMMs of the fused stack's backward
+// (PositionwiseFeedForward, module/GATLayer.py:35-44: dW2 = dY^T H and dW1 = dH^T X
+// over every application's rows, K = applications x rows = 38,400 at cfg2 for S2W).
+// Both operands are M/N-contiguous ([K][M] and [K][N] row-major: the activations as the
+// forward wrote them), the products fp32-accurate (three bf16 limbs per operand, six
+// products on v_mfma_f32_16x16x32_bf16, as k_gemm3; NL = 1: the bf16 mode's one
+// product), and the K slices are written as partial slabs [splits][M][N] that
+// hsg_slab_reduce sums in a fixed order (deterministic, no atomics).
+//
+// Why a kernel of its own (round 4): k_gemm3's 64x64 tiles move (64 + 64) x 4 B of
+// operand per K row for 4,096 outputs; at cfg2 the two S2W weight gradients pulled
+// 1.57 GB through L2 per step (99 + 98 us, L2->CU bound).  Here a
+// block owns 160 x 128 outputs (2 x 2 waves of 80 x 64, 16x16x32 MFMAs), so the
+// same work moves 0.71 GB, and both GEMMs of a layer share one grid of exactly two
+// blocks per CU (16 tiles x 32 K slices at cfg2): half the slab bytes of 64 slices.
+//
+// Pipeline (k_gemm3's): global -> registers (float4 along M/N), split into limbs,
+// ds_write_b64 into k-major limb images, two barriers per 32-deep K tile, the next
+// tile's global loads in flight during the MFMAs.  Fragments come back k-contiguous
+// through the hardware transpose read ds_read_b64_tr_b16 (two per fragment), on image
+// layouts chosen so that every such read is bank-conflict-free (Img below).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hsg.h"
+#include "hsg_wsplit.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+typedef short v8s16 __attribute__((ext_vector_type(8)));
+
+constexpr int kBK = 32;            // K rows per tile = one 16x16x32 MFMA step
+constexpr int kNT = 256;           // 4 waves, 2 x 2 over the output tile
+
+// k-major limb image of one operand's K tile: 32 rows (k) x ROWS columns (m or n), bf16.
+// A fragment read (16x16x32 operand: lane l takes column c0 + (l & 15), k = 8 (l >> 4)
+// + 0..7) touches, per 32-lane half, 8 image rows x 16 columns = 8 windows of 8 dwords;
+// the layout puts those 8 windows on 8 distinct 8-bank groups:
+//   ROWS % 128 == 0: a row is a multiple of 64 dwords (every row starts at bank 0), and
+//     16-column group j of row r sits at group j ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2;
+//   ROWS = 160 (80 dwords = 16 mod 64 per row): 16 bf16 of padding after every 8 rows,
+//     so rows r and r + 8 start 8 dwords apart.
+template <int ROWS>
+struct Img {
+    static_assert(ROWS % 128 == 0 || ROWS == 160, "image layout");
+    static constexpr bool XOR = ROWS % 128 == 0;
+    static constexpr int SIZE = XOR ? kBK * ROWS : kBK * ROWS + 16 * (kBK / 8);   // bf16 per limb plane
+    __device__ __forceinline__ static int off(int r, int c) {     // c % 4 == 0
+        if constexpr (XOR) {
+            const int f = (r & 3) | (((r >> 3) & 1) << 2);
+            return r * ROWS + (((c >> 4) ^ f) << 4) + (c & 15);
+        } else {
+            return r * ROWS + 16 * (r >> 3) + c;
+        }
+    }
+};
+
+// One operand's K tile in registers: thread t covers (k row, 4 consecutive columns)
+// units t, t + 256, ...; rows past the K slice and columns past M/N load zeros.
+template <int ROWS, int NL>
+struct Stage {
+    static constexpr int NU = kBK * ROWS / (4 * kNT);
+    static_assert(NU * 4 * kNT == kBK * ROWS, "tile must split evenly over the block");
+    f32x4 v[NU];
+
+    __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int c0, int nc, int k0, int k1) {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int idx = threadIdx.x + kNT * i;
+            const int kk = idx / (ROWS / 4), c = c0 + 4 * (idx % (ROWS / 4));
+            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            if (k0 + kk < k1 && c < nc) x = *reinterpret_cast<const f32x4 *>(g + (size_t)(k0 + kk) * ld + c);
+            v[i] = x;                                  // nc % 4 == 0 (host-checked): whole quads
+        }
+    }
+
+    __device__ __forceinline__ void store(__bf16 *img) const {
+#pragma unroll
+        for (int i = 0; i < NU; ++i) {
+            const int idx = threadIdx.x + kNT * i;
+            const int o = Img<ROWS>::off(idx / (ROWS / 4), 4 * (idx % (ROWS / 4)));
+            bf16x4 x0, x1, x2;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if constexpr (NL == 3) {
+                    __bf16 a, b, c;
+                    hsg_split3(v[i][e], a, b, c);
+                    x0[e] = a; x1[e] = b; x2[e] = c;
+                } else {
+                    x0[e] = (__bf16)v[i][e];             // RNE: the bf16 mode's operand
+                }
+            }
+            *reinterpret_cast<bf16x4 *>(&img[o]) = x0;
+            if constexpr (NL == 3) {
+                *reinterpret_cast<bf16x4 *>(&img[Img<ROWS>::SIZE + o]) = x1;
+                *reinterpret_cast<bf16x4 *>(&img[2 * Img<ROWS>::SIZE + o]) = x2;
+            }
+        }
+    }
+};
+
+// 16x16x32 operand fragment of image columns [c0, c0 + 16): lane l receives column
+// c0 + (l & 15), k = 8 (l >> 4) + 0..7.  ds_read_b64_tr_b16 per 16-lane group: lane
+// 4q + p addresses image row q of a 4 x 16 block at columns 4p..4p+3, and lane i of
+// the group receives column i, rows 0..3 -- two reads (k 0..3, 4..7) per fragment.
+template <int ROWS>
+__device__ __forceinline__ bf16x8 frag(const __bf16 *plane, int c0, int lane) {
+    const int i = lane & 15, q = i >> 2, p = i & 3, kb = 8 * (lane >> 4);
+    typedef __attribute__((address_space(3))) v4s16 lds_v4s16;
+    const v4s16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4s16 *)(const_cast<__bf16 *>(&plane[Img<ROWS>::off(kb + q, c0 + 4 * p)])));
+    const v4s16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_v4s16 *)(const_cast<__bf16 *>(&plane[Img<ROWS>::off(kb + 4 + q, c0 + 4 * p)])));
+    const v8s16 r = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, r);          // whole-vector reinterpretation
+}
+
+struct DwJob {
+    const float *A, *B;       // [K][M] (lda), [K][N] (ldb)
+    float *ws;                // [splits][M][N]
+    int M, N, lda, ldb;
+    int cfg;                  // tile: 0 = 160 x 128, 1 = 128 x 160, 2 = 128 x 128
+    int tiles_m, tiles_n;
+    int start;                // first logical block of the job
+};
+struct DwJobs {
+    DwJob j[2];
+    int nj, K, splits, ktps, total;
+};
+
+// Workgroup b runs on XCD b % 8 (for locality only): logical block xcd_order(b) gives
+// each XCD a contiguous run of (job, K slice, tile), so the tiles that share a slice's
+// operand rows meet in one L2.  A bijection on [0, total).
+__device__ __forceinline__ int xcd_order(int b, int total) {
+    const int x = b & 7, j = b >> 3, per = total >> 3, rem = total & 7;
+    return x * per + min(x, rem) + j;
+}
+
+template <int BM, int BN, int NL>
+__device__ __forceinline__ void dw_tile(const DwJob &jb, int tz, int t, const DwJobs &J, __bf16 *sA, __bf16 *sB) {
+    constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+    const int ty = t / jb.tiles_n, tx = t % jb.tiles_n;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int kt_total = (J.K + kBK - 1) / kBK;
+    const int kt0 = tz * J.ktps, kt1 = min(kt_total, kt0 + J.ktps);
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    Stage<BM, NL> ra;
+    Stage<BN, NL> rb;
+    if (kt0 < kt1) {
+        ra.load(jb.A, jb.lda, m0, jb.M, kt0 * kBK, J.K);
+        rb.load(jb.B, jb.ldb, n0, jb.N, kt0 * kBK, J.K);
+    }
+    for (int kt = kt0; kt < kt1; ++kt) {
+        __syncthreads();                          // every wave is done with the previous tile
+        ra.store(sA);
+        rb.store(sB);
+        __syncthreads();
+        if (kt + 1 < kt1) {                       // the next tile's loads overlap this tile's MFMAs
+            ra.load(jb.A, jb.lda, m0, jb.M, (kt + 1) * kBK, J.K);
+            rb.load(jb.B, jb.ldb, n0, jb.N, (kt + 1) * kBK, J.K);
+        }
+        bf16x8 a[NL][TM];
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) a[l][i] = frag<BM>(sA + l * Img<BM>::SIZE, wm * WM + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            bf16x8 b[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) b[l] = frag<BN>(sB + l * Img<BN>::SIZE, wn * WN + 16 * j, lane);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                if constexpr (NL == 3) {              // smallest limb products first, a0 b0 last
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+            }
+        }
+        __builtin_amdgcn_iglp_opt(0);
+    }
+
+    // the K slice's partial product: lane holds column (lane & 15), rows 4 (lane >> 4) + e
+    float *ws = jb.ws + (size_t)tz * jb.M * jb.N;
+    const int c = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WN + 16 * j + c;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int m = m0 + wm * WM + 16 * i + rq + e;
+                if (m < jb.M && n < jb.N) ws[(size_t)m * jb.N + n] = acc[i][j][e];
+            }
+        }
+}
+
+template <int NL>
+__global__ __launch_bounds__(kNT, 2) void k_dw(DwJobs J) {
+    __shared__ __attribute__((aligned(16))) __bf16 sA[NL * Img<160>::SIZE];
+    __shared__ __attribute__((aligned(16))) __bf16 sB[NL * Img<160>::SIZE];
+    const int L = xcd_order((int)blockIdx.x, J.total);
+    const int q = (J.nj > 1 && L >= J.j[1].start) ? 1 : 0;
+    const DwJob &jb = J.j[q];
+    const int loc = L - jb.start, tiles = jb.tiles_m * jb.tiles_n;
+    const int tz = loc / tiles, t = loc - tz * tiles;            // K slices outer: a slice's tiles adjacent
+    if (jb.cfg == 0) dw_tile<160, 128, NL>(jb, tz, t, J, sA, sB);
+    else if (jb.cfg == 1) dw_tile<128, 160, NL>(jb, tz, t, J, sA, sB);
+    else dw_tile<128, 128, NL>(jb, tz, t, J, sA, sB);
+}
+
+constexpr int kTileM[3] = {160, 128, 128}, kTileN[3] = {128, 160, 128};
+
+// the tile with the least padded output area (ties: the first)
+int pick_cfg(int M, int N) {
+    int best = 0;
+    long area = -1;
+    for (int c = 0; c < 3; ++c) {
+        const long a = (long)((M + kTileM[c] - 1) / kTileM[c]) * kTileM[c] * ((N + kTileN[c] - 1) / kTileN[c]) * kTileN[c];
+        if (area < 0 || a < area) { area = a; best = c; }
+    }
+    return best;
+}
+
+bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int hsg_gemm_dw_tiles(int M, int N) {
+    const int c = pick_cfg(M, N);
+    return ((M + kTileM[c] - 1) / kTileM[c]) * ((N + kTileN[c] - 1) / kTileN[c]);
+}
+
+int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float *const *A, const int *lda,
+                      const float *const *B, const int *ldb, int splits, int bf16, float *const *ws, void *stream) {
+    if (njobs < 1 || njobs > 2 || K < 1 || splits < 1 || !M || !N || !A || !B || !lda || !ldb || !ws)
+        return HSG_EINVAL;
+    DwJobs J{};
+    J.nj = njobs;
+    J.K = K;
+    const int kt_total = (K + kBK - 1) / kBK;
+    if (splits > kt_total) return HSG_EINVAL;
+    J.ktps = (kt_total + splits - 1) / splits;
+    J.splits = (kt_total + J.ktps - 1) / J.ktps;          // every slice non-empty
+    if (J.splits != splits) return HSG_EINVAL;             // the caller sized ws for `splits` slabs
+    int start = 0;
+    for (int q = 0; q < njobs; ++q) {
+        DwJob &jb = J.j[q];
+        if (M[q] < 1 || N[q] < 1 || (M[q] & 3) || (N[q] & 3) || lda[q] < M[q] || ldb[q] < N[q] || (lda[q] & 3) ||
+            (ldb[q] & 3) || !A[q] || !B[q] || !ws[q] || !al16(A[q]) || !al16(B[q]))
+            return HSG_EINVAL;
+        jb.A = A[q]; jb.B = B[q]; jb.ws = ws[q];
+        jb.M = M[q]; jb.N = N[q]; jb.lda = lda[q]; jb.ldb = ldb[q];
+        jb.cfg = pick_cfg(M[q], N[q]);
+        jb.tiles_m = (M[q] + kTileM[jb.cfg] - 1) / kTileM[jb.cfg];
+        jb.tiles_n = (N[q] + kTileN[jb.cfg] - 1) / kTileN[jb.cfg];
+        jb.start = start;
+        start += jb.tiles_m * jb.tiles_n * splits;
+    }
+    J.total = start;
+    hipStream_t st = (hipStream_t)stream;
+    if (bf16) hipLaunchKernelGGL(k_dw<1>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
+    else hipLaunchKernelGGL(k_dw<3>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

@@ -1349,6 +1349,275 @@ int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------
+// k_gemm11 (round 4): the pre-split-weight FFN GEMM on ONE round of big tiles.
+// k_gemm7's 128 x 64 blocks (two per CU) move (128 x 4 + 64 x 6) B of operand per K
+// for 8,192 outputs; at cfg2 its loads alone took 36 of its ~48 us per S2W FFN GEMM
+// (DESIGN §3), and 1,200 / 750 tiles ran in 2.3 / 1.5 rounds of the 512 resident
+// slots.  Here one block per CU (8 waves, 2 per SIMD) owns BM x BN outputs, with the
+// tile sized so the whole GEMM is ONE round of at most one block per CU:
+//   N > 320 (ffn1 H = x W1^T, dH = dy W2):  160 x 256, waves 2 x 4 of 80 x 64
+//   N <= 320 (ffn2 y = H W2^T, dx += dH W1): 192 x 160, waves 4 x 2 of 48 x 80
+// (cfg2: 240 / 200 tiles on 256 CUs), i.e. 2176 / 1728 B per K for 40,960 / 30,720
+// outputs -- 2.1x / 1.9x fewer operand bytes per output than k_gemm7.  Same staging as
+// k_gemm7 (global_load_lds_dwordx4 into two stages of 32-deep K tiles, swizzled
+// images, one barrier per K tile), fragments by ds_read_b128, the fp32 operand split
+// into three RNE bf16 limbs at fragment read (split_rne8), six products on
+// v_mfma_f32_16x16x32_bf16; PM = 2: the bf16 mode (one product, limb plane 0 only).
+// Epilogue through LDS (float4 bias / aux loads and C stores, as epi_rows), in two
+// passes of half the waves when the images of all eight do not fit; column partials
+// (colpart) are written per wave row band of WM rows (hsg_gemm_psw_row_tiles).
+// ---------------------------------------------------------------------------------
+template <int BM, int BN, int WGM, int WGN, int PM>
+struct Cfg11 {
+    static constexpr int NW = WGM * WGN, NT = 64 * NW;
+    static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+    static constexpr int NL = PM == 2 ? 1 : 3;
+    static constexpr int A_FL = BM * 32;                   // floats of the A tile
+    static constexpr int B_BF = BN * 32;                   // bf16 per limb-plane tile
+    static constexpr int STAGE_FL = A_FL + NL * B_BF / 2;
+    static constexpr int APC = BM / 8, BPC = BN / 16;      // 1-KB DMA pieces: A (8 rows), B (16 rows / limb)
+    static constexpr int NPC = APC + NL * BPC;
+    static constexpr int NLD = (NPC + NW - 1) / NW;        // DMA instructions per wave per K tile
+    static constexpr int LDW = WN + 4;                     // epilogue image row (floats)
+    static constexpr int EPW = WM * LDW;                   // floats per wave image
+    static constexpr int EPASS = 2 * STAGE_FL >= NW * EPW ? 1 : 2;
+    static constexpr int LDS_FL = 2 * STAGE_FL > NW * EPW / EPASS ? 2 * STAGE_FL : NW * EPW / EPASS;
+    // epilogue: float4 quads per row, rows per step (lanes past RPS * QPR idle)
+    static constexpr int QPR = WN / 4, RPS = 64 / QPR;
+    static constexpr int STEPS = (WM + RPS - 1) / RPS;
+    // steps whose global operands are in flight together: the largest divisor of STEPS <= 10
+    static constexpr int CH = STEPS % 10 == 0 ? 10 : STEPS % 8 == 0 ? 8 : STEPS % 6 == 0 ? 6 : STEPS % 5 == 0 ? 5
+                            : STEPS % 4 == 0 ? 4 : STEPS;
+    static_assert(WM % 16 == 0 && WN % 16 == 0 && QPR <= 64, "tile shape");
+    static_assert(LDS_FL * 4 <= 163840, "LDS");
+};
+
+template <int BM, int BN, int WGM, int WGN, int PM>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const __bf16 *__restrict__ planes, int Np,
+                                                              int Kp) {
+    using C = Cfg11<BM, BN, WGM, WGN, PM>;
+    constexpr int NW = C::NW, WM = C::WM, WN = C::WN, TM = C::TM, TN = C::TN, NL = C::NL;
+    __shared__ __attribute__((aligned(16))) float lds[C::LDS_FL];
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wid / WGN, wn = wid % WGN;
+    const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+    const int total = tiles_n * tiles_m;
+    const int lt = p.xcd ? xcd_tile(blockIdx.x, total) : (int)blockIdx.x;
+    const int tx = lt % tiles_n, ty = lt / tiles_n;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int nt = Kp / 32;
+
+    f32x4v7 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](int it) {
+        float *st = lds + (it & 1) * C::STAGE_FL;
+        __bf16 *sb = reinterpret_cast<__bf16 *>(st + C::A_FL);
+        const int k0 = it * 32;
+#pragma unroll
+        for (int i = 0; i < C::NLD; ++i) {
+            // NPC pieces over NW waves; a wave short of pieces repeats the last one (the
+            // same bytes to the same LDS address), so every wave issues NLD DMAs and one
+            // vmcnt count serves all of them
+            const int piece = min(i * NW + wid, C::NPC - 1);          // wave-uniform
+            if (piece < C::APC) {
+                const int r = piece * 8 + (lane >> 3);
+                const int q = (lane & 7) ^ swz(r);
+                const int k = k0 + 4 * q;
+                const int gr = min(m0 + r, p.M - 1);
+                const float *src = k < p.K ? p.A + (size_t)gr * p.lda + k : g_zero16;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(st + piece * 256), 16, 0, 0);
+            } else {
+                const int bp = piece - C::APC;
+                const int limb = bp / C::BPC, prow = (bp % C::BPC) * 16;
+                const int r = prow + (lane >> 2);
+                const int c = (lane & 3) ^ ((r >> 2) & 3);
+                const __bf16 *src = planes + ((size_t)(limb * Np + n0 + r) * Kp + k0 + 8 * c);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(sb + limb * C::B_BF + prow * 32),
+                                                 16, 0, 0);
+            }
+        }
+    };
+    if (nt > 0) issue(0);
+    const int li = lane & 15, kb = lane >> 4;
+    for (int it = 0; it < nt; ++it) {
+        wait_vmcnt<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (it + 1 < nt) issue(it + 1);                     // lands while this tile is multiplied
+        const float *sa = lds + (it & 1) * C::STAGE_FL;
+        const __bf16 *sb = reinterpret_cast<const __bf16 *>(sa + C::A_FL);
+        bf16x8 a[TM][3];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int r = wm * WM + 16 * i + li, sw = swz(r);
+            const f32x4 x = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb) ^ sw)]);
+            const f32x4 y = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb + 1) ^ sw)]);
+            if constexpr (PM == 2) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a[i][0][e] = (__bf16)(e < 4 ? x[e] : y[e - 4]);   // RNE
+            } else {
+                split_rne8(x, y, a[i][0], a[i][1], a[i][2]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int r = wn * WN + 16 * j + li;
+            const int off = r * 32 + 8 * (kb ^ ((r >> 2) & 3));
+            bf16x8 b[3];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) b[l] = *reinterpret_cast<const bf16x8 *>(&sb[l * C::B_BF + off]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                if constexpr (PM == 2) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
+                } else {                                    // small products first
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[0], acc[i][j], 0, 0, 0);
+                }
+            }
+        }
+        __builtin_amdgcn_iglp_opt(0);
+    }
+
+    // epilogue: each wave's WM x WN tile through LDS, float4 quads (lane: quad q of
+    // row rs of each RPS-row step), in EPASS passes of NW / EPASS waves
+    int q = lane % C::QPR, rs = lane / C::QPR;
+    // opaque to the scheduler: nothing of the epilogue (its operand addresses) is
+    // computed before the K loop ends, where it would hold registers across it
+    asm volatile("" : "+v"(q), "+v"(rs));
+    const int row0 = m0 + wm * WM, n = n0 + wn * WN + 4 * q;
+    const bool nok = n < p.N && rs < C::RPS;                   // N % 4 == 0: whole quads
+    const int nc = min(n, p.N - 4);
+    f32x4 bn = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.bias) bn = *reinterpret_cast<const f32x4 *>(p.bias + nc);
+    f32x4 csum = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int pass = 0; pass < C::EPASS; ++pass) {
+        __syncthreads();                                       // stages (or the previous pass) consumed
+        const bool mine = C::EPASS == 1 || (wid / (NW / C::EPASS)) == pass;
+        float *wl = lds + (wid % (NW / C::EPASS)) * C::EPW;
+        if (mine) {
+            const int c = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) wl[(16 * i + rq + e) * C::LDW + 16 * j + c] = acc[i][j][e];
+            __builtin_amdgcn_s_waitcnt(0xc07f);                // lgkmcnt(0): the wave's own LDS writes
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");                     // no epilogue load above the image writes
+            // CH steps of global operands in flight at a time
+            constexpr int CH = C::CH;
+#pragma unroll 1
+            for (int s0 = 0; s0 < C::STEPS; s0 += CH) {       // (unrolled, the chunks' loads pile up: spills)
+                asm volatile("" ::: "memory");                 // one chunk's loads in flight at a time
+                f32x4 aux[CH], ex[CH];
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int m = min(row0 + min((s0 + t) * C::RPS + rs, WM - 1), p.M - 1);
+                    if (p.epi != HSG_EPI_STORE) aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + nc);
+                    if (p.epi == HSG_EPI_ADD_ELUG) {
+                        const size_t o = (size_t)m * p.ldaux + nc;
+                        ex[t] = *reinterpret_cast<const f32x4 *>(p.aux2 + o) - *reinterpret_cast<const f32x4 *>(p.aux3 + o);
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int r = (s0 + t) * C::RPS + rs, m = row0 + r;
+                    if (!nok || r >= WM || m >= p.M) continue;
+                    f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * C::LDW + 4 * q]);
+                    if (p.epi == HSG_EPI_RELU_BWD) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
+                    } else {
+                        v += bn;
+                        if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
+                        if (p.relu) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        }
+                    }
+                    *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+                    if (p.epi == HSG_EPI_ADD_ELUG) {
+                        f32x4 g;                            // G = dOut * elu'(h), e = elu(h) = x - origin
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
+                        *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
+                    }
+                    csum += v;
+                }
+            }
+        }
+    }
+    if (p.colpart) {                  // one partial row per wave row band (WM rows), fixed order
+        f32x4 t = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < C::RPS; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] += __shfl(csum[e], k * C::QPR + q);
+        if (rs == 0 && n < p.N) *reinterpret_cast<f32x4 *>(p.colpart + (size_t)(ty * WGM + wm) * p.N + n) = t;
+    }
+}
+
+// cfg2-class shapes only: the two big-tile plans, picked when they run the GEMM in ONE
+// round of at most one block per CU at >= 75 % of the CUs; 0 = not applicable
+int plan11(int M, int N, int cus) {
+    if (N > 512) return 0;
+    const int BM = N > 320 ? 160 : 192, BN = N > 320 ? 256 : 160;
+    const long tiles = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    if (tiles > cus || 4 * tiles < 3L * cus) return 0;
+    return N > 320 ? 1 : 2;
+}
+
+int device_cus() {
+    static std::atomic<int> cached{-1};
+    int c = cached.load(std::memory_order_relaxed);
+    if (c < 0) {
+        int dev = 0;
+        c = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            c = 0;
+        cached.store(c, std::memory_order_relaxed);
+    }
+    return c;
+}
+
+template <int BM, int BN, int WGM, int WGN, int PM>
+int launch11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    p.splits = 1;
+    p.k_tiles_per_split = Kp / 32;
+    if ((p.N + BN - 1) / BN * BN > Np) return HSG_EINVAL;   // B tile rows must exist in the planes
+    if (!epi_rows_ok(p)) return HSG_EINVAL;
+    const long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
+    hipLaunchKernelGGL((k_gemm11<BM, BN, WGM, WGN, PM>), dim3((unsigned)g), dim3(64 * WGM * WGN), 0, st, p, planes, Np,
+                       Kp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+// the big-tile plan of this shape, or HSG_EINVAL when it does not apply
+template <int PM>
+int try11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    const int pl = plan11(p.M, p.N, device_cus());
+    if (pl == 1) return launch11<160, 256, 2, 4, PM>(p, planes, Np, Kp, st);
+    if (pl == 2) return launch11<192, 160, 4, 2, PM>(p, planes, Np, Kp, st);
+    return HSG_EINVAL;
+}
+
+// ---------------------------------------------------------------------------------
 // k_gemm6: k_gemm5's contract (fp32 A, pre-split weight planes) with A never staged
 // through LDS: each wave owns 32 A rows that no other wave reads, so every lane loads
 // its own fragment (row li, 8 consecutive k per 16-k step: 2 x dwordx4) straight
@@ -1999,13 +2268,28 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
     if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
     if (plan != 27) return launch5<64, 2>(p, pl, Np, Kp, st);
+    if (!(HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0))
 #endif
+    {
+        // one round of big tiles (k_gemm11) where the shape allows; its column partials
+        // are per WM-row band (hsg_gemm_psw_row_tiles), so with colsum_part it never
+        // falls back to the 64-row-slab kernels
+        const int rc = try11<0>(p, pl, Np, Kp, st);
+        if (rc != HSG_EINVAL || (colsum_part && plan11(M, N, device_cus()))) return rc;
+    }
     if (epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2, 0>(p, pl, Np, Kp, st);             // unaligned / ragged quads
 }
 
 // bf16-mode k_gemm7 (one product per tile): dev plans for the tile / depth / occupancy sweep
 static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
+#ifdef HSG_DEV
+    if (!(HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0))
+#endif
+    {
+        const int rc = try11<2>(p, pl, Np, Kp, st);        // one round of big tiles where it applies
+        if (rc != HSG_EINVAL || (p.colpart && plan11(p.M, p.N, device_cus()))) return rc;
+    }
     int plan = 0;
 #ifdef HSG_DEV
     if (const char *f = HSG_DEV_ENV("HSG_GEMM7B")) plan = atoi(f);
@@ -2044,6 +2328,18 @@ int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
     if (!epi_rows_ok(p)) return HSG_EINVAL;      // the caller keeps hsg_gemm_bf16 on the unsplit weight
     return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
+int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
+    (void)K; (void)bf16;
+    if (M < 0 || N < 1) return 0;
+    const int pl = plan11(M, N, device_cus());
+#ifdef HSG_DEV
+    if (HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0) return (M + 63) / 64;
+#endif
+    if (pl == 1) return (M + 159) / 160 * 2;               // k_gemm11<160, 256, 2, 4>: 80-row bands
+    if (pl == 2) return (M + 191) / 192 * 4;               // k_gemm11<192, 160, 4, 2>: 48-row bands
+    return (M + 63) / 64;
 }
 
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,

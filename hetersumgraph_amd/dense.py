@@ -168,6 +168,9 @@ def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, c
         rc = lib.hsg_gemm_bf16_psw(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias), ptr(aux),
                                    _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part), stream_of(A))
         if rc == HSG_EINVAL and Bs.W is not None:           # unaligned / ragged quads: the unsplit weight
+            if colsum_part is not None and colsum_part.shape[0] != row_tiles(M, N, K, 1):
+                raise RuntimeError("gemm_psw: column partials sized for the split-weight kernel, which "
+                                   "declined this call (alignment)")
             return gemm(A, Bs.W, b_t=not Bs.trans, out=out, bias=bias, relu=relu, relu_mask=relu_mask, add=add,
                         splits=1 if colsum_part is not None else 0, colsum_part=colsum_part, dtype="bf16")
         check(rc, "hsg_gemm_bf16_psw")
@@ -227,6 +230,50 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     return ws, splits
 
 
+def gemm_dw_slabs(pairs, splits=None):
+    """Split-K partial products of A_q^T B_q for up to two (A [K, M], B [K, N]) pairs
+    sharing K -- a layer's two FFN weight gradients dW2 = dY^T H and dW1 = dH^T X --
+    in ONE launch (hsg_gemm_dw_slabs: 160 x 128 / 128 x 160 tiles, fp32-accurate in
+    'f32' mode, one bf16 product in 'bf16').  Returns [(workspace [splits*M*N],
+    splits)] per pair, summed later by hsg_slab_reduce, or None when the shapes or the
+    GEMM mode are not covered (the caller then uses gemm_slabs per pair).
+    ``splits``: K slices (default: two blocks per CU over all pairs' tiles, at least
+    4 K tiles per slice)."""
+    lib = load()
+    if _GEMM_DTYPE not in ("f32", "bf16") or not pairs or len(pairs) > 2:
+        return None
+    K = pairs[0][0].shape[0]
+    for A, B in pairs:
+        if (not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32 or A.dim() != 2 or B.dim() != 2
+                or A.shape[0] != K or B.shape[0] != K or A.stride(1) != 1 or B.stride(1) != 1
+                or A.shape[1] % 4 or B.shape[1] % 4 or _ld(A) % 4 or _ld(B) % 4
+                or A.data_ptr() % 16 or B.data_ptr() % 16):
+            return None
+    kt = (K + 31) // 32
+    if splits is None:
+        tiles = sum(lib.hsg_gemm_dw_tiles(A.shape[1], B.shape[1]) for A, B in pairs)
+        splits = int(os.environ.get("HSG_DW2_SPLITS", "0")) or max(1, (2 * 256) // max(tiles, 1))   # dev A/B
+        splits = max(1, min(splits, kt // 4))
+    # every K slice non-empty (the kernel's slice length is ceil(kt / splits) tiles)
+    per = (kt + splits - 1) // splits
+    splits = (kt + per - 1) // per
+    if splits < 2:
+        return None
+    n = len(pairs)
+    arr = lambda t, xs: (t * n)(*xs)
+    ws = [pairs[q][0].new_empty(splits * pairs[q][0].shape[1] * pairs[q][1].shape[1]) for q in range(n)]
+    c_i, c_p = ctypes.c_int, ctypes.c_void_p
+    rc = lib.hsg_gemm_dw_slabs(n, arr(c_i, [A.shape[1] for A, _ in pairs]), arr(c_i, [B.shape[1] for _, B in pairs]),
+                               K, arr(c_p, [A.data_ptr() for A, _ in pairs]), arr(c_i, [_ld(A) for A, _ in pairs]),
+                               arr(c_p, [B.data_ptr() for _, B in pairs]), arr(c_i, [_ld(B) for _, B in pairs]),
+                               splits, int(_GEMM_DTYPE == "bf16"), arr(c_p, [w.data_ptr() for w in ws]),
+                               stream_of(pairs[0][0]))
+    if rc == HSG_EINVAL:
+        return None
+    check(rc, "hsg_gemm_dw_slabs")
+    return [(w, splits) for w in ws]
+
+
 def auto_splits(M, N, K):
     """hsg_gemm_f32's splits == 0 plan (so the workspace can be sized)."""
     return load().hsg_gemm_auto_splits(M, N, K)
@@ -235,6 +282,11 @@ def auto_splits(M, N, K):
 def row_tiles(M, N, K, splits=1):
     """Rows of hsg_gemm_f32's colsum_part slab for this shape."""
     return load().hsg_gemm_row_tiles(M, N, K, splits)
+
+
+def psw_row_tiles(M, N, K, mode="f32"):
+    """Rows of the colsum_part slab of gemm_psw on this shape (hsg_gemm_psw_row_tiles)."""
+    return load().hsg_gemm_psw_row_tiles(M, N, K, int(mode == "bf16"))
 
 
 def splits_for(M, N, K, n_cu=256):

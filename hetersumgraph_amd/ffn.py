@@ -26,7 +26,7 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, gemm_psw, gemm_psw_elug, get_gemm_dtype, row_tiles, split_weights
+from .dense import gemm, gemm_psw, gemm_psw_elug, get_gemm_dtype, psw_row_tiles, row_tiles, split_weights
 
 LN_EPS = 1e-5
 
@@ -142,7 +142,7 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
         part = x.new_empty(nb, 3, d)
         check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
                              ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
-        rt = row_tiles(n, d_hid, d)
+        rt = psw_row_tiles(n, d_hid, d, wsplit[2].mode) if wsplit is not None else row_tiles(n, d_hid, d)
         hpart = x.new_empty(rt, d_hid)
         dH_out = act_grads[1] if act_grads is not None else None
         if wsplit is not None:

@@ -36,7 +36,7 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import stream_of
-from .dense import gemm, gemm_slabs
+from .dense import gemm, gemm_dw_slabs, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
@@ -348,15 +348,21 @@ class _GatStack(torch.autograd.Function):
                 grads[org] = dx
         # FFN weight gradients, one GEMM per weight over every application's rows:
         # dW2 = dY^T H, dW1 = dH^T X with [applications * rows] as the reduction
+        # -- both of a layer in ONE launch (hsg_gemm_dw_slabs; HSG_DW_PAIR=0: one
+        # hsg_gemm_*_slabs launch each, for A/B)
         for lay, DY, DH in gbufs.values():
             X, Hh = ctx.bufs[id(lay)]
             d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
+            todo = []
             for p, A, B, (m, n) in ((lay.w2, DY.view(-1, d), Hh.view(-1, d_hid), (d, d_hid)),
                                     (lay.w1, DH.view(-1, d_hid), X.view(-1, d), (d_hid, d))):
                 dw, a_w = pgrads.dst(p)
-                if dw is None:
-                    continue
-                sl = gemm_slabs(A, B, a_t=True)             # split-K slabs, summed in the batch
+                if dw is not None:
+                    todo.append((p, A, B, m, n, dw, a_w))
+            pair = gemm_dw_slabs([(A, B) for _, A, B, *_ in todo]) \
+                if todo and os.environ.get("HSG_DW_PAIR", "1") != "0" else None
+            for k, (p, A, B, m, n, dw, a_w) in enumerate(todo):
+                sl = pair[k] if pair is not None else gemm_slabs(A, B, a_t=True)   # split-K slabs
                 if sl is not None:
                     batch.add((id(lay), id(p)), dw.view(-1), m * n, m * n, 0, 1.0, a_w, sl[0], sl[1])
                 else:

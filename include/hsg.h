@@ -266,6 +266,23 @@ int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcont
 int hsg_gemm_bf16_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig,
                         const float *B, int ldb, int b_kcontig, int splits, float *workspace,
                         void *stream);
+/* Rows of the column-partial slab (colsum_part [rows][N]) hsg_gemm_f32_psw /
+ * hsg_gemm_bf16_psw write for an M x N x K GEMM: the big-tile plan of the cfg2-class
+ * shapes sums per 80- / 48-row band, the others per 64 rows (hsg_gemm_row_tiles). */
+int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16);
+/* The FFN weight gradients of one layer in ONE launch (replaces PositionwiseFeedForward's
+ * dW2 = dY^T H and dW1 = dH^T X backward, module/GATLayer.py:39-41, summed over every
+ * application's rows): job q (njobs 1..2) computes the split-K partial products of
+ * A_q^T B_q with A_q [K][M_q] (row stride lda_q) and B_q [K][N_q] (ldb_q), both
+ * M/N-contiguous, into ws_q[splits][M_q][N_q], summed later by hsg_slab_reduce.
+ * fp32-accurate (three bf16 limbs per operand, six products), or with bf16 != 0 the
+ * bf16 mode's one product of RNE-rounded operands.  Requires M, N, lda, ldb multiples
+ * of 4 and 16-byte aligned A, B (HSG_EINVAL otherwise); splits must leave every K
+ * slice non-empty (ceil(ceil(K/32) / ceil(ceil(K/32)/splits)) == splits). */
+int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float *const *A, const int *lda,
+                      const float *const *B, const int *ldb, int splits, int bf16, float *const *ws, void *stream);
+/* Output tiles of one hsg_gemm_dw_slabs job of shape M x N (blocks = tiles x splits). */
+int hsg_gemm_dw_tiles(int M, int N);
 /* Deferred column sums of partial slabs, njobs (1..24) outputs in one deterministic
  * launch: out[q][b][c] = (accumulate[q] ? out[q][b][c] : 0) + scale[q] * sum over
  * job q's nseg[q] (1..4) segments s (in order) of the rows r in the b-th of

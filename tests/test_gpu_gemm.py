@@ -364,3 +364,101 @@ def test_psw_bf16_mode_is_the_rounded_product(M, N, K):
     scale = max(1.0, ref.abs().max().item())
     assert (C.double() - ref).abs().max().item() <= 1e-5 * scale * max(1.0, K ** 0.5)
     assert (C2.double() - ref).abs().max().item() <= 1e-5 * scale * max(1.0, K ** 0.5)
+
+
+# ---- hsg_gemm_dw_slabs: a layer's two FFN weight gradients in one launch ------------
+DW_PAIRS = [((38400, 300, 512), None),            # cfg2 S2W: dW2 = dY^T H, dW1 = dH^T X
+            ((3360, 64, 512), None),              # cfg2 W2S
+            ((1000, 20, 36), None),               # K tail (1000 = 31.25 tiles), ragged tiles
+            ((4096, 300, 512), 3)]                # explicit splits
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("shape,splits", DW_PAIRS)
+def test_dw_slabs_pair(shape, splits, dtype):
+    """Both weight gradients of a layer in ONE hsg_gemm_dw_slabs launch, slabs summed by
+    hsg_slab_reduce: 'f32' fp32-class per element (|err| / sum_k |a_k b_k| < 2e-6, the
+    split GEMM's bound), 'bf16' equal to an fp64 GEMM of the RNE-rounded operands up to
+    fp32 summation (< 2e-6 of sum |a b|); the pair's second job is the transposed shape."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_dw_slabs
+    from hetersumgraph_amd.reduce import SlabBatch
+    K, d, dh = shape
+    torch.manual_seed(K + d)
+    A1, B1 = mk(K, d), mk(K, dh)                    # dW2 = A1^T B1: [d, dh]
+    A2, B2 = mk(K, dh), mk(K, d)                    # dW1 = A2^T B2: [dh, d]
+    A1 = A1 * torch.exp(torch.randn_like(A1))
+    with gemm_dtype(dtype):
+        res = gemm_dw_slabs([(A1, B1), (A2, B2)], splits=splits)
+    assert res is not None
+    b = SlabBatch()
+    outs = []
+    for q, ((A, B), (ws, sp)) in enumerate(zip([(A1, B1), (A2, B2)], res)):
+        if splits is not None:
+            assert sp == splits
+        out = torch.full((A.shape[1] * B.shape[1],), 7.0, device="cuda")
+        b.add(q, out, out.numel(), out.numel(), 0, 1.0, False, ws, sp)
+        outs.append(out.view(A.shape[1], B.shape[1]))
+    b.flush()
+    torch.cuda.synchronize()
+    for (A, B), C in zip([(A1, B1), (A2, B2)], outs):
+        a64, b64 = A.double(), B.double()
+        if dtype == "bf16":
+            a64, b64 = A.bfloat16().double(), B.bfloat16().double()
+        ref, unit = a64.t() @ b64, a64.abs().t() @ b64.abs()
+        err = ((C.double() - ref).abs() / unit.clamp_min(1e-30)).max().item()
+        print(f"{dtype} K={K} {A.shape[1]}x{B.shape[1]}: max err / sum|ab| = {err:.2e}")
+        assert err < 2e-6
+
+
+# ---- k_gemm11: one round of big tiles for the cfg2-class FFN GEMMs -------------------
+BIG_SHAPES = [(19200, 512, 300), (19200, 300, 512), (18000, 512, 300), (20000, 300, 512)]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K", BIG_SHAPES)
+def test_big_tile_psw_epilogues(M, N, K, dtype):
+    """The pre-split-weight GEMM on the cfg2-class shapes, where hsg_gemm_*_psw runs one
+    round of 160 x 256 / 192 x 160 tiles (k_gemm11; hsg_gemm_psw_row_tiles reports its
+    80- / 48-row column-partial bands): every epilogue the FFN uses -- bias + ReLU,
+    ReLU' mask with column partials, accumulate, and the ELU-gate epilogue -- against
+    fp64 ('f32': fp32-class, |err| / sum_k |a_k b_k| < 2e-6; 'bf16': the GEMM of the
+    RNE-rounded operands)."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, gemm_psw_elug, psw_row_tiles, split_weights
+    torch.manual_seed(M + N)
+    A = mk(M, K)
+    W = mk(N, K) * 0.5
+    with gemm_dtype(dtype):
+        (S,) = split_weights((W, False))
+    rt = psw_row_tiles(M, N, K, dtype)
+    assert rt == (M + (159 if N > 320 else 191)) // (160 if N > 320 else 192) * (2 if N > 320 else 4)
+    a64 = A.double() if dtype == "f32" else A.bfloat16().double()
+    w64 = W.double() if dtype == "f32" else W.bfloat16().double()
+    ref, unit = a64 @ w64.t(), a64.abs() @ w64.abs().t()
+    tol = 2e-6
+
+    def rel(C, R):
+        return ((C.double() - R).abs() / unit.clamp_min(1e-30)).max().item()
+
+    bias = torch.randn(N, device="cuda")
+    C = gemm_psw(A, S, bias=bias, relu=True)
+    assert rel(C, torch.relu(ref + bias.double())) < tol
+    mask = torch.randn(M, N, device="cuda")
+    hpart = torch.empty(rt, N, device="cuda")
+    C = gemm_psw(A, S, relu_mask=mask, colsum_part=hpart)
+    R = torch.where(mask.double() > 0, ref, torch.zeros_like(ref))
+    assert rel(C, R) < tol
+    colsum = hpart.double().sum(0)
+    assert (colsum - C.double().sum(0)).abs().max().item() <= 1e-4 * max(1.0, C.double().abs().sum(0).max().item())
+    add = torch.randn(M, N, device="cuda")
+    C = gemm_psw(A, S, add=add.clone())
+    assert rel(C, ref + add.double()) < tol
+    # ELU gate: x = elu(h) + origin, G = dx * elu'(h) from e = x - origin
+    origin = torch.randn(M, N, device="cuda")
+    h = 2 * torch.randn(M, N, device="cuda")
+    x = torch.nn.functional.elu(h) + origin
+    out, G = add.clone(), torch.empty(M, N, device="cuda")
+    assert gemm_psw_elug(A, S, out, x, origin, G)
+    assert rel(out, ref + add.double()) < tol
+    e = x.double() - origin.double()
+    gref = torch.where(e > 0, out.double(), out.double() * (e + 1))
+    assert (G.double() - gref).abs().max().item() <= 1e-6 * max(1.0, gref.abs().max().item())
