@@ -32,7 +32,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
-           "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles")
+           "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -119,6 +119,7 @@ _SIGS = {
     "hsg_gemm_dw_slabs": [_I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "hsg_gemm_dw_tiles": [_I, _I],
     "hsg_gemm_psw_row_tiles": [_I, _I, _I, _I],
+    "hsg_gemm_psw_ln": [_I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _I, _P],
     "hsg_slab_reduce": [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_wsplit": [_I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_f32_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],

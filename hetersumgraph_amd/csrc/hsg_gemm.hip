@@ -45,6 +45,7 @@
 
 #include "../../include/hsg.h"
 #include "hsg_dev.h"
+#include "hsg_rng.h"
 #include "hsg_wsplit.h"
 
 namespace {
@@ -78,6 +79,13 @@ struct GemmArgs {
     const float *aux2 = nullptr;
     const float *aux3 = nullptr;
     float *C2 = nullptr;
+    // k_gemm11's LayerNorm epilogue only (hsg_gemm_*_psw_ln): C = the pre-dropout FFN
+    // output y, lnout = LN(dropout(y) + aux) with gamma / beta, per-row mean / rstd
+    const float *gamma = nullptr, *beta = nullptr;
+    float *lnout = nullptr, *mean = nullptr, *rstd = nullptr;
+    const int64_t *seed = nullptr;
+    float eps = 0.f, p_drop = 0.f;
+    uint32_t offset = 0;
 };
 
 // Workgroup b is dispatched to XCD b % 8, and so is tile t (the persistent grid is a
@@ -1392,12 +1400,15 @@ struct Cfg11 {
     static_assert(LDS_FL * 4 <= 163840, "LDS");
 };
 
-template <int BM, int BN, int WGM, int WGN, int PM>
+template <int BM, int BN, int WGM, int WGN, int PM, bool LN = false>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const __bf16 *__restrict__ planes, int Np,
                                                               int Kp) {
     using C = Cfg11<BM, BN, WGM, WGN, PM>;
     constexpr int NW = C::NW, WM = C::WM, WN = C::WN, TM = C::TM, TN = C::TN, NL = C::NL;
-    __shared__ __attribute__((aligned(16))) float lds[C::LDS_FL];
+    constexpr int LDT = BN - 12;                               // LN epilogue: the tile's image, N <= BN - 16 columns
+    constexpr int LDS_ALL = LN && BM * LDT > C::LDS_FL ? BM * LDT : C::LDS_FL;
+    static_assert(LDS_ALL * 4 <= 163840, "LDS");
+    __shared__ __attribute__((aligned(16))) float lds[LDS_ALL];
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wid / WGN, wn = wid % WGN;
@@ -1489,6 +1500,93 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const 
             }
         }
         __builtin_amdgcn_iglp_opt(0);
+    }
+
+    if constexpr (LN) {
+        // y = acc + b2 (stored: the backward's LN reads it), out = LN(dropout(y) + x):
+        // the whole BM x BN tile (BN >= N: full rows) imaged in LDS, then wave w takes
+        // rows w, w + NW, ...; lane = float4 quads 4 lane + 256 i of the row, the
+        // arithmetic (and dropout index r * N + c) of k_ln_fwd4, so the result is that
+        // kernel's on the same y
+        static_assert(BN <= 512, "two quads per lane per row");
+        __syncthreads();                                       // every wave is done with the stages
+        {
+            const int c = lane & 15, rq = 4 * (lane >> 4);
+            float *img = lds + (wm * WM) * LDT + wn * WN;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    if (wn * WN + 16 * j < p.N)                // subtiles past N (padding) are not imaged
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) img[(16 * i + rq + e) * LDT + 16 * j + c] = acc[i][j][e];
+        }
+        constexpr int RW = BM / NW;                            // rows per wave
+        static_assert(BM % NW == 0, "rows per wave");
+        // the residual rows and the per-column operands, requested before the barrier
+        f32x4 xr[RW][2], bq[2], gq[2], tq[2];
+        int rowv = wid;
+        asm volatile("" : "+v"(rowv));                         // after the image writes
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = min(4 * lane + 256 * i, p.N - 4);
+            bq[i] = *reinterpret_cast<const f32x4 *>(p.bias + c);
+            gq[i] = *reinterpret_cast<const f32x4 *>(p.gamma + c);
+            tq[i] = *reinterpret_cast<const f32x4 *>(p.beta + c);
+        }
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+            const int m = min(m0 + rowv + NW * t, p.M - 1);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = min(4 * lane + 256 * i, p.N - 4);
+                xr[t][i] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + c);
+            }
+        }
+        __syncthreads();
+        const uint32_t dkey = p.p_drop > 0.f ? hsg_drop_key((uint64_t)p.seed[0], p.offset) : 0u;
+        const uint32_t thr = hsg_drop_threshold(p.p_drop);
+        const float scale = p.p_drop > 0.f ? 1.f / (1.f - p.p_drop) : 1.f;
+#pragma unroll
+        for (int t = 0; t < RW; ++t) {
+            const int r = rowv + NW * t, m = m0 + r;
+            if (m >= p.M) break;                               // wave-uniform
+            f32x4 sv[2];
+            float sum = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = 4 * lane + 256 * i;
+                sv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (c < p.N) {
+                    f32x4 v = *reinterpret_cast<const f32x4 *>(&lds[r * LDT + c]) + bq[i];
+                    const size_t o = (size_t)m * p.N + c;
+                    *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + c) = v;
+                    if (p.p_drop > 0.f) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = hsg_keep32(dkey, (uint32_t)(o + e), thr) ? v[e] * scale : 0.f;
+                    }
+                    sv[i] = v + xr[t][i];
+                    sum += (sv[i][0] + sv[i][1]) + (sv[i][2] + sv[i][3]);
+                }
+            }
+            for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o);
+            const float mu = sum / p.N;
+            float var = 0.f;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                if (4 * lane + 256 * i < p.N)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { const float d = sv[i][e] - mu; var = fmaf(d, d, var); }
+            for (int o = 32; o >= 1; o >>= 1) var += __shfl_xor(var, o);
+            const float rsd = rsqrtf(var / p.N + p.eps);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = 4 * lane + 256 * i;
+                if (c < p.N) *reinterpret_cast<f32x4 *>(p.lnout + (size_t)m * p.N + c) = (sv[i] - mu) * rsd * gq[i] + tq[i];
+            }
+            if (lane == 0) { p.mean[m] = mu; p.rstd[m] = rsd; }
+        }
+        return;
     }
 
     // epilogue: each wave's WM x WN tile through LDS, float4 quads (lane: quad q of
@@ -1604,6 +1702,31 @@ int launch11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
     hipLaunchKernelGGL((k_gemm11<BM, BN, WGM, WGN, PM>), dim3((unsigned)g), dim3(64 * WGM * WGN), 0, st, p, planes, Np,
                        Kp);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+// the LayerNorm-epilogue plan (full rows: BN = 320 >= N), ONE round at >= 60 % of the
+// CUs: 96-row tiles (waves 2 x 4 of 48 x 80), else 128-row (64 x 80); 0 = none
+int plan11ln(int M, int N, int cus) {
+    if (N > 304 || N % 4) return 0;                         // the image holds 308 columns
+    const long t96 = (M + 95) / 96, t128 = (M + 127) / 128;
+    if (t96 <= cus && 5 * t96 >= 3L * cus) return 96;
+    if (t128 <= cus && 5 * t128 >= 3L * cus) return 128;
+    return 0;
+}
+
+template <int PM>
+int try11ln(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    const int bm = plan11ln(p.M, p.N, device_cus());
+    p.splits = 1;
+    p.k_tiles_per_split = Kp / 32;
+    if (!bm || 320 > Np) return HSG_EINVAL;
+    const unsigned g = (unsigned)((p.M + bm - 1) / bm);
+    if (bm == 96)
+        hipLaunchKernelGGL((k_gemm11<96, 320, 2, 4, PM, true>), dim3(g), dim3(512), 0, st, p, planes, Np, Kp);
+    else
+        hipLaunchKernelGGL((k_gemm11<128, 320, 2, 4, PM, true>), dim3(g), dim3(512), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -2328,6 +2451,28 @@ int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, bias, aux, ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
     if (!epi_rows_ok(p)) return HSG_EINVAL;      // the caller keeps hsg_gemm_bf16 on the unsplit weight
     return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
+int hsg_gemm_psw_ln(int M, int N, int K, const float *A, int lda, const void *planes, const float *bias, float *y,
+                    const float *x, const float *gamma, const float *beta, float eps, float p_drop, const int64_t *seed,
+                    uint32_t offset, float *out, float *mean, float *rstd, int bf16, void *stream) {
+    if (M < 0 || N < 4 || K < 0 || !A || !planes || !bias || !y || !x || !gamma || !beta || !out || !mean || !rstd)
+        return HSG_EINVAL;
+    if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K) return HSG_EINVAL;
+    if (p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && (!seed || (long)M * N >= (1L << 32)))) return HSG_EINVAL;
+    const auto al = [](const void *q) { return (((uintptr_t)q) & 15) == 0; };
+    if (!al(bias) || !al(gamma) || !al(beta) || !al(out) || !al(x) || !al(y)) return HSG_EINVAL;
+    if (M == 0) return 0;
+#ifdef HSG_DEV
+    if (HSG_DEV_ENV("HSG_GEMM11LN") && atoi(HSG_DEV_ENV("HSG_GEMM11LN")) == 0) return HSG_EINVAL;
+#endif
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, A, lda, nullptr, 0, y, N, bias, x, N, HSG_EPI_STORE, 0, Kp / 32, nullptr, nullptr, 1, 1};
+    p.gamma = gamma; p.beta = beta; p.lnout = out; p.mean = mean; p.rstd = rstd;
+    p.seed = seed; p.eps = eps; p.p_drop = p_drop; p.offset = offset;
+    const __bf16 *pl = reinterpret_cast<const __bf16 *>(planes);
+    return bf16 ? try11ln<2>(p, pl, Np, Kp, (hipStream_t)stream) : try11ln<0>(p, pl, Np, Kp, (hipStream_t)stream);
 }
 
 int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {

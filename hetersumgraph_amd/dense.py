@@ -181,6 +181,28 @@ def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, c
     return out
 
 
+def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out, mean, rstd):
+    """y = A @ B^T + bias and out = LayerNorm(dropout(y) + x) (mean / rstd per row) in
+    ONE launch (hsg_gemm_psw_ln: the wide FFN's second GEMM with the LayerNorm of
+    GATLayer.py:40-42 in its epilogue, the dropout stream of hsg_ln_fwd).  Returns
+    False (nothing launched) when the shape has no such plan; the caller then runs
+    gemm_psw + hsg_ln_fwd."""
+    if os.environ.get("HSG_FFN_LN_EPI", "1") == "0":                 # A/B: the separate LN launch
+        return False
+    lib = load()
+    M, K = A.shape
+    N = Bs.N
+    if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in (x, y, out)):
+        return False
+    rc = lib.hsg_gemm_psw_ln(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(bias), ptr(y), ptr(x), ptr(gamma),
+                             ptr(beta), float(eps), float(p_drop), ptr(seed_t), offset, ptr(out), ptr(mean),
+                             ptr(rstd), int(Bs.mode == "bf16"), stream_of(A))
+    if rc == HSG_EINVAL:
+        return False
+    check(rc, "hsg_gemm_psw_ln")
+    return True
+
+
 def gemm_psw_elug(A, Bs, out, x, origin, G):
     """out = out + A @ B^T (the FFN backward's dx += dH W1) and, in the same epilogue,
     G = out * elu'(h) with elu(h) = x - origin (hsg_gemm_f32_psw_elug: the edge

@@ -26,7 +26,8 @@ import torch
 
 from . import rng as hsg_rng
 from ._lib import check, load, ptr, stream_of
-from .dense import gemm, gemm_psw, gemm_psw_elug, get_gemm_dtype, psw_row_tiles, row_tiles, split_weights
+from .dense import (gemm, gemm_psw, gemm_psw_elug, gemm_psw_ln, get_gemm_dtype, psw_row_tiles, row_tiles,
+                    split_weights)
 
 LN_EPS = 1e-5
 
@@ -94,7 +95,17 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
         wsplit = ffn_wsplit(x, w1, b1, w2, b2)
     if wsplit is not None:
         H = gemm_psw(x, wsplit[0], bias=b1, relu=True, out=H_out)    # [n, d_hid]
-        y = gemm_psw(H, wsplit[1], bias=b2)                      # [n, d]
+        # the second GEMM with dropout + residual + LayerNorm in its epilogue when the
+        # shape has a one-round full-row plan (hsg_gemm_psw_ln), else GEMM + hsg_ln_fwd
+        seed_t, off = _draw(x, p_drop, rng)
+        y = torch.empty_like(x)
+        if b2 is not None and gemm_psw_ln(H, wsplit[1], b2, x, gamma, beta, eps, p_drop, seed_t, off, y, out,
+                                          mean, rstd):
+            return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
+        gemm_psw(H, wsplit[1], bias=b2, out=y)                   # [n, d]
+        check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
+                             ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
+        return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
     else:
         H = gemm(x, w1, b_t=True, bias=b1, relu=True, out=H_out)
         y = gemm(H, w2, b_t=True, bias=b2)

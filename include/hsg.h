@@ -266,6 +266,16 @@ int hsg_gemm_f32_slabs(int M, int N, int K, const float *A, int lda, int a_kcont
 int hsg_gemm_bf16_slabs(int M, int N, int K, const float *A, int lda, int a_kcontig,
                         const float *B, int ldb, int b_kcontig, int splits, float *workspace,
                         void *stream);
+/* The S2W FFN's second GEMM with dropout + residual + LayerNorm in its epilogue
+ * (GATLayer.py:39-42: y = w_2(relu(...)) + b2, out = LayerNorm(dropout(y) + x)):
+ * y = A B^T + bias (pre-split B, hsg_wsplit planes; bf16 != 0: the bf16 mode's one
+ * product), out, mean, rstd exactly as hsg_ln_fwd on that y (same dropout stream:
+ * seed[0], offset, index r*N + c).  y, x, out contiguous [M][N].  HSG_EINVAL when the
+ * shape has no one-round full-row plan (N <= 320, 60-100 % of the CUs busy): the caller
+ * then runs hsg_gemm_*_psw + hsg_ln_fwd. */
+int hsg_gemm_psw_ln(int M, int N, int K, const float *A, int lda, const void *planes, const float *bias, float *y,
+                    const float *x, const float *gamma, const float *beta, float eps, float p_drop, const int64_t *seed,
+                    uint32_t offset, float *out, float *mean, float *rstd, int bf16, void *stream);
 /* Rows of the column-partial slab (colsum_part [rows][N]) hsg_gemm_f32_psw /
  * hsg_gemm_bf16_psw write for an M x N x K GEMM: the big-tile plan of the cfg2-class
  * shapes sums per 80- / 48-row band, the others per 64 rows (hsg_gemm_row_tiles). */

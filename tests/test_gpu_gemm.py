@@ -462,3 +462,49 @@ def test_big_tile_psw_epilogues(M, N, K, dtype):
     e = x.double() - origin.double()
     gref = torch.where(e > 0, out.double(), out.double() * (e + 1))
     assert (G.double() - gref).abs().max().item() <= 1e-6 * max(1.0, gref.abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("M,p_drop", [(19200, 0.1), (19200, 0.0), (28800, 0.1), (17000, 0.1)])
+def test_psw_ln_epilogue_equals_gemm_plus_ln(M, p_drop, dtype):
+    """hsg_gemm_psw_ln (the wide FFN's second GEMM with dropout + residual + LayerNorm in
+    its epilogue, GATLayer.py:39-42) against gemm_psw + hsg_ln_fwd on the same operands
+    and dropout stream: y, out, mean and rstd bitwise equal (the same accumulation and
+    the arithmetic of k_ln_fwd4)."""
+    import ctypes
+    from hetersumgraph_amd import rng as hsg_rng
+    from hetersumgraph_amd._lib import load, ptr, stream_of
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, gemm_psw_ln, split_weights
+    N, K = 300, 512
+    torch.manual_seed(M)
+    Hm = torch.relu(torch.randn(M, K, device="cuda"))
+    W2 = torch.randn(N, K, device="cuda") / K ** 0.5
+    b2, gamma, beta = (torch.randn(N, device="cuda") for _ in range(3))
+    x = torch.randn(M, N, device="cuda")
+    with gemm_dtype(dtype):
+        (S,) = split_weights((W2, False))
+    hsg_rng.manual_seed(77)
+    seed_t, off = hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0)
+    y1, out1 = torch.empty(M, N, device="cuda"), torch.empty(M, N, device="cuda")
+    mean1, rstd1 = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    assert gemm_psw_ln(Hm, S, b2, x, gamma, beta, 1e-5, p_drop, seed_t, off, y1, out1, mean1, rstd1)
+    y2 = gemm_psw(Hm, S, bias=b2)
+    out2, mean2, rstd2 = torch.empty_like(out1), torch.empty_like(mean1), torch.empty_like(rstd1)
+    lib = load()
+    assert lib.hsg_ln_fwd(M, N, ptr(y2), ptr(x), ptr(gamma), ptr(beta), 1e-5, float(p_drop), ptr(seed_t), off,
+                          ptr(out2), ptr(mean2), ptr(rstd2), stream_of(x)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.equal(mean1, mean2) and torch.equal(rstd1, rstd2)
+    assert torch.equal(out1, out2)
+
+
+def test_psw_ln_declines_without_plan():
+    from hetersumgraph_amd.dense import gemm_psw_ln, split_weights
+    M, N, K = 1000, 300, 512                      # 11 tiles: far from one round of the GPU
+    A = torch.randn(M, K, device="cuda")
+    (S,) = split_weights((torch.randn(N, K, device="cuda"), False))
+    t = torch.empty(M, N, device="cuda")
+    v = torch.ones(N, device="cuda")
+    assert not gemm_psw_ln(A, S, v, t, v, v, 1e-5, 0.0, None, 0, t.clone(), t.clone(), torch.empty(M, device="cuda"),
+                           torch.empty(M, device="cuda"))
