@@ -1670,6 +1670,14 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const 
     }
 }
 
+// dev opt-in (HSG_GEMM11=1): k_gemm11 measured slower than k_gemm7 on every cfg2 FFN
+// shape (57.5 vs ~49 us: the one round of big tiles leaves the operand loads and the C
+// stores of all CUs unoverlapped at its two ends)
+bool gemm11_on() {
+    const char *e = HSG_DEV_ENV("HSG_GEMM11");
+    return e && atoi(e) == 1;
+}
+
 // cfg2-class shapes only: the two big-tile plans, picked when they run the GEMM in ONE
 // round of at most one block per CU at >= 75 % of the CUs; 0 = not applicable
 int plan11(int M, int N, int cus) {
@@ -2391,30 +2399,26 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
     if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
     if (plan != 27) return launch5<64, 2>(p, pl, Np, Kp, st);
-    if (!(HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0))
-#endif
-    {
-        // one round of big tiles (k_gemm11) where the shape allows; its column partials
-        // are per WM-row band (hsg_gemm_psw_row_tiles), so with colsum_part it never
-        // falls back to the 64-row-slab kernels
+    if (gemm11_on()) {
+        // one round of big tiles (k_gemm11, dev opt-in: measured slower)
+        // where the shape allows; its column partials are per WM-row band
+        // (hsg_gemm_psw_row_tiles), so with colsum_part it never falls back
         const int rc = try11<0>(p, pl, Np, Kp, st);
         if (rc != HSG_EINVAL || (colsum_part && plan11(M, N, device_cus()))) return rc;
     }
+#endif
     if (epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2, 0>(p, pl, Np, Kp, st);             // unaligned / ragged quads
 }
 
 // bf16-mode k_gemm7 (one product per tile): dev plans for the tile / depth / occupancy sweep
 static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
+    int plan = 0;
 #ifdef HSG_DEV
-    if (!(HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0))
-#endif
-    {
+    if (gemm11_on()) {
         const int rc = try11<2>(p, pl, Np, Kp, st);        // one round of big tiles where it applies
         if (rc != HSG_EINVAL || (p.colpart && plan11(p.M, p.N, device_cus()))) return rc;
     }
-    int plan = 0;
-#ifdef HSG_DEV
     if (const char *f = HSG_DEV_ENV("HSG_GEMM7B")) plan = atoi(f);
 #endif
     switch (plan) {
@@ -2463,9 +2467,12 @@ int hsg_gemm_psw_ln(int M, int N, int K, const float *A, int lda, const void *pl
     const auto al = [](const void *q) { return (((uintptr_t)q) & 15) == 0; };
     if (!al(bias) || !al(gamma) || !al(beta) || !al(out) || !al(x) || !al(y)) return HSG_EINVAL;
     if (M == 0) return 0;
-#ifdef HSG_DEV
-    if (HSG_DEV_ENV("HSG_GEMM11LN") && atoi(HSG_DEV_ENV("HSG_GEMM11LN")) == 0) return HSG_EINVAL;
-#endif
+#ifndef HSG_DEV
+    // measured break-even against hsg_gemm_f32_psw + hsg_ln_fwd: the
+    // product library declines, the caller runs the two launches
+    (void)eps; (void)offset;
+    return HSG_EINVAL;
+#else
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
     GemmArgs p{M, N, K, A, lda, nullptr, 0, y, N, bias, x, N, HSG_EPI_STORE, 0, Kp / 32, nullptr, nullptr, 1, 1};
@@ -2473,17 +2480,17 @@ int hsg_gemm_psw_ln(int M, int N, int K, const float *A, int lda, const void *pl
     p.seed = seed; p.eps = eps; p.p_drop = p_drop; p.offset = offset;
     const __bf16 *pl = reinterpret_cast<const __bf16 *>(planes);
     return bf16 ? try11ln<2>(p, pl, Np, Kp, (hipStream_t)stream) : try11ln<0>(p, pl, Np, Kp, (hipStream_t)stream);
+#endif
 }
 
 int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     (void)K; (void)bf16;
     if (M < 0 || N < 1) return 0;
-    const int pl = plan11(M, N, device_cus());
 #ifdef HSG_DEV
-    if (HSG_DEV_ENV("HSG_GEMM11") && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 0) return (M + 63) / 64;
-#endif
+    const int pl = gemm11_on() ? plan11(M, N, device_cus()) : 0;
     if (pl == 1) return (M + 159) / 160 * 2;               // k_gemm11<160, 256, 2, 4>: 80-row bands
     if (pl == 2) return (M + 191) / 192 * 4;               // k_gemm11<192, 160, 4, 2>: 48-row bands
+#endif
     return (M + 63) / 64;
 }
 

@@ -187,7 +187,7 @@ def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out
     GATLayer.py:40-42 in its epilogue, the dropout stream of hsg_ln_fwd).  Returns
     False (nothing launched) when the shape has no such plan; the caller then runs
     gemm_psw + hsg_ln_fwd."""
-    if os.environ.get("HSG_FFN_LN_EPI", "1") == "0":                 # A/B: the separate LN launch
+    if os.environ.get("HSG_FFN_LN_EPI", "0") != "1":                 # opt-in (dev library): break-even
         return False
     lib = load()
     M, K = A.shape

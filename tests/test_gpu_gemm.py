@@ -416,13 +416,15 @@ BIG_SHAPES = [(19200, 512, 300), (19200, 300, 512), (18000, 512, 300), (20000, 3
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("M,N,K", BIG_SHAPES)
-def test_big_tile_psw_epilogues(M, N, K, dtype):
+def test_big_tile_psw_epilogues(M, N, K, dtype, monkeypatch):
     """The pre-split-weight GEMM on the cfg2-class shapes, where hsg_gemm_*_psw runs one
     round of 160 x 256 / 192 x 160 tiles (k_gemm11; hsg_gemm_psw_row_tiles reports its
     80- / 48-row column-partial bands): every epilogue the FFN uses -- bias + ReLU,
     ReLU' mask with column partials, accumulate, and the ELU-gate epilogue -- against
     fp64 ('f32': fp32-class, |err| / sum_k |a_k b_k| < 2e-6; 'bf16': the GEMM of the
-    RNE-rounded operands)."""
+    RNE-rounded operands).  Dev library with HSG_GEMM11=1 (measured slower than k_gemm7)."""
+    skip_unless_dev(False)
+    monkeypatch.setenv("HSG_GEMM11", "1")
     from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, gemm_psw_elug, psw_row_tiles, split_weights
     torch.manual_seed(M + N)
     A = mk(M, K)
@@ -470,8 +472,10 @@ def test_psw_ln_epilogue_equals_gemm_plus_ln(M, p_drop, dtype):
     """hsg_gemm_psw_ln (the wide FFN's second GEMM with dropout + residual + LayerNorm in
     its epilogue, GATLayer.py:39-42) against gemm_psw + hsg_ln_fwd on the same operands
     and dropout stream: y, out, mean and rstd bitwise equal (the same accumulation and
-    the arithmetic of k_ln_fwd4)."""
-    import ctypes
+    the arithmetic of k_ln_fwd4).  Dev library (measured break-even: the product
+    library declines and the FFN runs the GEMM and hsg_ln_fwd)."""
+    skip_unless_dev(False)
+    import os
     from hetersumgraph_amd import rng as hsg_rng
     from hetersumgraph_amd._lib import load, ptr, stream_of
     from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, gemm_psw_ln, split_weights
@@ -487,7 +491,11 @@ def test_psw_ln_epilogue_equals_gemm_plus_ln(M, p_drop, dtype):
     seed_t, off = hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0)
     y1, out1 = torch.empty(M, N, device="cuda"), torch.empty(M, N, device="cuda")
     mean1, rstd1 = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
-    assert gemm_psw_ln(Hm, S, b2, x, gamma, beta, 1e-5, p_drop, seed_t, off, y1, out1, mean1, rstd1)
+    os.environ["HSG_FFN_LN_EPI"] = "1"
+    try:
+        assert gemm_psw_ln(Hm, S, b2, x, gamma, beta, 1e-5, p_drop, seed_t, off, y1, out1, mean1, rstd1)
+    finally:
+        del os.environ["HSG_FFN_LN_EPI"]
     y2 = gemm_psw(Hm, S, bias=b2)
     out2, mean2, rstd2 = torch.empty_like(out1), torch.empty_like(mean1), torch.empty_like(rstd1)
     lib = load()
