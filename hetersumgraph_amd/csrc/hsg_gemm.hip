@@ -1375,7 +1375,7 @@ int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
 // passes of half the waves when the images of all eight do not fit; column partials
 // (colpart) are written per wave row band of WM rows (hsg_gemm_psw_row_tiles).
 // ---------------------------------------------------------------------------------
-template <int BM, int BN, int WGM, int WGN, int PM>
+template <int BM, int BN, int WGM, int WGN, int PM, int S = 2>
 struct Cfg11 {
     static constexpr int NW = WGM * WGN, NT = 64 * NW;
     static constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
@@ -1388,8 +1388,8 @@ struct Cfg11 {
     static constexpr int NLD = (NPC + NW - 1) / NW;        // DMA instructions per wave per K tile
     static constexpr int LDW = WN + 4;                     // epilogue image row (floats)
     static constexpr int EPW = WM * LDW;                   // floats per wave image
-    static constexpr int EPASS = 2 * STAGE_FL >= NW * EPW ? 1 : 2;
-    static constexpr int LDS_FL = 2 * STAGE_FL > NW * EPW / EPASS ? 2 * STAGE_FL : NW * EPW / EPASS;
+    static constexpr int EPASS = S * STAGE_FL >= NW * EPW ? 1 : 2;
+    static constexpr int LDS_FL = S * STAGE_FL > NW * EPW / EPASS ? S * STAGE_FL : NW * EPW / EPASS;
     // epilogue: float4 quads per row, rows per step (lanes past RPS * QPR idle)
     static constexpr int QPR = WN / 4, RPS = 64 / QPR;
     static constexpr int STEPS = (WM + RPS - 1) / RPS;
@@ -1400,10 +1400,13 @@ struct Cfg11 {
     static_assert(LDS_FL * 4 <= 163840, "LDS");
 };
 
-template <int BM, int BN, int WGM, int WGN, int PM, bool LN = false>
-__global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const __bf16 *__restrict__ planes, int Np,
-                                                              int Kp) {
-    using C = Cfg11<BM, BN, WGM, WGN, PM>;
+// S: LDS stages (2: the next K tile's DMA overlaps this tile's MFMAs; 1: one stage,
+// several blocks per CU overlap each other instead), OCC: blocks per CU (launch bounds)
+template <int BM, int BN, int WGM, int WGN, int PM, bool LN = false, int S = 2, int OCC = 1>
+__global__ __launch_bounds__(64 * WGM * WGN, OCC) void k_gemm11(GemmArgs p, const __bf16 *__restrict__ planes,
+                                                                int Np, int Kp) {
+    static_assert(S == 1 || S == 2, "stages");
+    using C = Cfg11<BM, BN, WGM, WGN, PM, S>;
     constexpr int NW = C::NW, WM = C::WM, WN = C::WN, TM = C::TM, TN = C::TN, NL = C::NL;
     constexpr int LDT = BN - 12;                               // LN epilogue: the tile's image, N <= BN - 16 columns
     constexpr int LDS_ALL = LN && BM * LDT > C::LDS_FL ? BM * LDT : C::LDS_FL;
@@ -1426,7 +1429,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const 
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
 
     auto issue = [&](int it) {
-        float *st = lds + (it & 1) * C::STAGE_FL;
+        float *st = lds + (S == 2 ? (it & 1) : 0) * C::STAGE_FL;
         __bf16 *sb = reinterpret_cast<__bf16 *>(st + C::A_FL);
         const int k0 = it * 32;
 #pragma unroll
@@ -1455,15 +1458,19 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const 
             }
         }
     };
-    if (nt > 0) issue(0);
+    if (S == 2 && nt > 0) issue(0);
     const int li = lane & 15, kb = lane >> 4;
     for (int it = 0; it < nt; ++it) {
+        if constexpr (S == 1) {
+            if (it > 0) __syncthreads();                        // every wave is done with the stage
+            issue(it);
+        }
         wait_vmcnt<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (it + 1 < nt) issue(it + 1);                     // lands while this tile is multiplied
-        const float *sa = lds + (it & 1) * C::STAGE_FL;
+        if (S == 2 && it + 1 < nt) issue(it + 1);           // lands while this tile is multiplied
+        const float *sa = lds + (S == 2 ? (it & 1) : 0) * C::STAGE_FL;
         const __bf16 *sb = reinterpret_cast<const __bf16 *>(sa + C::A_FL);
         bf16x8 a[TM][3];
 #pragma unroll
@@ -1675,7 +1682,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void k_gemm11(GemmArgs p, const 
 // stores of all CUs unoverlapped at its two ends)
 bool gemm11_on() {
     const char *e = HSG_DEV_ENV("HSG_GEMM11");
-    return e && atoi(e) == 1;
+    return e && atoi(e) >= 1;
 }
 
 // cfg2-class shapes only: the two big-tile plans, picked when they run the GEMM in ONE
@@ -1701,14 +1708,14 @@ int device_cus() {
     return c;
 }
 
-template <int BM, int BN, int WGM, int WGN, int PM>
+template <int BM, int BN, int WGM, int WGN, int PM, int S = 2, int OCC = 1>
 int launch11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
     p.k_tiles_per_split = Kp / 32;
     if ((p.N + BN - 1) / BN * BN > Np) return HSG_EINVAL;   // B tile rows must exist in the planes
     if (!epi_rows_ok(p)) return HSG_EINVAL;
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm11<BM, BN, WGM, WGN, PM>), dim3((unsigned)g), dim3(64 * WGM * WGN), 0, st, p, planes, Np,
+    hipLaunchKernelGGL((k_gemm11<BM, BN, WGM, WGN, PM, false, S, OCC>), dim3((unsigned)g), dim3(64 * WGM * WGN), 0, st, p, planes, Np,
                        Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
@@ -1742,6 +1749,15 @@ int try11ln(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
 // the big-tile plan of this shape, or HSG_EINVAL when it does not apply
 template <int PM>
 int try11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    // HSG_GEMM11=2 / 3: 128 x 128 tiles of 4 waves (2 x 2 of 64 x 64; 64-row column-partial
+    // bands, as k_gemm7) for N > 320 only, one stage at 3 blocks per CU / two stages at 2
+    const char *e = HSG_DEV_ENV("HSG_GEMM11");
+    const int v = e ? atoi(e) : 0;
+    if (v == 2 || v == 3) {
+        if (p.N <= 320) return HSG_EINVAL;
+        return v == 2 ? launch11<128, 128, 2, 2, PM, 1, 3>(p, planes, Np, Kp, st)
+                      : launch11<128, 128, 2, 2, PM, 2, 2>(p, planes, Np, Kp, st);
+    }
     const int pl = plan11(p.M, p.N, device_cus());
     if (pl == 1) return launch11<160, 256, 2, 4, PM>(p, planes, Np, Kp, st);
     if (pl == 2) return launch11<192, 160, 4, 2, PM>(p, planes, Np, Kp, st);
@@ -2404,7 +2420,8 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
         // where the shape allows; its column partials are per WM-row band
         // (hsg_gemm_psw_row_tiles), so with colsum_part it never falls back
         const int rc = try11<0>(p, pl, Np, Kp, st);
-        if (rc != HSG_EINVAL || (colsum_part && plan11(M, N, device_cus()))) return rc;
+        if (rc != HSG_EINVAL || (colsum_part && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 1 && plan11(M, N, device_cus())))
+            return rc;
     }
 #endif
     if (epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
@@ -2417,7 +2434,8 @@ static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st
 #ifdef HSG_DEV
     if (gemm11_on()) {
         const int rc = try11<2>(p, pl, Np, Kp, st);        // one round of big tiles where it applies
-        if (rc != HSG_EINVAL || (p.colpart && plan11(p.M, p.N, device_cus()))) return rc;
+        if (rc != HSG_EINVAL || (p.colpart && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 1 && plan11(p.M, p.N, device_cus())))
+            return rc;
     }
     if (const char *f = HSG_DEV_ENV("HSG_GEMM7B")) plan = atoi(f);
 #endif
@@ -2487,7 +2505,7 @@ int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     (void)K; (void)bf16;
     if (M < 0 || N < 1) return 0;
 #ifdef HSG_DEV
-    const int pl = gemm11_on() ? plan11(M, N, device_cus()) : 0;
+    const int pl = gemm11_on() && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 1 ? plan11(M, N, device_cus()) : 0;
     if (pl == 1) return (M + 159) / 160 * 2;               // k_gemm11<160, 256, 2, 4>: 80-row bands
     if (pl == 2) return (M + 191) / 192 * 4;               // k_gemm11<192, 160, 4, 2>: 48-row bands
 #endif
