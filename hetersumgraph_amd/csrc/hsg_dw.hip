@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "../../include/hsg.h"
+#include "hsg_dev.h"
 #include "hsg_wsplit.h"
 
 namespace {
@@ -61,21 +62,23 @@ struct Img {
     }
 };
 
-// One operand's K tile in registers: thread t covers (k row, 4 consecutive columns)
-// units t, t + 256, ...; rows past the K slice and columns past M/N load zeros.
-template <int ROWS, int NL>
+// One operand's K tile in registers: thread t of NT covers (k row, 4 consecutive
+// columns) units t, t + NT, ...; rows past the K slice and columns past M/N load
+// zeros; units past the tile (NT not dividing it) are idle.
+template <int ROWS, int NL, int NT = kNT>
 struct Stage {
-    static constexpr int NU = kBK * ROWS / (4 * kNT);
-    static_assert(NU * 4 * kNT == kBK * ROWS, "tile must split evenly over the block");
+    static constexpr int UNITS = kBK * ROWS / 4;
+    static constexpr int NU = (UNITS + NT - 1) / NT;
     f32x4 v[NU];
 
     __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int c0, int nc, int k0, int k1) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const int idx = threadIdx.x + kNT * i;
+            const int idx = threadIdx.x + NT * i;
             const int kk = idx / (ROWS / 4), c = c0 + 4 * (idx % (ROWS / 4));
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
-            if (k0 + kk < k1 && c < nc) x = *reinterpret_cast<const f32x4 *>(g + (size_t)(k0 + kk) * ld + c);
+            if ((UNITS % NT == 0 || idx < UNITS) && k0 + kk < k1 && c < nc)
+                x = *reinterpret_cast<const f32x4 *>(g + (size_t)(k0 + kk) * ld + c);
             v[i] = x;                                  // nc % 4 == 0 (host-checked): whole quads
         }
     }
@@ -83,7 +86,8 @@ struct Stage {
     __device__ __forceinline__ void store(__bf16 *img) const {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const int idx = threadIdx.x + kNT * i;
+            const int idx = threadIdx.x + NT * i;
+            if (UNITS % NT != 0 && idx >= UNITS) continue;
             const int o = Img<ROWS>::off(idx / (ROWS / 4), 4 * (idx % (ROWS / 4)));
             bf16x4 x0, x1, x2;
 #pragma unroll
@@ -228,6 +232,122 @@ __global__ __launch_bounds__(kNT, 2) void k_dw(DwJobs J) {
     else dw_tile<128, 128, NL>(jb, tz, t, J, sA, sB);
 }
 
+// ---------------------------------------------------------------------------------
+// k_dw2: the same contract on one block of 8 waves per CU with a DOUBLE-buffered limb
+// image and register-staged loads two K tiles ahead: tile k+1 is split and stored
+// while tile k is multiplied (one barrier per K tile), the global loads of tile k+3
+// are in flight meanwhile.  k_dw (two blocks of 4 waves per CU, one image each) pays
+// two barriers and the store phase per K tile, and keeps one tile of loads in flight.
+// Waves: 2 x 4 over 160 x 128 (80 x 32 each), 4 x 2 over 128 x 160 (32 x 80), 2 x 4
+// over 128 x 128 (64 x 32).
+// ---------------------------------------------------------------------------------
+constexpr int kNT2 = 512;
+
+template <int BM, int BN, int WGM, int NL>
+__device__ __forceinline__ void dw2_tile(const DwJob &jb, int tz, int t, const DwJobs &J, __bf16 *lds) {
+    constexpr int WGN = 8 / WGM;
+    constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
+    constexpr int IA = NL * Img<BM>::SIZE, IB = NL * Img<BN>::SIZE, IMG = IA + IB;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wm = wid / WGN, wn = wid % WGN;
+    const int ty = t / jb.tiles_n, tx = t % jb.tiles_n;
+    const int m0 = ty * BM, n0 = tx * BN;
+    const int kt_total = (J.K + kBK - 1) / kBK;
+    const int kt0 = tz * J.ktps, kt1 = min(kt_total, kt0 + J.ktps);
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    Stage<BM, NL, kNT2> ra[2];
+    Stage<BN, NL, kNT2> rb[2];
+    auto load = [&](int s, int kt) {
+        if (kt < kt1) {
+            ra[s].load(jb.A, jb.lda, m0, jb.M, kt * kBK, J.K);
+            rb[s].load(jb.B, jb.ldb, n0, jb.N, kt * kBK, J.K);
+        }
+    };
+    auto store = [&](int s, int buf) {
+        ra[s].store(lds + buf * IMG);
+        rb[s].store(lds + buf * IMG + IA);
+    };
+    auto mma = [&](int buf) {
+        const __bf16 *sA = lds + buf * IMG, *sB = lds + buf * IMG + IA;
+        bf16x8 a[NL][TM];
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) a[l][i] = frag<BM>(sA + l * Img<BM>::SIZE, wm * WM + 16 * i, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            bf16x8 b[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l) b[l] = frag<BN>(sB + l * Img<BN>::SIZE, wn * WN + 16 * j, lane);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                if constexpr (NL == 3) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1], acc[i][j], 0, 0, 0);
+                }
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0], acc[i][j], 0, 0, 0);
+            }
+        }
+    };
+    // prologue: tile kt0 in image 0, tiles kt0 + 1 / kt0 + 2 in registers
+    load(0, kt0);
+    load(1, kt0 + 1);
+    store(0, 0);
+    load(0, kt0 + 2);
+    // K tile kt (image (kt - kt0) & 1) is multiplied while tile kt + 1 (register set
+    // (kt - kt0 + 1) & 1) goes into the other image; that set then loads tile kt + 3.
+    // Unrolled by two so the register sets stay compile-time.
+    for (int kt = kt0; kt < kt1; kt += 2) {
+        __syncthreads();
+        if (kt + 1 < kt1) store(1, 1);
+        load(1, kt + 3);
+        mma(0);
+        __builtin_amdgcn_iglp_opt(0);
+        if (kt + 1 >= kt1) break;
+        __syncthreads();
+        if (kt + 2 < kt1) store(0, 0);
+        load(0, kt + 4);
+        mma(1);
+        __builtin_amdgcn_iglp_opt(0);
+    }
+
+    float *ws = jb.ws + (size_t)tz * jb.M * jb.N;
+    const int c = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int n = n0 + wn * WN + 16 * j + c;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int m = m0 + wm * WM + 16 * i + rq + e;
+                if (m < jb.M && n < jb.N) ws[(size_t)m * jb.N + n] = acc[i][j][e];
+            }
+        }
+}
+
+template <int NL>
+__global__ __launch_bounds__(kNT2, 1) void k_dw2(DwJobs J) {
+    __shared__ __attribute__((aligned(16))) __bf16 lds[2 * NL * (Img<160>::SIZE + Img<128>::SIZE)];
+    const int L = xcd_order((int)blockIdx.x, J.total);
+    const int q = (J.nj > 1 && L >= J.j[1].start) ? 1 : 0;
+    const DwJob &jb = J.j[q];
+    const int loc = L - jb.start, tiles = jb.tiles_m * jb.tiles_n;
+    const int tz = loc / tiles, t = loc - tz * tiles;
+    if (jb.cfg == 0) dw2_tile<160, 128, 2, NL>(jb, tz, t, J, lds);
+    else if (jb.cfg == 1) dw2_tile<128, 160, 4, NL>(jb, tz, t, J, lds);
+    else dw2_tile<128, 128, 2, NL>(jb, tz, t, J, lds);
+}
+
 constexpr int kTileM[3] = {160, 128, 128}, kTileN[3] = {128, 160, 128};
 
 // the tile with the least padded output area (ties: the first)
@@ -242,6 +362,12 @@ int pick_cfg(int M, int N) {
 }
 
 bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+// k_dw2 (HSG_DW_V2=1, dev A/B until measured)
+bool dw_v2() {
+    const char *e = HSG_DEV_ENV("HSG_DW_V2");
+    return e && atoi(e) == 1;
+}
 
 }  // namespace
 
@@ -280,7 +406,10 @@ int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float 
     }
     J.total = start;
     hipStream_t st = (hipStream_t)stream;
-    if (bf16) hipLaunchKernelGGL(k_dw<1>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
+    if (dw_v2()) {
+        if (bf16) hipLaunchKernelGGL(k_dw2<1>, dim3((unsigned)J.total), dim3(kNT2), 0, st, J);
+        else hipLaunchKernelGGL(k_dw2<3>, dim3((unsigned)J.total), dim3(kNT2), 0, st, J);
+    } else if (bf16) hipLaunchKernelGGL(k_dw<1>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
     else hipLaunchKernelGGL(k_dw<3>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
