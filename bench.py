@@ -187,9 +187,11 @@ def edge_bytes_fwd(rel, H, D):
 
 
 def edge_bytes_bwd(rel, H, D):
-    """SURVEY §8(d) compulsory bytes of one edge backward (dst + src passes): read
-    dOut and the saved state, gather Z / write dZ and dsigma over the sources, the
-    CSR + CSC edge arrays (10 B / typed edge) and offsets."""
+    """SURVEY §8(d) compulsory bytes of one edge backward (dst + src passes; on S2W
+    the one source-centric pass hsg_gat_bwd_src_g, which reads G instead of dOut and
+    h -- the same count): read dOut and the saved state, gather Z / write dZ and
+    dsigma over the sources, the CSR + CSC edge arrays (10 B / typed edge) and
+    offsets."""
     W = H * D
     return (4 * (2 * rel.n_dst * W + 2 * rel.n_dst * H) + 8 * rel.n_src * (W + H) + 10 * rel.n_typed
             + 8 * (rel.n_dst + rel.n_src) + 8)
@@ -263,7 +265,8 @@ def time_edge_kernels_in_step(step, zero, n_steps):
     """Average duration of every edge-kernel launch INSIDE eager training steps:
     HIP events recorded by the kernels' own dispatch packets on the launching stream
     (hipExtLaunchKernel via hsg_kclock_arm) for each hsg_gat_fwd and each
-    (hsg_gat_bwd_dst + hsg_gat_bwd_src) pair (hetersumgraph_amd._lib.KernelClock),
+    (hsg_gat_bwd_dst + hsg_gat_bwd_src) pair or one-pass hsg_gat_bwd_src_g
+    (hetersumgraph_amd._lib.KernelClock),
     so each launch runs with the caches its real predecessors in the step leave.
     Returns tag -> (mean ms, launches per step)."""
     from hetersumgraph_amd._lib import KernelClock

@@ -32,7 +32,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
-           "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln")
+           "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
+           "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -126,6 +127,9 @@ _SIGS = {
     "hsg_gemm_f32_psw_elug": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P],
     "hsg_gemm_bf16_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
     "hsg_gat_bwd_dst_g": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_src_g_supported": [_RELP, _I, _I],
+    "hsg_gat_bwd_src_g": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gemm_psw_elug_rho": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P],
 }
 _RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_wsplit_dims": None, "hsg_gemm_workspace_floats": ctypes.c_size_t,
             "hsg_attn_params_bwd_workspace_floats": ctypes.c_size_t,

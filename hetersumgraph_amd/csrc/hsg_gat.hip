@@ -1025,6 +1025,165 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
     }
 }
 
+// ------------------------------------ backward: one source-centric pass (S2W) ----
+// (round 4) The edge backward without its destination pass.  The softmax backward of
+// edge e = (u -> v), head k, needs rho_v,k = G_v,k . h_v,k (G = dOut * elu'(h), h the
+// aggregated message; GATLayer.py:118-131 under autograd): the FFN backward GEMM that
+// makes G (hsg_gemm_psw_elug_rho) also writes rho as per-64-column partials, so
+//   dpre_e,k = alpha_e,k (G_v,k . Z_u,k - rho_v,k) * leaky'(pre_e,k)
+// is local to the edge and everything runs over the CSC segments.  Per source u the
+// block's 4 waves split its out-edges (subrange); in blocks of lph edges lane (k, l)
+// fetches edge l's destination, box, alpha and rho for head k, then per edge (4 rows in
+// flight) the lph lanes of head k form G_v,k . Z_u,k over their NE features and every
+// lane of the head accumulates alpha * G_v,k into its features of dZ_u, dpre into
+// dsigma_u,k and (one lane) the box's d tau.  The waves' partials are combined in wave
+// order; d tau and d a1 leave as per-block partials: deterministic.  Replaces the
+// hsg_gat_bwd_dst_g + hsg_gat_bwd_src pair (G read once, no dpre round trip).
+template <int NE, int OCC = 1, int EQ = 4>
+__global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, int D, int lph, float slope,
+                                                      const float *__restrict__ sigma,
+                                                      const float *__restrict__ tau,
+                                                      const float *__restrict__ mv,
+                                                      const float *__restrict__ lv,
+                                                      const float *__restrict__ G,
+                                                      const float *__restrict__ rhop, int rgroups,
+                                                      const float *__restrict__ a1,
+                                                      const float *__restrict__ Z,
+                                                      float *__restrict__ dZ, float *__restrict__ dsigma,
+                                                      float *__restrict__ da1_part,
+                                                      float *__restrict__ dtau_part) {
+    constexpr int WPN = HSG_WAVES;
+    __shared__ float s_acc[HSG_WAVES][512];
+    __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
+    __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const int k = lane / lph, l = lane - (lane / lph) * lph;
+    const bool kact = k < H;
+    const int kc = kact ? k : H - 1, gl = kc * lph, c0 = kc * D;
+    float *sd = s_dtau[wid];
+    for (int i = lane; i < HSG_NT * HSG_HMAX; i += 64) sd[i] = 0.f;
+    wave_lds_sync();
+    // rho partial addresses of head kc: 64-column groups r0 (and r1 when the head
+    // straddles two; D <= 64), slot = head - first head of the group
+    const int r0 = c0 / 64, r1 = (c0 + D - 1) / 64;
+    const int o0 = r0 * 3 + (kc - (64 * r0) / D), o1 = r1 * 3 + (kc - (64 * r1) / D);
+    float da1[NE];                                // wave 0: sum_u dsigma[u,k] Z[u,k,:], (k, l) features
+    int fo[NE];                                   // the lane's features c0 + d, clamped to the head
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+        da1[i] = 0.f;
+        fo[i] = c0 + min(l + lph * i, D - 1);
+    }
+
+    const WorkRange wr = work_range(R.n_src, 1, 0, R.xcd);
+    for (int u_ = wr.first; u_ < wr.end; u_ += wr.stride) {
+        const int u = __builtin_amdgcn_readfirstlane(u_);
+        // opaque per source: the compiler would otherwise hoist a 64-bit address per
+        // feature and array (Z, a1, dZ, s_acc) out of the source loop and spill them
+#pragma unroll
+        for (int i = 0; i < NE; ++i) asm volatile("" : "+v"(fo[i]));
+        const int beg = R.cindptr[u], end = R.cindptr[u + 1];
+        int eb, ee;
+        subrange(beg, end, wid, WPN, eb, ee);
+        const float sig = kact ? sigma[u * H + k] : 0.f;
+        float zk[NE], acc[NE];
+#pragma unroll
+        for (int i = 0; i < NE; ++i) {
+            zk[i] = kact && l + lph * i < D ? Z[(size_t)u * HD + fo[i]] : 0.f;
+            acc[i] = 0.f;
+        }
+        float dsig = 0.f;
+        #pragma unroll 1
+        for (int jb = eb; jb < ee; jb += lph) {
+            const int nb = min(lph, ee - jb);
+            int vA = 0, tA = 0;
+            float aA = 0.f, rA = 0.f, pA = 0.f;
+            if (l < nb) {                                  // edge jb + l, head k
+                const int p = jb + l;
+                vA = R.cdst[p];
+                tA = (int)R.tf[R.cperm[p]];
+                if (kact) {
+                    const float *rr = rhop + (size_t)vA * rgroups * 3;
+                    rA = rr[o0] + (r1 != r0 ? rr[o1] : 0.f);
+                    pA = sig + tau[tA * H + k];
+                    aA = __expf(leaky(pA, slope) - mv[vA * H + k]) / lv[vA * H + k];
+                }
+            }
+            #pragma unroll 1
+            for (int j0 = 0; j0 < nb; j0 += EQ) {
+                float gv[EQ][NE];
+#pragma unroll
+                for (int q = 0; q < EQ; ++q) {
+                    // lane j = (head 0, l = j) holds edge j's destination; scalar row base,
+                    // per-lane feature offsets shared by every row (saddr + voffset loads)
+                    const int v = __builtin_amdgcn_readfirstlane(__shfl(vA, min(j0 + q, nb - 1)));
+                    const float *gr = G + (size_t)v * HD;
+#pragma unroll
+                    for (int i = 0; i < NE; ++i) gv[q][i] = gr[fo[i]];
+                }
+#pragma unroll
+                for (int q = 0; q < EQ; ++q) {
+                    const int j = j0 + q;
+                    if (j >= nb) break;                        // wave-uniform
+                    float dot = 0.f;
+#pragma unroll
+                    for (int i = 0; i < NE; ++i) dot = fmaf(gv[q][i], zk[i], dot);     // zk = 0 past D
+                    dot = group_sum(dot, lph);
+                    const float a = __shfl(aA, gl + j), r = __shfl(rA, gl + j), pr = __shfl(pA, gl + j);
+                    const int t = __shfl(tA, gl + j);
+                    const float ds = a * (dot - r);
+                    const float dp = pr > 0.f ? ds : ds * slope;
+#pragma unroll
+                    for (int i = 0; i < NE; ++i) acc[i] = fmaf(a, gv[q][i], acc[i]);
+                    dsig += dp;
+                    if (kact && l == 0) sd[t * H + k] += dp;
+                }
+            }
+        }
+        // combine the 4 waves' partials in wave order
+#pragma unroll
+        for (int i = 0; i < NE; ++i)
+            if (kact && l + lph * i < D) s_acc[wid][fo[i]] = acc[i];
+        if (kact && l == 0) s_dsig[wid][k] = dsig;
+        __syncthreads();
+        if (wid == 0) {
+            float ds = 0.f;
+#pragma unroll
+            for (int w = 0; w < WPN; ++w) ds += s_dsig[w][kc];
+            if (dsigma && kact && l == 0) dsigma[u * H + k] = ds;
+#pragma unroll
+            for (int i = 0; i < NE; ++i) {
+                if (kact && l + lph * i < D) {
+                    const int f = fo[i];
+                    float a = 0.f;
+#pragma unroll
+                    for (int w = 0; w < WPN; ++w) a += s_acc[w][f];
+                    if (a1) a = fmaf(ds, a1[f], a);
+                    dZ[(size_t)u * HD + f] = a;
+                    da1[i] = fmaf(ds, zk[i], da1[i]);
+                }
+            }
+        }
+        __syncthreads();                                   // s_acc / s_dsig reused by the next source
+    }
+    if (wid == 0 && da1_part) {                            // block partial of d a1
+#pragma unroll
+        for (int i = 0; i < NE; ++i)
+            if (kact && l + lph * i < D) da1_part[(size_t)blockIdx.x * HD + fo[i]] = da1[i];
+    }
+    // block partial of d tau (s_dtau written by lane (k, 0) of each wave; the loop's
+    // last barrier orders them, this one covers a block without sources)
+    __syncthreads();
+    const int nt = HSG_NT * H;
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+        float a = 0.f;
+#pragma unroll
+        for (int w = 0; w < HSG_WAVES; ++w) a += s_dtau[w][i];
+        dtau_part[(size_t)blockIdx.x * nt + i] = a;
+    }
+}
+
 // Head-lane src pass for narrow heads (D = DV = 8, short CSC segments: the W2S word
 // sources, ~2 sentence edges each at config 2).  Lane = (source slot s, head k) with
 // hp = nextpow2(H) lanes per source, so a wave carries 64 / hp sources at once and each
@@ -1664,6 +1823,38 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
     if (tau_mode == HSG_TAU_TABLE) return HSG_S(HSG_TAU_TABLE, 1);      // wpn == 4 took the w = 5 kernel above
     return HSG_S(HSG_TAU_PER_EDGE, 1);
 #undef HSG_S
+}
+
+int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D) {
+    if (!rel || !shape_ok(H, D) || D < 32 || D > 64 || src_wpn(rel) != 4) return 0;
+    return (D + lanes_per_head(H) - 1) / lanes_per_head(H) <= 8;
+}
+
+int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                      const float *m, const float *l, const float *G, const float *rho, int rho_groups,
+                      const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                      float *dtau_part, void *stream) {
+    if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !G || !rho || !Z || !dZ || !dtau_part) return HSG_EINVAL;
+    if (rho_groups != (H * D + 63) / 64) return HSG_EINVAL;
+    const RelPtrs R = rel_ptrs(rel);
+    const dim3 grid(hsg_gat_bwd_src_blocks(rel));
+    hipStream_t st = (hipStream_t)stream;
+    const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;
+#define HSG_SG(NE_, OCC_, EQ_)                                                                               \
+    HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope, sigma,   \
+                tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part)
+    // EQ: destination rows in flight per wave, as many as fit 5 blocks per CU unspilled
+#ifdef HSG_DEV
+    const char *eq = HSG_DEV_ENV("HSG_SRCG_EQ");                               // dev A/B
+    if (eq && atoi(eq) == 4 && ne > 4 && ne <= 7) HSG_SG(7, 4, 4);
+    else if (eq && atoi(eq) == 1 && ne > 4 && ne <= 7) HSG_SG(7, 5, 1);
+    else
+#endif
+    if (ne <= 4) HSG_SG(4, 5, 4);
+    else if (ne <= 7) HSG_SG(7, 5, 2);
+    else HSG_SG(8, 5, 1);
+#undef HSG_SG
+    return launch_status();
 }
 
 int hsg_attn_src_logits(int n, int H, int D, const float *Z, const float *a1, float *sigma,

@@ -38,6 +38,7 @@
 // replace eight v_mfma_f32_32x32x2_f32 (64 cycles) per 16-deep k step: a 2.67x
 // higher MFMA ceiling than the exact-f32 instruction (gfx950 has no xf32).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -79,6 +80,11 @@ struct GemmArgs {
     const float *aux2 = nullptr;
     const float *aux3 = nullptr;
     float *C2 = nullptr;
+    // optional with HSG_EPI_ADD_ELUG: rho partials of the edge backward, rho[m][g][s] =
+    // sum over the columns c of 64-column group g in head c / rho_d = 64 g / rho_d + s
+    // of C2 * h with h = elu^-1(e) (hsg_gemm_psw_elug_rho)
+    float *rho = nullptr;
+    int rho_d = 0;
     // k_gemm11's LayerNorm epilogue only (hsg_gemm_*_psw_ln): C = the pre-dropout FFN
     // output y, lnout = LN(dropout(y) + aux) with gamma / beta, per-row mean / rstd
     const float *gamma = nullptr, *beta = nullptr;
@@ -925,6 +931,21 @@ __device__ __forceinline__ void epi_store(const f32x16 (&acc)[TN], int row0, int
 // -4..-9 us per launch).  Lane -> (row step, quad): QPR quads per row, RPS = 64 / QPR
 // rows per step; lanes past RPS * QPR idle.  Each lane keeps one quad, so its column
 // sums are per-lane partials over its rows.
+// sum over each aligned 16-lane row of the wave, in every lane: four DPP adds (xor 1,
+// xor 2 by quad permutes, then half-row and row mirrors) -- VALU only, where
+// __shfl_xor lowers to a chain of ds_bpermute round trips through the LDS path
+__device__ __forceinline__ float row16_sum(float x) {
+    const auto dpp = [](float v, auto ctrl) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), decltype(ctrl)::value,
+                                                                  0xf, 0xf, true));
+    };
+    x += dpp(x, std::integral_constant<int, 0xb1>{});     // quad_perm [1,0,3,2]
+    x += dpp(x, std::integral_constant<int, 0x4e>{});     // quad_perm [2,3,0,1]
+    x += dpp(x, std::integral_constant<int, 0x141>{});    // row_half_mirror
+    x += dpp(x, std::integral_constant<int, 0x140>{});    // row_mirror
+    return x;
+}
+
 template <int BN>
 struct EpiRows {
     static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
@@ -965,32 +986,69 @@ struct EpiRows {
         const int q = lane % QPR, rs = lane / QPR;
         const int n = col0 + 4 * q;
         const bool qok = rs < RPS && n < p.N;
+        // rho partials (BN % 64 == 0: the 16 lanes of a 64-column group are lanes
+        // 16c .. 16c + 15 of one row step): head slot of each of the lane's 4 columns
+        constexpr bool RHO_OK = BN % 64 == 0;
+        const bool rho = RHO_OK && p.epi == HSG_EPI_ADD_ELUG && p.rho;
+        int slot[4] = {3, 3, 3, 3};
+        if (rho) {
+            const int hb = (n & ~63) / p.rho_d;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) slot[e] = n + e < p.N ? (n + e) / p.rho_d - hb : 3;
+        }
         csum = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < STEPS; ++t) {
             const int r = t * RPS + rs, m = row0 + r;
-            if (!qok || r >= 32 || m >= p.M) continue;
-            f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
-            if (p.epi == HSG_EPI_RELU_BWD) {
+            const bool rok = r < 32 && m < p.M;
+            float c[3] = {0.f, 0.f, 0.f};
+            if (qok && rok) {
+                f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
+                if (p.epi == HSG_EPI_RELU_BWD) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
-            } else {
-                v += bn;
-                if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
-                if (p.relu) {
+                    for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
+                } else {
+                    v += bn;
+                    if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
+                    if (p.relu) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                    }
+                }
+                if (!NS || v[0] == 1234.5f) *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+                if (p.epi == HSG_EPI_ADD_ELUG) {
+                    // G = dOut * elu'(h): 1 for e = elu(h) > 0, else e + 1 = exp(h) (continuous at 0)
+                    f32x4 g;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
+                    *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
+                    if (rho) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            // h = log1p(e) for e <= 0 as log(u) * e / (u - 1), u = 1 + e (a few
+                            // ulp without libm's log1pf).  u <= 0: the rounded e reached -1
+                            // (exp(h) below ulp(origin)), G h -> 0 there
+                            const float x = ex[t][e], u = 1.f + x;
+                            const float h = x > 0.f ? x : (u == 1.f ? x : __logf(u) * __fdividef(x, u - 1.f));
+                            const float gh = x > 0.f || u > 0.f ? g[e] * h : 0.f;
+                            c[0] += slot[e] == 0 ? gh : 0.f;
+                            c[1] += slot[e] == 1 ? gh : 0.f;
+                            c[2] += slot[e] == 2 ? gh : 0.f;
+                        }
+                    }
+                }
+                csum += v;
+            }
+            if (rho) {                                      // wave-uniform: sums over the group
+#pragma unroll
+                for (int s = 0; s < 3; ++s) c[s] = row16_sum(c[s]);
+                if ((q & 15) == 0 && qok && rok) {
+                    float *dst = p.rho + ((size_t)m * ((p.N + 63) / 64) + n / 64) * 3;
+                    dst[0] = c[0];
+                    dst[1] = c[1];
+                    dst[2] = c[2];
                 }
             }
-            if (!NS || v[0] == 1234.5f) *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
-            if (p.epi == HSG_EPI_ADD_ELUG) {
-                // G = dOut * elu'(h): 1 for e = elu(h) > 0, else e + 1 = exp(h) (continuous at 0)
-                f32x4 g;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
-                *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
-            }
-            csum += v;
         }
     }
 };
@@ -2512,20 +2570,30 @@ int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     return (M + 63) / 64;
 }
 
-int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
-                          const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
-                          void *stream) {
+int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                          const float *aux, const float *x, const float *origin, float *G, int ld, float *rho,
+                          int head_dim, int bf16, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G) return HSG_EINVAL;
     if ((lda & 3) || (K & 3) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N)
         return HSG_EINVAL;
+    if (rho && (head_dim < 32 || N % head_dim)) return HSG_EINVAL;   // <= 3 heads per 64-column group
     if (M == 0 || N == 0) return 0;
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
     GemmArgs p{M, N, K, A, lda, nullptr, 0, C, ldc, nullptr, aux, ld, HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr,
                1, 1, x, origin, G};
+    p.rho = rho;
+    p.rho_d = head_dim;
     if (!epi_rows_ok(p)) return HSG_EINVAL;
+    // every psw plan's column tile is a multiple of 64 (EpiRows' rho groups)
     if (bf16) return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
     return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
+int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                          const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
+                          void *stream) {
+    return hsg_gemm_psw_elug_rho(M, N, K, A, lda, planes, C, ldc, aux, x, origin, G, ld, nullptr, 0, bf16, stream);
 }
 
 #ifdef HSG_GEMM_CENSUS

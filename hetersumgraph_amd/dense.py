@@ -203,22 +203,27 @@ def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out
     return True
 
 
-def gemm_psw_elug(A, Bs, out, x, origin, G):
+def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
     """out = out + A @ B^T (the FFN backward's dx += dH W1) and, in the same epilogue,
     G = out * elu'(h) with elu(h) = x - origin (hsg_gemm_f32_psw_elug: the edge
-    layer's ELU gate, GAT.py:56-57, moved out of its dst pass).  Returns False (nothing
-    launched) when the shape / alignment does not allow the fused epilogue."""
+    layer's ELU gate, GAT.py:56-57, moved out of its dst pass).  ``rho`` ([M,
+    ceil(N/64), 3]): also the per-64-column partials of G . h per head of ``head_dim``
+    columns (hsg_gemm_psw_elug_rho) for the one-pass edge backward.  Returns False
+    (nothing launched) when the shape / alignment does not allow the fused epilogue."""
     lib = load()
     M, K = A.shape
     N = Bs.N
     ts = (out, x, origin, G)
     if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in ts):
         return False
-    rc = lib.hsg_gemm_f32_psw_elug(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
-                                   ptr(origin), ptr(G), N, int(Bs.mode == "bf16"), stream_of(A))
+    if rho is not None and (rho.shape != (M, (N + 63) // 64, 3) or not rho.is_contiguous()):
+        return False
+    rc = lib.hsg_gemm_psw_elug_rho(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
+                                   ptr(origin), ptr(G), N, ptr(rho), int(head_dim), int(Bs.mode == "bf16"),
+                                   stream_of(A))
     if rc == HSG_EINVAL:
         return False
-    check(rc, "hsg_gemm_f32_psw_elug")
+    check(rc, "hsg_gemm_psw_elug_rho")
     return True
 
 

@@ -127,8 +127,10 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
     there (one job per output across every call with the same key) instead of run
     here.  ``elug`` = (origin, G): the FFN input x is the edge layer's elu(h) + origin,
     and its ELU gate G = dx * elu'(h) goes into G from the last GEMM's epilogue
-    (hsg_gemm_f32_psw_elug) -- only on the pre-split-weight path.  Returns dx (a fresh
-    tensor), or (dx, G produced?) with ``elug``."""
+    (hsg_gemm_f32_psw_elug) -- only on the pre-split-weight path; (origin, G, rho,
+    head_dim): also the rho partials of the one-pass edge backward
+    (hsg_gemm_psw_elug_rho).  Returns dx (a fresh tensor), or (dx, G produced?) with
+    ``elug``."""
     lib = load()
     x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off, wsplit = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
@@ -158,7 +160,7 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
         dH_out = act_grads[1] if act_grads is not None else None
         if wsplit is not None:
             dH = gemm_psw(dy, wsplit[2], relu_mask=H, colsum_part=hpart, out=dH_out)
-            if elug is not None and gemm_psw_elug(dH, wsplit[3], dx, x, elug[0], elug[1]):
+            if elug is not None and gemm_psw_elug(dH, wsplit[3], dx, x, *elug):
                 g_done = True
             else:
                 gemm_psw(dH, wsplit[3], out=dx, add=dx)

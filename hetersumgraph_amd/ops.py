@@ -188,7 +188,7 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     return (out if origin is not None else h), saved
 
 
-def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None):
+def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
     """Backward of :func:`gat_table_fwd`: 3 launches (dst pass, src pass with the
     d a1 partials, parameter backward).  Returns dZ (None with dZ=False).  ``dst`` =
     (dattn, dwf, dbf, dT, acc_head, acc_T): gradient buffers written or added into
@@ -197,7 +197,9 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None):
     caller runs :func:`attn_params_finish` once for all applications of the layer.
     The origin gradient is ``dout`` itself.  ``G``: the rows dOut * elu'(h), already
     made by the FFN's last GEMM (a forward without h): the dst pass reads them
-    (hsg_gat_bwd_dst_g)."""
+    (hsg_gat_bwd_dst_g).  ``rho`` (with G): that GEMM's per-64-column partials of
+    G_v . h_v (hsg_gemm_psw_elug_rho) -- the whole backward is then ONE source-centric
+    launch (hsg_gat_bwd_src_g) instead of the dst + src pair."""
     lib = load()
     Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin, xo = saved
     dout = dout.contiguous()
@@ -206,30 +208,38 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None):
     g_given = G is not None
     if not g_given:
         G = torch.empty_like(dout)
-    dpre = Z.new_empty(rel.n_typed, H)
-    nbd = lib.hsg_gat_bwd_blocks(relp)
+    merged = rho is not None
+    if merged and not g_given:
+        raise ValueError("gat_table_bwd: rho partials without their G rows")
+    nbs = lib.hsg_gat_bwd_src_blocks(relp)
+    nbd = nbs if merged else lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
     dZt = torch.empty_like(Z)
-    nbs = lib.hsg_gat_bwd_src_blocks(relp)
     da1p = Z.new_empty(nbs, H * D)
     tok = _clock_start(("gat_bwd", rel.kind), Z)
     try:
-        if g_given:                         # G from the FFN epilogue (forward without h)
-            if xo is None:
-                raise ValueError("gat_table_bwd: G rows given for a forward that stored h")
-            check(lib.hsg_gat_bwd_dst_g(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau), ptr(m),
-                                        ptr(l), ptr(G), ptr(dpre), ptr(dtp), st), "hsg_gat_bwd_dst_g")
-        elif xo is not None:                # forward without h (keep_h=False)
-            check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                                          ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                                          ptr(dtp), st), "hsg_gat_bwd_dst_noh")
+        if g_given and xo is None:
+            raise ValueError("gat_table_bwd: G rows given for a forward that stored h")
+        if merged:                          # one source-centric pass (G and rho from the FFN epilogue)
+            check(lib.hsg_gat_bwd_src_g(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G), ptr(rho),
+                                        rho.shape[1], ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp), st),
+                  "hsg_gat_bwd_src_g")
         else:
-            check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
-                                      ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
-                                      ptr(dtp), st), "hsg_gat_bwd_dst")
-        check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
-                                  ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
-              "hsg_gat_bwd_src")
+            dpre = Z.new_empty(rel.n_typed, H)
+            if g_given:                     # G from the FFN epilogue (forward without h)
+                check(lib.hsg_gat_bwd_dst_g(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau), ptr(m),
+                                            ptr(l), ptr(G), ptr(dpre), ptr(dtp), st), "hsg_gat_bwd_dst_g")
+            elif xo is not None:            # forward without h (keep_h=False)
+                check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                              ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                              ptr(dtp), st), "hsg_gat_bwd_dst_noh")
+            else:
+                check(lib.hsg_gat_bwd_dst(relp, H, D, HSG_TAU_TABLE, int(has_origin), slope, ptr(Z), ptr(sigma),
+                                          ptr(tau), ptr(h), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
+                                          ptr(dtp), st), "hsg_gat_bwd_dst")
+            check(lib.hsg_gat_bwd_src(relp, H, D, HSG_TAU_TABLE, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l),
+                                      ptr(G), ptr(dpre), ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), st),
+                  "hsg_gat_bwd_src")
     except BaseException:
         _clock_abort(tok)
         raise

@@ -30,12 +30,13 @@ HSG_CHECK_NAN=1).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
 
 from . import rng as hsg_rng
-from ._lib import stream_of
+from ._lib import load, stream_of
 from .dense import gemm, gemm_dw_slabs, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
@@ -168,6 +169,15 @@ def _attn_dst(grads, lay, T):
     return dattn, dwf, dbf, dT, a_h, a_T
 
 
+def _merged_bwd(gsaved):
+    """The one-pass edge backward (hsg_gat_bwd_src_g) covers this application's
+    relation and head shape (HSG_GAT_MERGED=0: the dst + src pair, for A/B tests)."""
+    if os.environ.get("HSG_GAT_MERGED", "1") == "0":
+        return False
+    rel, H, D = gsaved[11], gsaved[12], gsaved[13]
+    return bool(load().hsg_gat_bwd_src_g_supported(ctypes.byref(rel.cstruct()), H, D))
+
+
 def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grads=None, batch=None):
     """Backward of one application.  Parameter gradients go to ``grads``; the
     neighbour's gradient is written (or added, nb_acc) into ``nb_grad`` when that is
@@ -182,9 +192,13 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
     # forward without h and the FFN on the pre-split path: the G rows of the edge
     # backward come out of the FFN's last GEMM (dx epilogue)
-    G = None
+    G = rho = None
     elug = (gsaved[16][1], torch.empty_like(fsaved[0])) if gsaved[16] is not None and fsaved[11] is not None \
         else None
+    if elug is not None and _merged_bwd(gsaved):
+        # ... and the rho partials, so the edge backward is one source-centric pass
+        n_dst, HD = elug[1].shape
+        elug += (elug[1].new_empty(n_dst, (HD + 63) // 64, 3), gsaved[13])
     if act_grads is None:
         dw1, a_w1 = grads.dst(lay.w1)
         dw2, a_w2 = grads.dst(lay.w2)
@@ -197,11 +211,12 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     if elug is not None:
         dx, g_done = dx
         G = elug[1] if g_done else None
+        rho = elug[2] if g_done and len(elug) > 2 else None
     need_dz = nb_grad is not None or lay.W.requires_grad
     if stage is not None:
-        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage, G=G)
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage, G=G, rho=rho)
     else:
-        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(grads, lay, T), G=G)
+        dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, dst=_attn_dst(grads, lay, T), G=G, rho=rho)
     if need_dz:
         dW, a_W = grads.dst(lay.W)
         if hsaved is not None:

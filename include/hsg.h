@@ -112,6 +112,21 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
 /* Number of partial rows hsg_gat_bwd_src writes into da1_part. */
 int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
 
+/* The whole backward of one table-mode application in ONE source-centric pass (the
+ * S2W shape: D in [32, 64], long CSC segments -- hsg_gat_bwd_src_g_supported), given
+ * G = dOut * elu'(h) and rho[v][g][s] = the per-64-column-group partials of
+ * G_v . h_v that hsg_gemm_psw_elug_rho writes (rho_groups = ceil(H*D / 64)):
+ *   dpre[e,k]   = alpha_ek (G[v,k,:] . Z[u,k,:] - rho_vk) * leaky'(pre_ek)
+ *   dZ, dsigma, da1_part as hsg_gat_bwd_src, dtau_part[b][box][k] per-block partials
+ * with b < hsg_gat_bwd_src_blocks(rel) for both slabs.  Replaces hsg_gat_bwd_dst_g +
+ * hsg_gat_bwd_src (GATLayer.py:118-131 backward); results equal up to fp32 rounding
+ * (rho is summed from G.h instead of sum_e alpha_e G.Z_u). */
+int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D);
+int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                      const float *m, const float *l, const float *G, const float *rho, int rho_groups,
+                      const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                      float *dtau_part, void *stream);
+
 /* Measurement hook (bench.py's in-step kernel clock; not part of the reference
  * surface): the next hsg_gat_fwd launched FROM THE CALLING THREAD ON `stream` records
  * start_event / stop_event (hipEvent_t created with timing) from its kernel's own
@@ -244,6 +259,13 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
                           const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
                           void *stream);
+/* hsg_gemm_f32_psw_elug that also writes rho (optional: NULL = the call above) for
+ * hsg_gat_bwd_src_g: rho[m][g][s], g < ceil(N / 64), s < 3, = sum of G[m,c] * h[m,c]
+ * over the columns c of group g (64g <= c < 64g + 64) in head c / head_dim =
+ * 64g / head_dim + s, h = e for e > 0 else log1p(e); head_dim >= 32 divides N. */
+int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
+                          const float *aux, const float *x, const float *origin, float *G, int ld, float *rho,
+                          int head_dim, int bf16, void *stream);
 /* hsg_gemm_bf16 (A and the weight rounded to bf16 RNE, fp32 accumulation: config 5's
  * mode) on the pre-split weight: only its limb plane 0 = RNE(W) is read, one bf16
  * MFMA product per element pair.  Same arguments as hsg_gemm_f32_psw; N % 4 == 0 and

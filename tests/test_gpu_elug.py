@@ -131,3 +131,120 @@ def test_dst_pass_with_given_G_equals_noh_pass():
         torch.cuda.synchronize()
         outs.append((dpre, dtp))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def _rho_ref(G, h, D):
+    """fp64 rho partials: [M, ceil(N/64), 3], slot s of 64-column group g = the sum of
+    G * h over the group's columns in head 64g // D + s (hsg_gemm_psw_elug_rho)."""
+    M, N = G.shape
+    ng = (N + 63) // 64
+    prod = G.double() * h.double()
+    out = torch.zeros(M, ng, 3, dtype=torch.float64, device=G.device)
+    for g in range(ng):
+        hb = 64 * g // D
+        for s in range(3):
+            cols = [c for c in range(64 * g, min(64 * g + 64, N)) if c // D == hb + s]
+            if cols:
+                out[:, g, s] = prod[:, cols].sum(1)
+    return out
+
+
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+@pytest.mark.parametrize("M", [19200, 777])
+def test_psw_elug_rho_partials(M, mode):
+    """hsg_gemm_psw_elug_rho: the same C and G as hsg_gemm_f32_psw_elug (bitwise), and
+    rho = per-head sums of G * h over each 64-column group, h = elu^-1(x - origin),
+    against fp64 on the kernel's own G with the TRUE h.  G h = v (1 + e) log(1 + e)
+    is taken from the rounded e = x - origin, whose error delta is <= 4 ulp(|x| +
+    |origin|) + ulp(1); its derivative in e is v (h + 1), so the bound per entry is
+    sum |v| delta (|h| + 1) + 1e-5 sum |G| (|h| + 1) over the entry's columns (the
+    second term: log / division / summation roundings).  Rows with h = -20 take the
+    e <= -1 branch (G h = 0) where e + 1 rounds to zero or below."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    N, K, D = 300, 512, 50
+    torch.manual_seed(M + 1)
+    dH = torch.randn(M, K, device="cuda")
+    W1 = torch.randn(K, N, device="cuda") / K ** 0.5
+    with gemm_dtype(mode):
+        (S,) = split_weights((W1, True))
+    ds = torch.randn(M, N, device="cuda")
+    origin = torch.randn(M, N, device="cuda")
+    h = 2 * torch.randn(M, N, device="cuda")
+    h[::7] = 0.0
+    h[1::11] = -20.0                                           # exp(h) ~ 2e-9: e + 1 rounds to ~0
+    x = torch.nn.functional.elu(h) + origin
+    outs = []
+    for with_rho in (False, True):
+        out = ds.clone()
+        G = torch.empty_like(ds)
+        rho = torch.full((M, (N + 63) // 64, 3), float("nan"), device="cuda") if with_rho else None
+        assert gemm_psw_elug(dH, S, out, x, origin, G, rho, D if with_rho else 0)
+        outs.append((out, G, rho))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    G, rho = outs[1][1], outs[1][2]
+    ref = _rho_ref(G, h, D)
+    out = outs[1][0]
+    delta = 4 * 2.0 ** -23 * (x.abs() + origin.abs()) + 2.0 ** -23
+    bound = _rho_ref(out.abs(), delta * (h.abs() + 1), D) + 1e-5 * _rho_ref(G.abs(), h.abs() + 1, D) + 1e-12
+    err = (rho.double() - ref).abs()
+    print(f"{mode} M={M}: worst rho error / bound {(err / bound).max().item():.3f}")
+    assert torch.isfinite(rho).all()
+    assert (err <= bound).all()
+
+
+def test_psw_elug_rho_declines_bad_head_dim():
+    from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
+    W1 = torch.randn(64, 300, device="cuda")
+    (S,) = split_weights((W1, True))
+    t = torch.randn(50, 300, device="cuda")
+    rho = torch.empty(50, 5, 3, device="cuda")
+    for hd in (16, 70):                                         # < 32 / does not divide N
+        assert not gemm_psw_elug(torch.randn(50, 64, device="cuda"), S, t.clone(), t, t, torch.empty_like(t),
+                                 rho, hd)
+
+
+@pytest.mark.parametrize("n_docs,N,W,k", [(4, 35, 600, 36), (3, 20, 200, 24)])
+def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k):
+    """hsg_gat_bwd_src_g (one source-centric pass on G and the rho partials) against
+    hsg_gat_bwd_dst_g + hsg_gat_bwd_src on the same S2W application, forward stats
+    from a real forward: dZ and every attention-parameter gradient within 1e-5 of the
+    output's scale (the passes differ only in where rho = G_v . h_v is summed)."""
+    import ctypes
+    from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd._lib import load
+    from hetersumgraph_amd.ops import LEAKY_SLOPE, gat_table_bwd, gat_table_fwd
+    lib = load()
+    rng = np.random.default_rng(n_docs)
+    docs = [synth.make_hsg_doc(rng, N=N, W=W, k=k) for _ in range(n_docs)]
+    Gr = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
+    Gr.to(torch.device("cuda"))
+    rel = Gr.relation("S2W")
+    H, D = 6, 50
+    assert lib.hsg_gat_bwd_src_g_supported(ctypes.byref(rel.cstruct()), H, D)
+    torch.manual_seed(k)
+    Z = torch.randn(rel.n_src, H * D, device="cuda")
+    attn = torch.randn(H, 3 * D, device="cuda") * 0.3
+    T = torch.randn(10, 50, device="cuda")
+    wf = torch.randn(H, D, 50, device="cuda") * 0.1
+    bf = torch.randn(H, D, device="cuda") * 0.1
+    org = torch.randn(rel.n_dst, H * D, device="cuda")
+    out, saved = gat_table_fwd(Z, attn, T, wf, bf, org, rel, H, D, LEAKY_SLOPE, no_h=True)
+    assert saved[16] is not None
+    dout = torch.randn_like(out)
+    e = (out - org).double()
+    G = torch.where(e > 0, dout.double(), dout.double() * (e + 1)).float()
+    h = torch.where(e > 0, e, torch.log1p(e.clamp_min(-1 + 1e-12)))
+    rho = _rho_ref(G, h, D).float().contiguous()
+    res = []
+    for merged in (False, True):
+        dst = (torch.zeros_like(attn), torch.zeros_like(wf), torch.zeros_like(bf), torch.zeros_like(T), False, False)
+        dZ = gat_table_bwd(saved, dout, dst=dst, G=G, rho=rho if merged else None)
+        res.append((dZ,) + dst[:4])
+    torch.cuda.synchronize()
+    for name, a, b in zip(("dZ", "dattn", "dwf", "dbf", "dT"), res[1], res[0]):
+        tol = 1e-5 * max(1.0, b.abs().max().item())
+        err = (a - b).abs().max().item()
+        print(f"{name}: max |one-pass - two-pass| {err:.3e} (tol {tol:.3e})")
+        assert err <= tol, name
