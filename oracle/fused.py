@@ -98,26 +98,52 @@ def gat_heads(rel, X, params, T, prefix="", keep=None, scale=1.0):
     return torch.cat(outs, 1)
 
 
-def ffn(x, params, prefix="", keep=None, scale=1.0):
+# ReLU gates within fp32 resolution of zero (see ``ffn``): |v| below this fraction of
+# the pre-activation's magnitude sum sum_c |x_c w_c| + |b|
+GATE_BAND = 2.0 ** -16
+
+
+def ffn(x, params, prefix="", keep=None, scale=1.0, gate=None):
     """PositionwiseFeedForward (GATLayer.py:35-44).  ``keep``: train mode, the bool
-    [n, d] keep-mask of the output dropout (GATLayer.py:41), kept values x ``scale``."""
+    [n, d] keep-mask of the output dropout (GATLayer.py:41), kept values x ``scale``.
+    ``gate``: the bool [n, d_hid] ReLU gates an fp32 implementation took (H > 0).
+    Where the fp64 pre-activation v lies within GATE_BAND of its magnitude sum of
+    zero, fp32 rounding of the inputs decides the gate either way, so the oracle takes
+    the implementation's gate there (its backward then follows the same branch; the
+    forward value moves by at most |v|); everywhere else the gates must agree, which
+    is asserted."""
     w1 = params[f"{prefix}ffn.w_1.weight"].squeeze(-1)
     w2 = params[f"{prefix}ffn.w_2.weight"].squeeze(-1)
-    y = F.relu(x @ w1.t() + params[f"{prefix}ffn.w_1.bias"]) @ w2.t() + params[f"{prefix}ffn.w_2.bias"]
+    b1 = params[f"{prefix}ffn.w_1.bias"]
+    v = x @ w1.t() + b1
+    if gate is None:
+        h = F.relu(v)
+    else:
+        g = torch.as_tensor(gate).to(torch.bool)
+        with torch.no_grad():
+            band = GATE_BAND * (x.abs() @ w1.abs().t() + b1.abs())
+            prone = v.abs() < band
+            on = v > 0
+            bad = (on != g) & ~prone
+            assert not bad.any(), f"{int(bad.sum())} ReLU gates differ outside the fp32 band"
+            mask = torch.where(prone, g, on).to(v.dtype)
+        h = v * mask
+    y = h @ w2.t() + params[f"{prefix}ffn.w_2.bias"]
     if keep is not None:
         y = y * (torch.as_tensor(keep).to(y.dtype) * scale)
     return F.layer_norm(y + x, (x.shape[1],), params[f"{prefix}ffn.layer_norm.weight"],
                         params[f"{prefix}ffn.layer_norm.bias"], 1e-5)
 
 
-def wswgat_layer(kind, rel, Xw, Xs, params, T, prefix="", masks=None):
+def wswgat_layer(kind, rel, Xw, Xs, params, T, prefix="", masks=None, gate=None):
     """WSWGAT.forward(g, w, s) (GAT.py:45-59).  Eval mode, or train mode with
     ``masks`` = (head keep [H, n_src, in], head scale, FFN keep [n_dst, d], FFN
-    scale) -- e.g. oracle/masks.py's restatement of the kernels' masks."""
+    scale) -- e.g. oracle/masks.py's restatement of the kernels' masks.  ``gate``:
+    the FFN's ReLU gates of an fp32 run (``ffn``)."""
     origin, neighbor = (Xs, Xw) if kind == "W2S" else (Xw, Xs)
     hk, hs, fk, fs = masks if masks is not None else (None, 1.0, None, 1.0)
     h = F.elu(gat_heads(rel, neighbor, params, T, prefix, keep=hk, scale=hs)) + origin
-    return ffn(h, params, prefix, keep=fk, scale=fs)
+    return ffn(h, params, prefix, keep=fk, scale=fs, gate=gate)
 
 
 def as_params(module_or_dict, dtype=torch.float64, requires_grad=True):

@@ -87,9 +87,12 @@ def train_masks(drop_seed, off0, n_w, n_s, p=0.1, n_iter=N_ITER):
     return out
 
 
-def oracle_stack(z, seed, masks=None, n_iter=N_ITER):
+def oracle_stack(z, seed, masks=None, n_iter=N_ITER, gates=None):
     """fp64 oracle: s1 = W2S(w0, s0); then n_iter x (w = S2W(w, s); s = W2S(w, s)).
-    ``masks``: train mode, one (head keep, scale, FFN keep, scale) per application."""
+    ``masks``: train mode, one (head keep, scale, FFN keep, scale) per application.
+    ``gates``: {"W2S": [...], "S2W": [...]} the GPU run's FFN ReLU gates per
+    application (fused.ffn: taken only inside the fp32 band around zero, asserted
+    equal elsewhere)."""
     from oracle import fused
     a = concat_arrays(z)
     rws = fused.typed_relation("W2S", a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
@@ -100,10 +103,13 @@ def oracle_stack(z, seed, masks=None, n_iter=N_ITER):
     p1, p2 = fused.as_params(w2s), fused.as_params(s2w)
     m = iter(masks) if masks is not None else None
     nxt = (lambda: next(m)) if m is not None else (lambda: None)
-    w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T, masks=nxt())
+    gw = iter(gates["W2S"]) if gates is not None else None
+    gs = iter(gates["S2W"]) if gates is not None else None
+    gate = (lambda it: next(it) if it is not None else None)
+    w, s = Xw, fused.wswgat_layer("W2S", rws, Xw, Xs, p1, T, masks=nxt(), gate=gate(gw))
     for _ in range(n_iter):
-        w = fused.wswgat_layer("S2W", rsw, w, s, p2, T, masks=nxt())
-        s = fused.wswgat_layer("W2S", rws, w, s, p1, T, masks=nxt())
+        w = fused.wswgat_layer("S2W", rsw, w, s, p2, T, masks=nxt(), gate=gate(gs))
+        s = fused.wswgat_layer("W2S", rws, w, s, p1, T, masks=nxt(), gate=gate(gw))
     R = torch.from_numpy(np.random.default_rng(seed).standard_normal(tuple(s.shape)))
     (s * R).sum().backward()
     return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, p1=p1, p2=p2, R=R)
@@ -135,9 +141,14 @@ def gpu_stack(z, seed, R, train_seed=None, n_iter=N_ITER):
     if train_seed is not None:
         assert rng.get(dev).offset == off0 + 2 * (2 * n_iter + 1)     # one head + one FFN draw per application
     assert type(s.grad_fn).__name__.startswith("_GatStack")        # the timed node, not the layer path
+    # the FFN ReLU gates each application took (the per-layer hidden buffers), for the
+    # oracle's fp32-band gate choice (oracle.fused.ffn)
+    ctx = s.grad_fn
+    gates = {kind: [(h > 0).cpu() for h in ctx.bufs[id(lay)][1]]
+             for kind, lay in (("W2S", ctx.cfg[1]), ("S2W", ctx.cfg[2]))}
     s.backward(R.to(dev, torch.float32))
     torch.cuda.synchronize()
-    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w, off0=off0)
+    return dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, w2s=w2s, s2w=s2w, off0=off0, gates=gates)
 
 
 # (config, GEMM dtype, seed, n_iter): n_iter 2 is the bench's, 1 train.py's default
@@ -188,9 +199,14 @@ def test_stack_vs_oracle_full_size(config, dtype, seed, n_iter):
     docs = synth.make_batch_docs(config, seed=0)
     z = synth_fixture(docs)
     n_edges = int(z["g_n_edges"].sum())
-    o = oracle_stack(z, seed, n_iter=n_iter)
+    R = torch.from_numpy(np.random.default_rng(seed).standard_normal((int(z["n_s"]), 64)))
     with gemm_dtype(dtype):
-        r = gpu_stack(z, seed, o["R"], n_iter=n_iter)
+        r = gpu_stack(z, seed, R, n_iter=n_iter)
+    # f32: the oracle follows the GPU's ReLU gates inside the fp32 band around zero
+    # (a gate flip there moves a W2S weight gradient -- 8 rows, a sum over every
+    # sentence -- by ~1e-3 as a whole); bf16 operands move gates far outside it
+    o = oracle_stack(z, seed, n_iter=n_iter, gates=r["gates"] if dtype == "f32" else None)
+    assert torch.equal(o["R"], R)
     compare(config, dtype, r, o, len(docs), n_edges)
 
 
@@ -215,6 +231,6 @@ def test_train_stack_vs_oracle_full_size(config, dtype, seed, n_iter):
     with gemm_dtype(dtype):
         r = gpu_stack(z, seed, R, train_seed=drop_seed, n_iter=n_iter)
     ms = train_masks(drop_seed, r["off0"], int(z["n_w"]), int(z["n_s"]), n_iter=n_iter)
-    o = oracle_stack(z, seed, masks=ms, n_iter=n_iter)
+    o = oracle_stack(z, seed, masks=ms, n_iter=n_iter, gates=r["gates"] if dtype == "f32" else None)
     assert torch.equal(o["R"], R)
     compare(config, dtype, r, o, len(docs), n_edges)

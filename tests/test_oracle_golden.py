@@ -96,3 +96,41 @@ def test_phantom_edges_are_load_bearing():
         nop = fused.wswgat_layer("W2S", rel0, Xw.double(), Xs.double(), p, T.double())
     close(base, z["out64_w2s"], 1e-6)
     assert (base - nop).abs().max() > 1e-2
+
+
+def test_oracle_ffn_gate_band():
+    """oracle.fused.ffn with an implementation's ReLU gates: the fp64 gates reproduce
+    the plain ReLU path exactly; a gate flipped inside the fp32 band around zero is
+    followed (the backward takes that branch); one flipped outside it is rejected."""
+    import pytest
+    import torch
+    from oracle import fused
+    torch.manual_seed(0)
+    n, d, dh = 40, 16, 32
+    x = torch.randn(n, d, dtype=torch.float64)
+    params = {"ffn.w_1.weight": torch.randn(dh, d, dtype=torch.float64) * 0.3,
+              "ffn.w_1.bias": torch.randn(dh, dtype=torch.float64) * 0.1,
+              "ffn.w_2.weight": torch.randn(d, dh, dtype=torch.float64) * 0.3,
+              "ffn.w_2.bias": torch.randn(d, dtype=torch.float64) * 0.1,
+              "ffn.layer_norm.weight": torch.ones(d, dtype=torch.float64),
+              "ffn.layer_norm.bias": torch.zeros(d, dtype=torch.float64)}
+    # put one pre-activation inside the band: v[3, 5] = 1e-9 * (its magnitude sum)
+    v = x @ params["ffn.w_1.weight"].t() + params["ffn.w_1.bias"]
+    mag = (x.abs() @ params["ffn.w_1.weight"].abs().t() + params["ffn.w_1.bias"].abs())[3, 5]
+    params["ffn.w_1.bias"][5] -= v[3, 5] - 1e-9 * mag
+    v = x @ params["ffn.w_1.weight"].t() + params["ffn.w_1.bias"]
+    gate = v > 0
+    assert torch.equal(fused.ffn(x, params), fused.ffn(x, params, gate=gate))
+    flipped = gate.clone()
+    flipped[3, 5] = ~flipped[3, 5]
+    R = torch.randn(n, d, dtype=torch.float64)         # (a plain sum of LN rows has no gradient)
+    xg = x.clone().requires_grad_()
+    (fused.ffn(xg, params, gate=flipped) * R).sum().backward()
+    xr = x.clone().requires_grad_()
+    (fused.ffn(xr, params) * R).sum().backward()
+    assert not torch.allclose(xg.grad[3], xr.grad[3]) and torch.allclose(xg.grad[4:], xr.grad[4:])
+    far = gate.clone()
+    i, j = [int(t) for t in torch.nonzero(v.abs() > 0.1)[0]]
+    far[i, j] = ~far[i, j]
+    with pytest.raises(AssertionError):
+        fused.ffn(x, params, gate=far)
