@@ -1025,12 +1025,12 @@ struct EpiRows {
                     if (rho) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            // h = log1p(e) for e <= 0 as log(u) * e / (u - 1), u = 1 + e (a few
-                            // ulp without libm's log1pf).  u <= 0: the rounded e reached -1
-                            // (exp(h) below ulp(origin)), G h -> 0 there
+                            // e <= 0: G h = v u log(u), u = 1 + e rounded: d(u log u)/du =
+                            // log u + 1, so the rounding of u moves G h by <= |v| ulp(1) -- no
+                            // log1p needed.  u <= 0: the rounded e reached -1 (exp(h) below
+                            // ulp(origin)), G h -> 0 there
                             const float x = ex[t][e], u = 1.f + x;
-                            const float h = x > 0.f ? x : (u == 1.f ? x : __logf(u) * __fdividef(x, u - 1.f));
-                            const float gh = x > 0.f || u > 0.f ? g[e] * h : 0.f;
+                            const float gh = x > 0.f ? g[e] * x : (u > 0.f ? g[e] * __logf(u) : 0.f);
                             c[0] += slot[e] == 0 ? gh : 0.f;
                             c[1] += slot[e] == 1 ? gh : 0.f;
                             c[2] += slot[e] == 2 ? gh : 0.f;

@@ -783,7 +783,12 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
                                                   const uint32_t *__restrict__ bits, float *__restrict__ part) {
     __shared__ __attribute__((aligned(16))) float Xs[32][kDwXs];
     constexpr int ZC = SL * 16, NZ = 32 * ZC / 256, NM = SL * 64 / 256;   // slot columns, per-thread loads
-    __shared__ __attribute__((aligned(16))) float Zs[32][ZC + 16];
+    // dZ stage: slot q at column ZS q.  VEC: slots 24 apart, so the eight 16-byte
+    // stores of a row (slot halves at 24q + 4h) fall on distinct banks mod 32 (at 16
+    // apart slots q and q + 2 collided: 2-way on every stage store), and rows 112 apart
+    // (16 mod 32: the reads of rows rr and rr + 1 in one 32-lane group stay disjoint)
+    constexpr int ZS = VEC ? 24 : 16, ZW = VEC ? 112 : ZC + 16;
+    __shared__ __attribute__((aligned(16))) float Zs[32][ZW];
     __shared__ uint32_t Ms[SL][64];
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int SPH = (D + 15) / 16, NS = H * SPH;
@@ -858,7 +863,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
                 *reinterpret_cast<f32x4v *>(&Xs[e >> 4][(e & 15) * 4]) = xq[u];
             }
             const int q = tid & 7;
-            *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][(q >> 1) * 16 + (q & 1) * 4]) = zq;
+            *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][(q >> 1) * ZS + (q & 1) * 4]) = zq;
         } else {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -879,7 +884,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
         }
     };
     if constexpr (VEC)                                    // dZ stage columns 8..15 of each slot: zero
-        *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][((tid >> 1) & 3) * 16 + 8 + (tid & 1) * 4]) =
+        *reinterpret_cast<f32x4v *>(&Zs[tid >> 3][((tid >> 1) & 3) * ZS + 8 + (tid & 1) * 4]) =
             f32x4v{0.f, 0.f, 0.f, 0.f};
     f32x4v acc[SL];
 #pragma unroll
@@ -900,7 +905,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
 #pragma unroll
             for (int q = 0; q < SL; ++q) {
                 const float a = ((Ms[q][col] >> rr) & 1u) ? xv : 0.f;
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Zs[rr][q * 16 + li], acc[q], 0, 0, 0);
+                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Zs[rr][q * ZS + li], acc[q], 0, 0, 0);
             }
         }
     }

@@ -158,8 +158,9 @@ def test_psw_elug_rho_partials(M, mode):
     is taken from the rounded e = x - origin, whose error delta is <= 4 ulp(|x| +
     |origin|) + ulp(1); its derivative in e is v (h + 1), so the bound per entry is
     sum |v| delta (|h| + 1) + 1e-5 sum |G| (|h| + 1) over the entry's columns (the
-    second term: log / division / summation roundings).  Rows with h = -20 take the
-    e <= -1 branch (G h = 0) where e + 1 rounds to zero or below."""
+    second term: the log and the summation roundings; the kernel takes u log u with
+    u = 1 + e rounded, whose rounding moves G h by <= |v| ulp(1)).  Rows with h = -20
+    take the e <= -1 branch (G h = 0) where e + 1 rounds to zero or below."""
     from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
     N, K, D = 300, 512, 50
     torch.manual_seed(M + 1)
