@@ -33,7 +33,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
            "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
-           "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho")
+           "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -108,6 +108,7 @@ _SIGS = {
     "hsg_ffn_small_supported": [_I, _I],
     "hsg_ffn_small_bwd_blocks": [_I],
     "hsg_ffn_small_bwd": [_I, _I, _I] + [_P] * 9 + [_F, _P, ctypes.c_uint32] + [_P] * 6,
+    "hsg_ffn_small_bwd_gate": [_I, _I, _I] + [_P] * 9 + [_F, _P, ctypes.c_uint32] + [_P] * 9,
     "hsg_ffn_small_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P, _P,
                           _P],
     "hsg_ln_bwd": [_I, _I, _P, _P, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],

@@ -21,6 +21,7 @@
 // MFMA operand layout (16x16x4): lane (li = l&15, lk = l>>4) feeds k = k0 + 4lk + e
 // to the e-th of 4 consecutive MFMAs, so every operand read is one 16-byte quad.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "../../include/hsg.h"
@@ -360,6 +361,19 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd(int n, const float *__res
 constexpr int kRG = 2;           // 4-row groups per block of the 4x4x1 kernels
 constexpr int kRB4 = 4 * kRG;    // their rows per block (cfg2 W2S: 140 blocks, one round)
 
+// sum over each aligned 8-lane group, in every lane: quad permutes (xor 1, xor 2) and
+// the half-row mirror -- DPP, no LDS round trip
+__device__ __forceinline__ float row8_sum(float x) {
+    const auto dpp = [](float v, auto ctrl) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), decltype(ctrl)::value,
+                                                                  0xf, 0xf, true));
+    };
+    x += dpp(x, std::integral_constant<int, 0xb1>{});     // quad_perm [1,0,3,2]
+    x += dpp(x, std::integral_constant<int, 0x4e>{});     // quad_perm [2,3,0,1]
+    x += dpp(x, std::integral_constant<int, 0x141>{});    // row_half_mirror
+    return x;
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
@@ -499,7 +513,8 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd4(int n, const float *__re
                                                         const int64_t *__restrict__ seedp, uint32_t offset,
                                                         float *__restrict__ dy, float *__restrict__ dH,
                                                         float *__restrict__ dx, float *__restrict__ lnpart,
-                                                        float *__restrict__ hpart) {
+                                                        float *__restrict__ hpart, const float *__restrict__ hg,
+                                                        float *__restrict__ Gout, float *__restrict__ rho) {
     constexpr int NW = 8, LY = D + 4, LH = HID + 4;
     static_assert(D == 64 && HID == 64 * NW && kRB4 == NW, "one instruction spans 64 columns; a wave per row");
     __shared__ __attribute__((aligned(16))) float dys[kRB4 * LY];
@@ -587,11 +602,23 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd4(int n, const float *__re
             for (int i = 0; i < 4; ++i) ps[w][(4 * g + i) * D + lane] = acc[g][i];
     }
     __syncthreads();
-    if (r0 + w < n) {
+    if (r0 + w < n) {                                    // wave-uniform
         float v = ps[0][w * D + lane];
 #pragma unroll
         for (int q = 1; q < NW; ++q) v += ps[q][w * D + lane];
-        dx[(size_t)(r0 + w) * D + lane] = dss[w * D + lane] + v;
+        const size_t o = (size_t)(r0 + w) * D + lane;
+        const float dxv = dss[w * D + lane] + v;
+        dx[o] = dxv;
+        if (Gout) {
+            // the W2S edge layer's backward operands from this dx (= its dOut): G =
+            // dOut * elu'(h) (elu'(h) = 1 for h > 0, else exp(h): as hsg_gat_bwd_dst) and
+            // rho[row][k] = G_k . h_k over head k's 8 columns (lanes 8k .. 8k + 7)
+            const float hv = hg[o];
+            const float g = hv > 0.f ? dxv : dxv * __expf(hv);
+            Gout[o] = g;
+            const float gh = row8_sum(g * hv);
+            if ((lane & 7) == 0) rho[(size_t)(r0 + w) * (D / 8) + lane / 8] = gh;
+        }
     }
 }
 
@@ -637,25 +664,46 @@ int hsg_ffn_small_bwd_blocks(int n) {
     return n > 0 ? (n + rb - 1) / rb : 0;
 }
 
-int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x, const float *H, const float *y,
-                      const float *w1, const float *w2, const float *gamma, const float *mean, const float *rstd,
-                      float p_drop, const int64_t *seed, uint32_t offset, float *dy, float *dH, float *dx,
-                      float *lnpart, float *hpart, void *stream) {
+namespace {
+int ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x, const float *H, const float *y,
+                  const float *w1, const float *w2, const float *gamma, const float *mean, const float *rstd,
+                  float p_drop, const int64_t *seed, uint32_t offset, float *dy, float *dH, float *dx, float *lnpart,
+                  float *hpart, const float *hg, float *G, float *rho, void *stream) {
     if (n < 0 || !hsg_ffn_small_supported(d, d_hid) || p_drop < 0.f || p_drop >= 1.f) return HSG_EINVAL;
     if (!dout || !x || !H || !y || !w1 || !w2 || !gamma || !mean || !rstd || !dy || !dH || !dx || !lnpart || !hpart)
         return HSG_EINVAL;
     if (p_drop > 0.f && (!seed || (long)n * d >= (1L << 32))) return HSG_EINVAL;   // 32-bit mask index
+    if (G && (!hg || !rho || ffn_rows_per_block() != kRB4)) return HSG_EINVAL;
     if (n == 0) return 0;
     if (ffn_rows_per_block() == kRB4)
         hipLaunchKernelGGL((k_ffn_small_bwd4<64, 512>), dim3((unsigned)hsg_ffn_small_bwd_blocks(n)), dim3(512), 0,
                            (hipStream_t)stream, n, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy,
-                           dH, dx, lnpart, hpart);
+                           dH, dx, lnpart, hpart, hg, G, rho);
     else
         hipLaunchKernelGGL((k_ffn_small_bwd<64, 512>), dim3((unsigned)hsg_ffn_small_bwd_blocks(n)), dim3(512), 0,
                            (hipStream_t)stream, n, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy,
                            dH, dx, lnpart, hpart);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+}  // namespace
+
+int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x, const float *H, const float *y,
+                      const float *w1, const float *w2, const float *gamma, const float *mean, const float *rstd,
+                      float p_drop, const int64_t *seed, uint32_t offset, float *dy, float *dH, float *dx,
+                      float *lnpart, float *hpart, void *stream) {
+    return ffn_small_bwd(n, d, d_hid, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy, dH, dx,
+                         lnpart, hpart, nullptr, nullptr, nullptr, stream);
+}
+
+int hsg_ffn_small_bwd_gate(int n, int d, int d_hid, const float *dout, const float *x, const float *H,
+                           const float *y, const float *w1, const float *w2, const float *gamma, const float *mean,
+                           const float *rstd, float p_drop, const int64_t *seed, uint32_t offset, float *dy,
+                           float *dH, float *dx, float *lnpart, float *hpart, const float *h_edge, float *G,
+                           float *rho, void *stream) {
+    if (!h_edge || !G || !rho) return HSG_EINVAL;
+    return ffn_small_bwd(n, d, d_hid, dout, x, H, y, w1, w2, gamma, mean, rstd, p_drop, seed, offset, dy, dH, dx,
+                         lnpart, hpart, h_edge, G, rho, stream);
 }
 
 }  // extern "C"

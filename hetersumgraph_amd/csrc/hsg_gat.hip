@@ -1194,7 +1194,14 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
 // pairs are requested together; accumulation is in edge order (fmaf per edge, as
 // gather_rows), dsigma in edge order.  d a1 block partials are summed over the
 // block's sources in (wave, slot) order: deterministic.
-template <int DV, int TAU_MODE>
+// RHO (round 4, table mode): the whole edge backward in this pass, as
+// k_gat_bwd_src_g does for S2W: rho[v][k] = G_v,k . h_v,k comes from the narrow FFN's
+// backward epilogue (hsg_ffn_small_bwd_gate, beside G), so each edge's
+// dpre = alpha (G_v,k . Z_u,k - rho_v,k) * leaky'(pre) is formed here from the G quads
+// the lane loads anyway and its own Z quads; d tau per box goes to per-lane registers
+// (one add per box under a select) and leaves as per-block partials summed over the
+// block's lanes in (wave, slot) order.  The dst pass is not launched.
+template <int DV, int TAU_MODE, bool RHO = false>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D, int hp, float slope,
                                                         const float *__restrict__ sigma,
                                                         const float *__restrict__ tau,
@@ -1205,12 +1212,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
                                                         const float *__restrict__ a1,
                                                         const float *__restrict__ Z,
                                                         float *__restrict__ dZ, float *__restrict__ dsigma,
-                                                        float *__restrict__ da1_part) {
+                                                        float *__restrict__ da1_part,
+                                                        const float *__restrict__ rho,
+                                                        float *__restrict__ dtau_part) {
     static_assert(DV % 4 == 0, "features move as float4");
+    static_assert(!RHO || TAU_MODE == HSG_TAU_TABLE, "per-box d tau partials: table mode");
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = DV / 4;
     __shared__ float s_tau[HSG_NT * HSG_HMAX];
     __shared__ __attribute__((aligned(16))) float s_da1[HSG_WAVES][64 * DV];
+    __shared__ float s_dt[RHO ? 256 * HSG_NT : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int sl = lane / hp, k = lane - sl * hp;
@@ -1227,6 +1238,9 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
         a1v[q] = a1 ? *reinterpret_cast<const f4 *>(a1 + kc * D + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
         da1[q] = f4{0.f, 0.f, 0.f, 0.f};
     }
+    float dt[RHO ? HSG_NT : 1];                               // RHO: this lane's d tau per box
+#pragma unroll
+    for (int t = 0; t < (RHO ? HSG_NT : 1); ++t) dt[t] = 0.f;
     const WorkRange wr = work_range((R.n_src + wpw - 1) / wpw, HSG_WAVES, wid, R.xcd);   // in wave groups
     for (int q0 = wr.first; q0 < wr.end; q0 += wr.stride) {
         const int u0 = q0 * wpw;
@@ -1238,7 +1252,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
         f4 zr[NQ], acc[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
-            zr[q] = da1_part ? *reinterpret_cast<const f4 *>(Z + (size_t)uc * HD + kc * D + 4 * q) : f4{0.f, 0.f, 0.f, 0.f};
+            zr[q] = (RHO || da1_part) ? *reinterpret_cast<const f4 *>(Z + (size_t)uc * HD + kc * D + 4 * q)
+                                      : f4{0.f, 0.f, 0.f, 0.f};
             acc[q] = f4{0.f, 0.f, 0.f, 0.f};
         }
         float dsig = 0.f;
@@ -1248,7 +1263,14 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
             const int v0 = R.cdst[p], e0 = R.cperm[p], v1 = R.cdst[p1], e1 = R.cperm[p1];
             const int t0 = tau_row<TAU_MODE>(R, e0), t1 = tau_row<TAU_MODE>(R, e1);
             const float M0 = mv[v0 * H + k], L0 = lv[v0 * H + k], M1 = mv[v1 * H + k], L1 = lv[v1 * H + k];
-            const float d0 = dpre[(size_t)e0 * H + k], d1 = dpre[(size_t)e1 * H + k];
+            float d0, d1, r0v = 0.f, r1v = 0.f;
+            if constexpr (RHO) {
+                r0v = rho[v0 * H + k];
+                r1v = rho[v1 * H + k];
+            } else {
+                d0 = dpre[(size_t)e0 * H + k];
+                d1 = dpre[(size_t)e1 * H + k];
+            }
             f4 g0[NQ], g1[NQ];
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
@@ -1260,6 +1282,24 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
             else { tv0 = tau[(size_t)t0 * H + k]; tv1 = tau[(size_t)t1 * H + k]; }
             const float al0 = __expf(leaky(sig + tv0, slope) - M0) / L0;
             const float al1 = __expf(leaky(sig + tv1, slope) - M1) / L1;
+            if constexpr (RHO) {
+                float dot0 = 0.f, dot1 = 0.f;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        dot0 = fmaf(g0[q][j], zr[q][j], dot0);
+                        dot1 = fmaf(g1[q][j], zr[q][j], dot1);
+                    }
+                const float s0 = al0 * (dot0 - r0v), s1 = al1 * (dot1 - r1v);
+                d0 = sig + tv0 > 0.f ? s0 : s0 * slope;
+                d1 = sig + tv1 > 0.f ? s1 : s1 * slope;
+#pragma unroll
+                for (int t = 0; t < HSG_NT; ++t) {
+                    dt[t] += t == t0 ? d0 : 0.f;
+                    if (two) dt[t] += t == t1 ? d1 : 0.f;
+                }
+            }
 #pragma unroll
             for (int q = 0; q < NQ; ++q)
 #pragma unroll
@@ -1299,6 +1339,20 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
             for (int w = 0; w < HSG_WAVES; ++w)
                 for (int ss = 0; ss < wpw; ++ss) a += s_da1[w][(ss * hp + kk) * DV + d];
             da1_part[(size_t)blockIdx.x * HD + f] = a;
+        }
+    }
+    if constexpr (RHO) {                     // d tau block partials, lanes in (wave, slot) order
+#pragma unroll
+        for (int t = 0; t < HSG_NT; ++t) s_dt[threadIdx.x * HSG_NT + t] = dt[t];
+        __syncthreads();
+        const int nt = HSG_NT * H;
+        for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+            const int t = i / H, kk = i - t * H;
+            float a = 0.f;
+#pragma unroll
+            for (int w = 0; w < HSG_WAVES; ++w)
+                for (int ss = 0; ss < wpw; ++ss) a += s_dt[(w * 64 + ss * hp + kk) * HSG_NT + t];
+            dtau_part[(size_t)blockIdx.x * nt + i] = a;
         }
     }
 }
@@ -1802,10 +1856,10 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
         const int hp = next_pow2(H);
         if (tau_mode == HSG_TAU_TABLE)
             HSG_KLAUNCH(false, true, (k_gat_bwd_src_hl<8, HSG_TAU_TABLE>), grid, dim3(256), st, R, H, D, hp, slope,
-                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
+                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part, nullptr, nullptr);
         else
             HSG_KLAUNCH(false, true, (k_gat_bwd_src_hl<8, HSG_TAU_PER_EDGE>), grid, dim3(256), st, R, H, D, hp, slope,
-                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part);
+                        sigma, tau, m, l, G, dpre, a1, Z, dZ, dsigma, da1_part, nullptr, nullptr);
         return launch_status();
     }
     if (wpn == 4 && bwd_occ()) {
@@ -1825,9 +1879,17 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
 #undef HSG_S
 }
 
+// the two shapes of the one-pass edge backward: wide heads over long CSC segments
+// (S2W; rho as 64-column-group partials) and D = 8 heads over short ones (W2S: the
+// head-lane kernel; rho per head)
+bool srcg_wide(const hsg_rel *rel, int H, int D) {
+    return D >= 32 && D <= 64 && src_wpn(rel) == 4 && (D + lanes_per_head(H) - 1) / lanes_per_head(H) <= 8;
+}
+bool srcg_narrow(const hsg_rel *rel, int H, int D) { return D == 8 && H <= 8 && src_wpn(rel) == 1; }
+
 int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D) {
-    if (!rel || !shape_ok(H, D) || D < 32 || D > 64 || src_wpn(rel) != 4) return 0;
-    return (D + lanes_per_head(H) - 1) / lanes_per_head(H) <= 8;
+    if (!rel || !shape_ok(H, D)) return 0;
+    return srcg_wide(rel, H, D) || srcg_narrow(rel, H, D);
 }
 
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
@@ -1835,10 +1897,22 @@ int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float
                       const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                       float *dtau_part, void *stream) {
     if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !G || !rho || !Z || !dZ || !dtau_part) return HSG_EINVAL;
-    if (rho_groups != (H * D + 63) / 64) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
     const dim3 grid(hsg_gat_bwd_src_blocks(rel));
     hipStream_t st = (hipStream_t)stream;
+    if (rho_groups == 0) {                   // per-head rho: the narrow head-lane kernel
+        if (!srcg_narrow(rel, H, D) || ((uintptr_t)G | (uintptr_t)dZ | (uintptr_t)Z | (uintptr_t)a1) & 15)
+            return HSG_EINVAL;
+        if (rel->n_src == 0) {
+            if (da1_part && hipMemsetAsync(da1_part, 0, sizeof(float) * H * D * grid.x, st) != hipSuccess)
+                return HSG_EINVAL;
+            return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
+        }
+        HSG_KLAUNCH(true, true, (k_gat_bwd_src_hl<8, HSG_TAU_TABLE, true>), grid, dim3(256), st, R, H, D,
+                    next_pow2(H), slope, sigma, tau, m, l, G, nullptr, a1, Z, dZ, dsigma, da1_part, rho, dtau_part);
+        return launch_status();
+    }
+    if (!srcg_wide(rel, H, D) || rho_groups != (H * D + 63) / 64) return HSG_EINVAL;
     const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;
 #define HSG_SG(NE_, OCC_, EQ_)                                                                               \
     HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope, sigma,   \

@@ -25,7 +25,7 @@ import os
 import torch
 
 from . import rng as hsg_rng
-from ._lib import check, load, ptr, stream_of
+from ._lib import HSG_EINVAL, check, load, ptr, stream_of
 from .dense import (gemm, gemm_psw, gemm_psw_elug, gemm_psw_ln, get_gemm_dtype, psw_row_tiles, row_tiles,
                     split_weights)
 
@@ -115,7 +115,7 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
 
 
-def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
+def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, gate=None):
     """Backward of :func:`ffn_fwd`.  ``dst`` = (dw1, acc_w1, dw2, acc_w2, db1, db2,
     dgamma, dbeta, acc_b): gradient buffers shaped [d_hid, d], [d, d_hid], [d_hid],
     [d], [d], [d] (None when not needed), each written or -- with its accumulate
@@ -129,8 +129,10 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
     and its ELU gate G = dx * elu'(h) goes into G from the last GEMM's epilogue
     (hsg_gemm_f32_psw_elug) -- only on the pre-split-weight path; (origin, G, rho,
     head_dim): also the rho partials of the one-pass edge backward
-    (hsg_gemm_psw_elug_rho).  Returns dx (a fresh tensor), or (dx, G produced?) with
-    ``elug``."""
+    (hsg_gemm_psw_elug_rho).  ``gate`` = (h_edge, G, rho): the same for the narrow
+    one-launch FFN (W2S: the edge layer stored h; G and per-head rho from its epilogue,
+    hsg_ffn_small_bwd_gate).  Returns dx (a fresh tensor), or (dx, G produced?) with
+    ``elug`` or ``gate``."""
     lib = load()
     x, w1, w2, gamma, H, y, mean, rstd, p_drop, seed_t, off, wsplit = saved
     dw1, acc_w1, dw2, acc_w2, db1, db2, dg, dbt, acc = dst
@@ -147,9 +149,15 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
         part = x.new_empty(nb, 3, d)
         hpart = x.new_empty(rt, d_hid)
         dH = act_grads[1] if act_grads is not None else x.new_empty(n, d_hid)
-        check(lib.hsg_ffn_small_bwd(n, d, d_hid, ptr(dout), ptr(x), ptr(H), ptr(y), ptr(w1), ptr(w2), ptr(gamma),
-                                    ptr(mean), ptr(rstd), p_drop, ptr(seed_t), off, ptr(dy), ptr(dH), ptr(dx),
-                                    ptr(part), ptr(hpart), st), "hsg_ffn_small_bwd")
+        args = (n, d, d_hid, ptr(dout), ptr(x), ptr(H), ptr(y), ptr(w1), ptr(w2), ptr(gamma), ptr(mean), ptr(rstd),
+                p_drop, ptr(seed_t), off, ptr(dy), ptr(dH), ptr(dx), ptr(part), ptr(hpart))
+        rc = HSG_EINVAL
+        if gate is not None:
+            rc = lib.hsg_ffn_small_bwd_gate(*args, ptr(gate[0]), ptr(gate[1]), ptr(gate[2]), st)
+            g_done = rc == 0
+        if rc == HSG_EINVAL:                # no gate asked, or declined: the plain launch
+            rc = lib.hsg_ffn_small_bwd(*args, st)
+        check(rc, "hsg_ffn_small_bwd")
     else:
         nb = lib.hsg_ln_bwd_blocks(n)
         part = x.new_empty(nb, 3, d)
@@ -179,13 +187,13 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None):
         for o, name, off in ((dg, "g", 0), (dbt, "bt", d), (db2, "b2", 2 * d)):
             if o is not None:
                 batch.add((key, name), o, d, 3 * d, off, 1.0, acc, part, nb)
-        return (dx, g_done) if elug is not None else dx
+        return (dx, g_done) if elug is not None or gate is not None else dx
     if any(o is not None for o in outs):
         db1, dg, dbt, db2 = [o if o is not None else x.new_empty(n_)
                              for o, n_ in zip(outs, (d_hid, d, d, d))]   # scratch for unneeded ones
         check(lib.hsg_ffn_colsums(rt, d_hid, ptr(hpart), ptr(db1), nb, d, ptr(part), ptr(dg), ptr(dbt), ptr(db2),
                                   int(bool(acc)), st), "hsg_ffn_colsums")
-    return (dx, g_done) if elug is not None else dx
+    return (dx, g_done) if elug is not None or gate is not None else dx
 
 
 class _FFN(torch.autograd.Function):

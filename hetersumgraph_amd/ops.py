@@ -198,8 +198,10 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
     The origin gradient is ``dout`` itself.  ``G``: the rows dOut * elu'(h), already
     made by the FFN's last GEMM (a forward without h): the dst pass reads them
     (hsg_gat_bwd_dst_g).  ``rho`` (with G): that GEMM's per-64-column partials of
-    G_v . h_v (hsg_gemm_psw_elug_rho) -- the whole backward is then ONE source-centric
-    launch (hsg_gat_bwd_src_g) instead of the dst + src pair."""
+    G_v . h_v (hsg_gemm_psw_elug_rho, [n_dst, groups, 3]) or, for narrow heads, the
+    per-head G_v . h_v of the narrow FFN's epilogue (hsg_ffn_small_bwd_gate, [n_dst, H])
+    -- the whole backward is then ONE source-centric launch (hsg_gat_bwd_src_g) instead
+    of the dst + src pair."""
     lib = load()
     Z, attn, T, wf, bf, a1, sigma, tau, h, m, l, rel, H, D, slope, has_origin, xo = saved
     dout = dout.contiguous()
@@ -218,11 +220,13 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
     da1p = Z.new_empty(nbs, H * D)
     tok = _clock_start(("gat_bwd", rel.kind), Z)
     try:
-        if g_given and xo is None:
+        if g_given and not merged and xo is None:
             raise ValueError("gat_table_bwd: G rows given for a forward that stored h")
         if merged:                          # one source-centric pass (G and rho from the FFN epilogue)
+            # rho [n_dst, groups, 3]: 64-column-group partials (wide heads); [n_dst, H]: per head
+            groups = rho.shape[1] if rho.dim() == 3 else 0
             check(lib.hsg_gat_bwd_src_g(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G), ptr(rho),
-                                        rho.shape[1], ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp), st),
+                                        groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp), st),
                   "hsg_gat_bwd_src_g")
         else:
             dpre = Z.new_empty(rel.n_typed, H)

@@ -199,6 +199,12 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
         # ... and the rho partials, so the edge backward is one source-centric pass
         n_dst, HD = elug[1].shape
         elug += (elug[1].new_empty(n_dst, (HD + 63) // 64, 3), gsaved[13])
+    # narrow heads (W2S) with h stored: the narrow FFN's backward epilogue makes G and the
+    # per-head rho, and the edge backward is one head-lane pass over the words
+    gate = None
+    if elug is None and gsaved[8] is not None and gsaved[13] == 8 and _merged_bwd(gsaved):
+        h = gsaved[8]
+        gate = (h, torch.empty_like(h), h.new_empty(h.shape[0], gsaved[12]))
     if act_grads is None:
         dw1, a_w1 = grads.dst(lay.w1)
         dw2, a_w2 = grads.dst(lay.w2)
@@ -207,11 +213,14 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     (db1, db2, dg, dbt), a_b = grads.group([lay.b1, lay.b2, lay.gamma, lay.beta])
     dx = ffn_bwd(fsaved, dout, (dw1.view(d_hid, d) if dw1 is not None else None, a_w1,
                                 dw2.view(d, d_hid) if dw2 is not None else None, a_w2, db1, db2, dg, dbt, a_b),
-                 act_grads=act_grads, batch=batch, key=id(lay), elug=elug)
+                 act_grads=act_grads, batch=batch, key=id(lay), elug=elug, gate=gate)
     if elug is not None:
         dx, g_done = dx
         G = elug[1] if g_done else None
         rho = elug[2] if g_done and len(elug) > 2 else None
+    elif gate is not None:
+        dx, g_done = dx
+        G, rho = (gate[1], gate[2]) if g_done else (None, None)
     need_dz = nb_grad is not None or lay.W.requires_grad
     if stage is not None:
         dZ = gat_table_bwd(gsaved, dx, dZ=need_dz, stage=stage, G=G, rho=rho)

@@ -121,6 +121,9 @@ int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
  * with b < hsg_gat_bwd_src_blocks(rel) for both slabs.  Replaces hsg_gat_bwd_dst_g +
  * hsg_gat_bwd_src (GATLayer.py:118-131 backward); results equal up to fp32 rounding
  * (rho is summed from G.h instead of sum_e alpha_e G.Z_u). */
+/* rho_groups == 0: the narrow-head shape (D = 8, H <= 8, short CSC segments: the W2S
+ * words) with rho[v][k] = G_v,k . h_v,k per head, as hsg_ffn_small_bwd_gate writes it
+ * (the head-lane kernel; G, Z, dZ, a1 16-byte aligned). */
 int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D);
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
                       const float *m, const float *l, const float *G, const float *rho, int rho_groups,
@@ -372,6 +375,16 @@ int hsg_ffn_small_bwd(int n, int d, int d_hid, const float *dout, const float *x
                       const float *mean, const float *rstd, float p_drop, const int64_t *seed,
                       uint32_t offset, float *dy, float *dH, float *dx, float *lnpart, float *hpart,
                       void *stream);
+/* hsg_ffn_small_bwd that also hands the W2S edge layer its backward operands from dx
+ * (= the edge layer's dOut; GAT.py:56-57, GATLayer.py:118-131): G = dx * elu'(h)
+ * (1 for h > 0, else exp(h)) and rho[row][k] = sum over head k's 8 columns of G * h,
+ * h_edge the edge layer's saved h [n][d] (d = 64 = 8 heads x 8), for
+ * hsg_gat_bwd_src_g with rho_groups = 0.  HSG_EINVAL when a pointer is NULL. */
+int hsg_ffn_small_bwd_gate(int n, int d, int d_hid, const float *dout, const float *x, const float *H,
+                           const float *y, const float *w1, const float *w2, const float *gamma, const float *mean,
+                           const float *rstd, float p_drop, const int64_t *seed, uint32_t offset, float *dy,
+                           float *dH, float *dx, float *lnpart, float *hpart, const float *h_edge, float *G,
+                           float *rho, void *stream);
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta,
                float eps, float p_drop, const int64_t *seed, uint32_t offset,
                float *out, float *mean, float *rstd, void *stream);

@@ -249,3 +249,90 @@ def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k):
         err = (a - b).abs().max().item()
         print(f"{name}: max |one-pass - two-pass| {err:.3e} (tol {tol:.3e})")
         assert err <= tol, name
+
+
+@pytest.mark.parametrize("n", [1120, 37])
+def test_narrow_ffn_gate_epilogue(n):
+    """hsg_ffn_small_bwd_gate: the same dx (bitwise) as hsg_ffn_small_bwd, and G =
+    dx * elu'(h) (exp(h) for h <= 0, as the W2S dst pass) and the per-head rho =
+    sum over each head's 8 columns of G * h (fp64 of the kernel's own G, 1e-6 of
+    sum |G h|)."""
+    from hetersumgraph_amd import rng
+    from hetersumgraph_amd.ffn import ffn_bwd, ffn_fwd
+    torch.manual_seed(n)
+    dev = "cuda"
+    x = torch.randn(n, 64, device=dev)
+    w1 = torch.randn(512, 64, device=dev) / 8
+    b1 = torch.randn(512, device=dev) * 0.1
+    w2 = torch.randn(64, 512, device=dev) / 22
+    b2 = torch.randn(64, device=dev) * 0.1
+    g = 1 + 0.1 * torch.randn(64, device=dev)
+    bt = 0.1 * torch.randn(64, device=dev)
+    dout = torch.randn(n, 64, device=dev)
+    h = 2 * torch.randn(n, 64, device=dev)
+    h[::5] = 0.0
+    rng.manual_seed(5)
+    out, saved = ffn_fwd(x, w1, b1, w2, b2, g, bt, 0.1)
+    res = []
+    for with_gate in (False, True):
+        grads = [torch.empty_like(t) for t in (w1, w2, b1, b2, g, bt)]
+        gate = (h, torch.empty_like(h), h.new_empty(n, 8)) if with_gate else None
+        r = ffn_bwd(saved, dout, (grads[0], False, grads[1], False, grads[2], grads[3], grads[4], grads[5], False),
+                    gate=gate)
+        res.append((r, gate))
+    torch.cuda.synchronize()
+    dx0 = res[0][0]
+    (dx1, done), (_, G, rho) = res[1]
+    assert done and torch.equal(dx0, dx1)
+    gref = torch.where(h > 0, dx1, dx1 * torch.exp(h))
+    assert (G - gref).abs().max().item() <= 1e-6 * max(1.0, gref.abs().max().item())
+    prod = (G.double() * h.double()).view(n, 8, 8)
+    err = (rho.double() - prod.sum(2)).abs()
+    assert (err <= 1e-6 * prod.abs().sum(2) + 1e-12).all()
+
+
+@pytest.mark.parametrize("n_docs,N,W,k", [(4, 35, 600, 36), (2, 9, 40, 5)])
+def test_one_pass_w2s_edge_bwd_equals_two_pass(n_docs, N, W, k):
+    """W2S (D = 8 narrow heads, h stored): hsg_gat_bwd_src_g with per-head rho
+    (the head-lane kernel forming dpre itself) against the dst + src pair on the
+    same G rows -- dZ and every attention-parameter gradient within 1e-5 of scale."""
+    import ctypes
+    from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd._lib import load
+    from hetersumgraph_amd.ops import LEAKY_SLOPE, gat_table_bwd, gat_table_fwd
+    lib = load()
+    rng_ = np.random.default_rng(n_docs + 10)
+    docs = [synth.make_hsg_doc(rng_, N=N, W=W, k=k) for _ in range(n_docs)]
+    Gr = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
+    Gr.to(torch.device("cuda"))
+    rel = Gr.relation("W2S")
+    H, D = 8, 8
+    assert lib.hsg_gat_bwd_src_g_supported(ctypes.byref(rel.cstruct()), H, D)
+    torch.manual_seed(k)
+    Z = torch.randn(rel.n_src, H * D, device="cuda")
+    attn = torch.randn(H, 3 * D, device="cuda") * 0.3
+    T = torch.randn(10, 50, device="cuda")
+    wf = torch.randn(H, D, 50, device="cuda") * 0.1
+    bf = None
+    org = torch.randn(rel.n_dst, H * D, device="cuda")
+    out, saved = gat_table_fwd(Z, attn, T, wf, bf, org, rel, H, D, LEAKY_SLOPE)
+    h = saved[8]
+    assert h is not None
+    dout = torch.randn_like(out)
+    G = torch.where(h > 0, dout, dout * torch.exp(h)).contiguous()
+    rho = (G.double() * h.double()).view(-1, H, D).sum(2).float().contiguous()
+    res = []
+    for merged in (False, True):
+        dst = (torch.zeros_like(attn), torch.zeros_like(wf), None, torch.zeros_like(T), False, False)
+        if merged:
+            dZ = gat_table_bwd(saved, dout, dst=dst, G=G, rho=rho)
+        else:
+            dZ = gat_table_bwd(saved, dout, dst=dst)
+        res.append((dZ, dst[0], dst[1], dst[3]))
+    torch.cuda.synchronize()
+    for name, a, b in zip(("dZ", "dattn", "dwf", "dT"), res[1], res[0]):
+        tol = 1e-5 * max(1.0, b.abs().max().item())
+        err = (a - b).abs().max().item()
+        print(f"{name}: max |one-pass - two-pass| {err:.3e} (tol {tol:.3e})")
+        assert err <= tol, name
