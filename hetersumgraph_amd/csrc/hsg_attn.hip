@@ -299,6 +299,43 @@ __global__ __launch_bounds__(256) void k_attn_params_bwd_pair(AttnBwdPair j, int
             dtau[q][c] = attn_bwd_dtau_col(q ? n1 : n0, j.ws[q], srows, c);
         }
         __syncthreads();
+        if ((j.H[0] + j.H[1]) * F <= kWfLds) {
+            // both layers' v_k in ONE pass, then each dT element takes layer 0's update
+            // and then layer 1's in one thread (the same values as the two passes in
+            // that order, also when both layers write the same dT): half the dependent
+            // load phases of this block, the launch's critical path
+            const int n0v = j.H[0] * F, nv = n0v + j.H[1] * F;
+            for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+                const int q = i >= n0v ? 1 : 0, ii = i - (q ? n0v : 0);
+                const int kk = ii / F, f = ii - kk * F, D = j.D[q];
+                const float *wk = j.wf[q] + (size_t)kk * D * F;
+                const float *a3 = j.attn[q] + kk * 3 * D + 2 * D;
+                float sv = 0.f;
+                for (int d0 = 0; d0 < D; d0 += 32) {          // as attn_bwd_dT: 32 at a time, d order
+                    float w[32], a[32];
+#pragma unroll
+                    for (int u = 0; u < 32; ++u) {
+                        const int d = min(d0 + u, D - 1);
+                        w[u] = wk[d * F + f];
+                        a[u] = a3[d];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 32; ++u)
+                        if (d0 + u < D) sv = fmaf(a[u], w[u], sv);
+                }
+                wlds[i] = sv;
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i < (kNT - 1) * F; i += blockDim.x) {
+                const int t = i / F, f = i - t * F;
+                float s0 = 0.f, s1 = 0.f;
+                for (int kk = 0; kk < j.H[0]; ++kk) s0 = fmaf(dtau[0][t * j.H[0] + kk], wlds[kk * F + f], s0);
+                for (int kk = 0; kk < j.H[1]; ++kk) s1 = fmaf(dtau[1][t * j.H[1] + kk], wlds[n0v + kk * F + f], s1);
+                j.dT[0][i] = (j.acc[0] & 2) ? j.dT[0][i] + s0 : s0;
+                j.dT[1][i] = (j.acc[1] & 2) ? j.dT[1][i] + s1 : s1;
+            }
+            return;
+        }
         for (int q = 0; q < 2; ++q)
             attn_bwd_dT(j.H[q], j.D[q], F, dtau[q], j.attn[q], j.wf[q], wlds, j.dT[q], (j.acc[q] & 2) != 0);
         return;
