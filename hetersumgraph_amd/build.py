@@ -24,7 +24,7 @@ DEV_OUT = os.path.join(HERE, "libhsg_dev.so")
 DEV_OBJDIR = os.path.join(ROOT, "build", "obj_dev")
 ARCH = os.environ.get("HSG_OFFLOAD_ARCH", "gfx950")
 HEADERS = [os.path.join(ROOT, "include", "hsg.h")] + [os.path.join(HERE, "csrc", h) for h in
-                                                      ("hsg_rng.h", "hsg_wsplit.h", "hsg_dev.h")]
+                                                      ("hsg_rng.h", "hsg_wsplit.h", "hsg_dev.h", "hsg_wave.h")]
 # host-only graph builder (no HIP runtime: usable in DataLoader workers)
 HOST_SOURCES = [os.path.join(HERE, "csrc", "hsg_graphbuild.cpp")]
 HOST_HEADERS = [os.path.join(ROOT, "include", "hsg_graph.h")]

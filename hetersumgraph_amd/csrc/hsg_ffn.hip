@@ -27,6 +27,7 @@
 #include "../../include/hsg.h"
 #include "hsg_rng.h"
 #include "hsg_dev.h"
+#include "hsg_wave.h"
 #include <stdlib.h>
 
 namespace {
@@ -361,18 +362,8 @@ __global__ __launch_bounds__(512) void k_ffn_small_bwd(int n, const float *__res
 constexpr int kRG = 2;           // 4-row groups per block of the 4x4x1 kernels
 constexpr int kRB4 = 4 * kRG;    // their rows per block (cfg2 W2S: 140 blocks, one round)
 
-// sum over each aligned 8-lane group, in every lane: quad permutes (xor 1, xor 2) and
-// the half-row mirror -- DPP, no LDS round trip
-__device__ __forceinline__ float row8_sum(float x) {
-    const auto dpp = [](float v, auto ctrl) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), decltype(ctrl)::value,
-                                                                  0xf, 0xf, true));
-    };
-    x += dpp(x, std::integral_constant<int, 0xb1>{});     // quad_perm [1,0,3,2]
-    x += dpp(x, std::integral_constant<int, 0x4e>{});     // quad_perm [2,3,0,1]
-    x += dpp(x, std::integral_constant<int, 0x141>{});    // row_half_mirror
-    return x;
-}
+// sum over each aligned 8-lane group, in every lane (DPP, hsg_wave.h)
+__device__ __forceinline__ float row8_sum(float x) { return hsg_group_sum<8>(x); }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);

@@ -46,6 +46,7 @@
 
 #include "../../include/hsg.h"
 #include "hsg_dev.h"
+#include "hsg_wave.h"
 #include "hsg_rng.h"
 #include "hsg_wsplit.h"
 
@@ -931,20 +932,9 @@ __device__ __forceinline__ void epi_store(const f32x16 (&acc)[TN], int row0, int
 // -4..-9 us per launch).  Lane -> (row step, quad): QPR quads per row, RPS = 64 / QPR
 // rows per step; lanes past RPS * QPR idle.  Each lane keeps one quad, so its column
 // sums are per-lane partials over its rows.
-// sum over each aligned 16-lane row of the wave, in every lane: four DPP adds (xor 1,
-// xor 2 by quad permutes, then half-row and row mirrors) -- VALU only, where
+// sum over each aligned 16-lane row of the wave, in every lane (DPP, hsg_wave.h):
 // __shfl_xor lowers to a chain of ds_bpermute round trips through the LDS path
-__device__ __forceinline__ float row16_sum(float x) {
-    const auto dpp = [](float v, auto ctrl) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), decltype(ctrl)::value,
-                                                                  0xf, 0xf, true));
-    };
-    x += dpp(x, std::integral_constant<int, 0xb1>{});     // quad_perm [1,0,3,2]
-    x += dpp(x, std::integral_constant<int, 0x4e>{});     // quad_perm [2,3,0,1]
-    x += dpp(x, std::integral_constant<int, 0x141>{});    // row_half_mirror
-    x += dpp(x, std::integral_constant<int, 0x140>{});    // row_mirror
-    return x;
-}
+__device__ __forceinline__ float row16_sum(float x) { return hsg_group_sum<16>(x); }
 
 template <int BN>
 struct EpiRows {
