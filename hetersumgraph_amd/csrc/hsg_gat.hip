@@ -155,7 +155,11 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
 // ---------------------------------------------------------------- forward ----
 // PF (one destination per wave only): the next destination's indptr / phantom are
 // requested one iteration ahead (vector loads, consumed by readfirstlane), and the
-// residual row is requested before the score phase.
+// residual row is requested before the score phase.  PF = 2 (round 4, the default): also
+// the next destination's first lph edges -- (source, box) requested after this
+// destination's score phase, their (sigma, tau) after its gather, before its stores
+// (vmcnt retires in issue order: the next score phase then waits for neither the
+// stores nor the next residual row) -- so its score phase starts with the scores.
 template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0>
 __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
@@ -192,9 +196,32 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     const WorkRange wr = work_range(R.n_dst, NPB, wid / WPN, R.xcd);
     const int vstride = wr.stride;
     int pf_beg = 0, pf_end = 0, pf_c = 0;
+    int pu = 0, pt = 0;                                   // PF = 2: next destination, edge l
+    float psg = 0.f, ptu = 0.f;
+    bool pok = false;
     if constexpr (PF) {
         const int v0 = wr.first;
         if (v0 < wr.end) { pf_beg = R.indptr[v0]; pf_end = R.indptr[v0 + 1]; pf_c = R.phantom[v0]; }
+    }
+    // PF = 2: the scores of edge l of the next destination (pok: it exists)
+    auto pf_edges = [&](int nb, int ne) {
+        pok = kact && nb + l < ne;
+        if (pok) {
+            pu = R.src[nb + l];
+            pt = tau_row<TAU_MODE>(R, nb + l);
+        }
+    };
+    auto pf_scores = [&]() {
+        if (pok) {
+            psg = sigma[pu * H + k];
+            ptu = tau[pt * H + k];
+        }
+    };
+    if constexpr (PF == 2) {
+        if (wr.first < wr.end) {
+            pf_edges(__builtin_amdgcn_readfirstlane(pf_beg), __builtin_amdgcn_readfirstlane(pf_end));
+            pf_scores();
+        }
     }
     for (int v_ = wr.first; v_ < wr.end; v_ += vstride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
@@ -225,8 +252,15 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         if (kact) {
             for (int j = l; j < n1; j += lph) {
                 const int e = eb + j;
-                const int u = R.src[e];
-                const float s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                int u;
+                float s;
+                if (PF == 2 && j == l && pok) {            // prefetched last iteration
+                    u = pu;
+                    s = leaky(psg + ptu, slope);
+                } else {
+                    u = R.src[e];
+                    s = leaky(sigma[u * H + k] + tau[tau_row<TAU_MODE>(R, e) * H + k], slope);
+                }
                 if (single) {
                     sa[j * H + k] = s;
                     if (k == 0) sn[j] = u;
@@ -250,6 +284,12 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             }
         }
         if (c > 0) lse_merge(mx, sm, 0.f, (float)c);     // phantom in-edges: e = 0
+        if constexpr (PF == 2) {                          // the next destination's (src, box)
+            if (v_ + vstride < wr.end)
+                pf_edges(__builtin_amdgcn_readfirstlane(pf_beg), __builtin_amdgcn_readfirstlane(pf_end));
+            else
+                pok = false;
+        }
         const bool any = end > beg;
         const float inv = any ? 1.f / sm : 0.f;
         // the residual row: independent of the gathers below
@@ -296,6 +336,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 }
             }
         }
+        if constexpr (PF == 2) pf_scores();              // ... and its (sigma, tau), before the stores
         // epilogue: h, and elu(h) + origin (GAT.py:56-57)
         if (writer) {
 #pragma unroll
@@ -1560,9 +1601,12 @@ bool bwd_occ() {
 // next-destination prefetch in the one-destination-per-wave forward: cfg2 S2W
 // forward 17.8 -> 17.2 us in-step, step 1.3084 -> 1.3049 ms in one A/B (round 3);
 // HSG_GAT_FWD_PF=0 drops it
+// round 4: two-level prefetch by default (S2W forward 16.53 / 16.59 -> 16.09 / 16.14 us
+// per launch in two alternations of rocprofv3 step traces, profiles/r04_dev/pf{1,2}_step_*.txt);
+// HSG_GAT_FWD_PF=1 / 0 (dev) restore one level / none
 int fwd_pf() {
     const char *e = HSG_DEV_ENV("HSG_GAT_FWD_PF");
-    return e && atoi(e) == 0 ? 0 : 1;
+    return e ? (atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : 2) : 2;
 }
 
 // occupancy hint of the one-destination-per-wave forward: 7 waves per SIMD (73 -> 64
@@ -1689,9 +1733,16 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
         const int pf = fwd_pf();
-        if (pf == 1 || occ != 8) {
+        if (pf != 0 || occ != 8) {
 #ifdef HSG_DEV
-            if (pf != 1) {
+            if (pf == 1) {                                 // one-level prefetch (dev A/B)
+                if (tau_mode == HSG_TAU_TABLE)
+                    return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                origin, h, out, m, l);
+                return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                               origin, h, out, m, l);
+            }
+            if (pf == 0) {
                 if (tau_mode == HSG_TAU_TABLE)
                     return fwd_dispatch<HSG_TAU_TABLE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                              origin, h, out, m, l);
@@ -1700,9 +1751,9 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
             }
 #endif
             if (tau_mode == HSG_TAU_TABLE)
-                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 2>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                             origin, h, out, m, l);
-            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
+            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 2>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                            origin, h, out, m, l);
         }
 #ifdef HSG_DEV
