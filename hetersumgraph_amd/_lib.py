@@ -33,7 +33,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
            "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
-           "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate")
+           "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate",
+           "hsg_gat_bwd_src_g_blocks")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -129,6 +130,7 @@ _SIGS = {
     "hsg_gemm_bf16_psw": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _P],
     "hsg_gat_bwd_dst_g": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gat_bwd_src_g_supported": [_RELP, _I, _I],
+    "hsg_gat_bwd_src_g_blocks": [_RELP, _I, _I],
     "hsg_gat_bwd_src_g": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_psw_elug_rho": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P],
 }

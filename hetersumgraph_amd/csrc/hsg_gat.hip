@@ -1943,13 +1943,27 @@ int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D) {
     return srcg_wide(rel, H, D) || srcg_narrow(rel, H, D);
 }
 
+int hsg_gat_bwd_src_g_blocks(const hsg_rel *rel, int H, int D) {
+    if (!hsg_gat_bwd_src_g_supported(rel, H, D)) return 0;
+    const char *e = HSG_DEV_ENV("HSG_SRCG_GRID");                         // dev A/B: 0 = the src grid
+    if (srcg_narrow(rel, H, D) && !(e && atoi(e) == 0)) {
+        // the head-lane kernel takes 64 / nextpow2(H) sources per wave: one block per 4
+        // such wave groups (cfg2 W2S: 600 blocks of busy waves instead of 2,048 blocks of
+        // which 70 % of the waves had no source -- and 600 partial rows to reduce)
+        const int groups = (rel->n_src + 64 / next_pow2(H) - 1) / (64 / next_pow2(H));
+        const int b = (groups + HSG_WAVES - 1) / HSG_WAVES;
+        return b < 1 ? 1 : (b < kBwdSrcGridCap ? b : kBwdSrcGridCap);
+    }
+    return hsg_gat_bwd_src_blocks(rel);
+}
+
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
                       const float *m, const float *l, const float *G, const float *rho, int rho_groups,
                       const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                       float *dtau_part, void *stream) {
     if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !G || !rho || !Z || !dZ || !dtau_part) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
-    const dim3 grid(hsg_gat_bwd_src_blocks(rel));
+    const dim3 grid(hsg_gat_bwd_src_g_blocks(rel, H, D));
     hipStream_t st = (hipStream_t)stream;
     if (rho_groups == 0) {                   // per-head rho: the narrow head-lane kernel
         if (!srcg_narrow(rel, H, D) || ((uintptr_t)G | (uintptr_t)dZ | (uintptr_t)Z | (uintptr_t)a1) & 15)

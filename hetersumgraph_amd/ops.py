@@ -213,7 +213,7 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
     merged = rho is not None
     if merged and not g_given:
         raise ValueError("gat_table_bwd: rho partials without their G rows")
-    nbs = lib.hsg_gat_bwd_src_blocks(relp)
+    nbs = lib.hsg_gat_bwd_src_g_blocks(relp, H, D) if merged else lib.hsg_gat_bwd_src_blocks(relp)
     nbd = nbs if merged else lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
     dZt = torch.empty_like(Z)

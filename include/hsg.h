@@ -118,13 +118,15 @@ int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
  * G_v . h_v that hsg_gemm_psw_elug_rho writes (rho_groups = ceil(H*D / 64)):
  *   dpre[e,k]   = alpha_ek (G[v,k,:] . Z[u,k,:] - rho_vk) * leaky'(pre_ek)
  *   dZ, dsigma, da1_part as hsg_gat_bwd_src, dtau_part[b][box][k] per-block partials
- * with b < hsg_gat_bwd_src_blocks(rel) for both slabs.  Replaces hsg_gat_bwd_dst_g +
+ * with b < hsg_gat_bwd_src_g_blocks(rel, H, D) for both slabs.  Replaces hsg_gat_bwd_dst_g +
  * hsg_gat_bwd_src (GATLayer.py:118-131 backward); results equal up to fp32 rounding
  * (rho is summed from G.h instead of sum_e alpha_e G.Z_u). */
 /* rho_groups == 0: the narrow-head shape (D = 8, H <= 8, short CSC segments: the W2S
  * words) with rho[v][k] = G_v,k . h_v,k per head, as hsg_ffn_small_bwd_gate writes it
  * (the head-lane kernel; G, Z, dZ, a1 16-byte aligned). */
 int hsg_gat_bwd_src_g_supported(const hsg_rel *rel, int H, int D);
+/* Number of partial rows hsg_gat_bwd_src_g writes into da1_part and dtau_part. */
+int hsg_gat_bwd_src_g_blocks(const hsg_rel *rel, int H, int D);
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
                       const float *m, const float *l, const float *G, const float *rho, int rho_groups,
                       const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
