@@ -134,6 +134,92 @@ __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__re
     }
 }
 
+// Round 4 (257..512 columns, the S2W FFN at d = 300): k_ln_fwd4 on a persistent grid
+// of kLnFwdPBlocks blocks, each wave walking row groups g, g + waves, ... with the next
+// group's y / x loads issued before this group's reductions and stores, so the HBM read
+// of one group overlaps the write of the previous one (k_ln_fwd4: one round of waves,
+// every load first, then every store).  Same arithmetic per row (bitwise equal,
+// tests/test_gpu_ffn.py).  cfg2 in-step at 1,536 blocks: 15.6-15.8 vs 17.7 us per launch
+// (profiles/r04_dev/ln_fwdp/); dev: HSG_LN_FWDP=<blocks> (0: k_ln_fwd4), HSG_LN_FWDP_R=2.
+template <int NV, int RPW>
+__global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__restrict__ y,
+                                                  const float *__restrict__ x, const float *__restrict__ gamma,
+                                                  const float *__restrict__ beta, float eps, float p_drop,
+                                                  const int64_t *__restrict__ seedp, uint32_t offset,
+                                                  float *__restrict__ out, float *__restrict__ mean,
+                                                  float *__restrict__ rstd) {
+    const int lane = threadIdx.x & 63;
+    const int ng = (n + RPW - 1) / RPW, nw = gridDim.x * 4;
+    int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (g >= ng) return;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    f32x4r yv[RPW][NV], xv[RPW][NV];
+    auto load = [&](int gg) {
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int r = min(gg * RPW + q, n - 1);
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int c = min(4 * lane + 256 * i, d - 4);        // clamped: unused past d
+                yv[q][i] = *reinterpret_cast<const f32x4r *>(y + (size_t)r * d + c);
+                xv[q][i] = *reinterpret_cast<const f32x4r *>(x + (size_t)r * d + c);
+            }
+        }
+    };
+    load(g);
+    for (; g < ng; g += nw) {
+        f32x4r s[RPW][NV];
+        float acc[RPW];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int r = min(g * RPW + q, n - 1);
+            acc[q] = 0.f;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int c = 4 * lane + 256 * i;
+                s[q][i] = f32x4r{0.f, 0.f, 0.f, 0.f};
+                if (c < d) {
+                    const size_t o = (size_t)r * d + c;
+                    f32x4r v = yv[q][i];
+                    if (p_drop > 0.f) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            v[e] = hsg_keep32(dkey, (uint32_t)(o + e), thr) ? v[e] * scale : 0.f;
+                    }
+                    s[q][i] = v + xv[q][i];
+                    acc[q] += (s[q][i][0] + s[q][i][1]) + (s[q][i][2] + s[q][i][3]);
+                }
+            }
+        }
+        if (g + nw < ng) load(g + nw);
+#pragma unroll
+        for (int q = 0; q < RPW; ++q) {
+            const int r = g * RPW + q;
+            const float mu = wsum(acc[q]) / d;
+            float var = 0.f;
+#pragma unroll
+            for (int i = 0; i < NV; ++i)
+                if (4 * lane + 256 * i < d)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { const float t = s[q][i][e] - mu; var = fmaf(t, t, var); }
+            const float rs = rsqrtf(wsum(var) / d + eps);
+            if (r >= n) continue;
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                const int c = 4 * lane + 256 * i;
+                if (c < d) {
+                    const f32x4r gm = *reinterpret_cast<const f32x4r *>(gamma + c);
+                    const f32x4r b = *reinterpret_cast<const f32x4r *>(beta + c);
+                    *reinterpret_cast<f32x4r *>(out + (size_t)r * d + c) = (s[q][i] - mu) * rs * gm + b;
+                }
+            }
+            if (lane == 0) { mean[r] = mu; rstd[r] = rs; }
+        }
+    }
+}
+
 // Backward: one wave per row, two rows in flight per wave (their loads are
 // issued together).  Per block, column partials of dgamma, dbeta and of dy (the
 // gradient of W2's bias, b2) go to part[block][3][d].
@@ -275,6 +361,7 @@ int grid_rows(int n, int cap) {
     return b < cap ? b : cap;
 }
 constexpr int kLnBwdGridCap = 512;
+constexpr int kLnFwdPBlocks = 1536;   // persistent LayerNorm forward: 6 waves per SIMD (768 / 1024 / 2048: slower)
 
 int status() {
     hipError_t e = hipGetLastError();
@@ -305,6 +392,23 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
     if (const char *e = HSG_DEV_ENV("HSG_LN_FWD")) {                   // dev A/B: 0 = scalar, 1-4 rows per wave
         rpw = atoi(e);
         vec = vec && rpw > 0;
+    }
+    int pblocks = HSG_DEV_ENV("HSG_LN_FWD") ? 0 : kLnFwdPBlocks, prow = 1;   // HSG_LN_FWD: k_ln_fwd4 / k_ln_fwd
+    if (const char *e = HSG_DEV_ENV("HSG_LN_FWDP")) pblocks = atoi(e);
+    if (const char *e = HSG_DEV_ENV("HSG_LN_FWDP_R")) prow = atoi(e);
+    if (pblocks > 0 && vec && (d + 255) / 256 == 2) {
+        const int ng = (n + prow - 1) / prow;
+        const int blocks = pblocks < (ng + 3) / 4 ? pblocks : (ng + 3) / 4;
+#ifdef HSG_DEV
+        if (prow == 2) {
+            hipLaunchKernelGGL((k_ln_fwd4p<2, 2>), dim3(blocks), block, 0, st, n, d, y, x, gamma, beta, eps, p_drop,
+                               seed, offset, out, mean, rstd);
+            return status();
+        }
+#endif
+        hipLaunchKernelGGL((k_ln_fwd4p<2, 1>), dim3(blocks), block, 0, st, n, d, y, x, gamma, beta, eps, p_drop, seed,
+                           offset, out, mean, rstd);
+        return status();
     }
     if (vec) {
         const int nv = (d + 255) / 256;

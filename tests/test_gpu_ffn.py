@@ -139,3 +139,34 @@ def test_one_launch_narrow_ffn_matches_split_path(monkeypatch, n, p):
     if p > 0:
         y, out = b[2], b[0]
         assert torch.isfinite(out).all() and y.shape == (n, 64)
+
+
+@pytest.mark.parametrize("variant", ["1024,1", "512,2", "7,1", "3,2"])
+@pytest.mark.parametrize("n,p", [(3000, 0.1), (77, 0.0), (1, 0.1)])
+def test_ln_fwd_persistent_variant_bitwise(monkeypatch, variant, n, p):
+    """The persistent LayerNorm forward (k_ln_fwd4p, the product default for 257..512
+    columns: next row group's loads ahead; dev grids / two-row groups) against the
+    one-round k_ln_fwd4 (HSG_LN_FWDP=0): the same per-row arithmetic, so out, mean and
+    rstd are bitwise equal; tiny grids force many groups per wave, odd n a ragged pair."""
+    from helpers import skip_unless_dev
+    from hetersumgraph_amd._lib import check, load
+    skip_unless_dev(False)
+    torch.manual_seed(n)
+    d = 300
+    y, x = torch.randn(n, d, device="cuda"), torch.randn(n, d, device="cuda")
+    g, b = 1 + 0.1 * torch.randn(d, device="cuda"), 0.1 * torch.randn(d, device="cuda")
+    seed = torch.tensor([77], dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for v in ("0,1", variant):
+        blocks, r = v.split(",")
+        monkeypatch.setenv("HSG_LN_FWDP", blocks)
+        monkeypatch.setenv("HSG_LN_FWDP_R", r)
+        out, mean, rstd = torch.empty_like(y), torch.empty(n, device="cuda"), torch.empty(n, device="cuda")
+        check(load().hsg_ln_fwd(n, d, y.data_ptr(), x.data_ptr(), g.data_ptr(), b.data_ptr(), 1e-5, p,
+                                seed.data_ptr(), 9, out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), st),
+              "hsg_ln_fwd")
+        res[v] = (out, mean, rstd)
+    torch.cuda.synchronize()
+    for a, c in zip(res["0,1"], res[variant]):
+        assert torch.equal(a, c)
