@@ -316,6 +316,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
     }
 }
 
+// Vector backward (d % 4 == 0, 16-byte aligned rows, 257..512 columns): lane owns the
+// column quads 4*lane + 256*i (float4 loads and stores: 6 instead of 15 row loads), each
+// wave walks rows r, r + waves, ... with the next row's dout / y / x requested before
+// this row's wave sums and stores (as k_ln_fwd4p).  Same per-element arithmetic as
+// k_ln_bwd; the row sums add a lane's columns in another order (fp32 noise), and the
+// block partials go to the same part[block][3][d] layout.  cfg2 in-step: 23.0-23.1 vs
+// 24.6 us per launch at the 512-block cap (1,024 / 1,536 blocks: 25.3 / 24.0 us and
+// larger partial slabs; profiles/r04_dev/ln_bwdp/).
+template <int NV>
+__global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__restrict__ dout,
+                                                  const float *__restrict__ y, const float *__restrict__ x,
+                                                  const float *__restrict__ gamma, const float *__restrict__ mean,
+                                                  const float *__restrict__ rstd, float p_drop,
+                                                  const int64_t *__restrict__ seedp, uint32_t offset,
+                                                  float *__restrict__ dy, float *__restrict__ dx,
+                                                  float *__restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float s_red[4][kMaxPerLane * 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
+    const uint32_t thr = hsg_drop_threshold(p_drop);
+    const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+    int cq[NV];
+    bool cok[NV];
+    f32x4r dg[NV], db[NV], dyb[NV], gam[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        cok[i] = 4 * lane + 256 * i < d;
+        cq[i] = cok[i] ? 4 * lane + 256 * i : d - 4;               // clamped: loads unused past d
+        dg[i] = db[i] = dyb[i] = f32x4r{0.f, 0.f, 0.f, 0.f};
+        gam[i] = cok[i] ? *reinterpret_cast<const f32x4r *>(gamma + cq[i]) : f32x4r{0.f, 0.f, 0.f, 0.f};
+    }
+    const int nw = gridDim.x * 4;
+    int r = blockIdx.x * 4 + wid;
+    f32x4r yv[NV], xv[NV], gv[NV];
+    float mu = 0.f, rs = 0.f;
+    auto load = [&](int rr) {
+        mu = mean[rr];
+        rs = rstd[rr];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const size_t o = (size_t)rr * d + cq[i];
+            yv[i] = *reinterpret_cast<const f32x4r *>(y + o);
+            xv[i] = *reinterpret_cast<const f32x4r *>(x + o);
+            gv[i] = *reinterpret_cast<const f32x4r *>(dout + o);
+        }
+    };
+    if (r < n) load(r);
+    for (; r < n; r += nw) {
+        const size_t rb = (size_t)r * d;
+        f32x4r xh[NV], g[NV];
+        uint32_t keep = 0xFFFFFFFFu;                                 // bit 4 i + e
+        float sg = 0.f, sgx = 0.f;
+        const float rsr = rs;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            xh[i] = g[i] = f32x4r{0.f, 0.f, 0.f, 0.f};
+            if (cok[i]) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float v = yv[i][e];
+                    if (p_drop > 0.f) {
+                        const bool k = hsg_keep32(dkey, (uint32_t)(rb + cq[i] + e), thr);
+                        if (!k) keep &= ~(1u << (4 * i + e));
+                        v = k ? v * scale : 0.f;
+                    }
+                    xh[i][e] = (v + xv[i][e] - mu) * rs;
+                    const float go = gv[i][e];
+                    g[i][e] = go * gam[i][e];
+                    sg += g[i][e];
+                    sgx = fmaf(g[i][e], xh[i][e], sgx);
+                    dg[i][e] = fmaf(go, xh[i][e], dg[i][e]);
+                    db[i][e] += go;
+                }
+            }
+        }
+        if (r + nw < n) load(r + nw);
+        const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            if (cok[i]) {
+                f32x4r ds, dyv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    ds[e] = rsr * (g[i][e] - mg - xh[i][e] * mgx);
+                    dyv[e] = (keep >> (4 * i + e)) & 1u ? ds[e] * scale : 0.f;
+                }
+                *reinterpret_cast<f32x4r *>(dx + rb + cq[i]) = ds;
+                *reinterpret_cast<f32x4r *>(dy + rb + cq[i]) = dyv;
+                dyb[i] += dyv;
+            }
+        }
+    }
+    // block partials, three passes through one LDS slab (fixed order: deterministic)
+    float *dst = part + (size_t)blockIdx.x * 3 * d;
+#pragma unroll
+    for (int which = 0; which < 3; ++which) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            if (cok[i])
+                *reinterpret_cast<f32x4r *>(&s_red[wid][cq[i]]) = which == 0 ? dg[i] : which == 1 ? db[i] : dyb[i];
+        __syncthreads();
+        for (int c = threadIdx.x; c < d; c += blockDim.x)
+            dst[which * d + c] = s_red[0][c] + s_red[1][c] + s_red[2][c] + s_red[3][c];
+        __syncthreads();
+    }
+}
+
 // Column sums of the FFN backward's block-row partial slabs in one launch: the dH
 // GEMM's column partials hpart[rows_h][d_hid] -> db1, and hsg_ln_bwd's
 // part[rows_ln][3][d] -> dgamma, dbeta, db2.  Block = (32 columns) x (8 row
@@ -361,6 +468,12 @@ int grid_rows(int n, int cap) {
     return b < cap ? b : cap;
 }
 constexpr int kLnBwdGridCap = 512;
+constexpr bool kLnBwdVec = true;       // k_ln_bwd4p for 257..512 aligned columns (dev: HSG_LN_BWDP=0)
+// the backward's grid cap: hsg_ln_bwd_blocks and hsg_ln_bwd must agree (part rows)
+int ln_bwd_cap() {
+    if (const char *e = HSG_DEV_ENV("HSG_LN_BWD_CAP")) return atoi(e) > 0 ? atoi(e) : kLnBwdGridCap;
+    return kLnBwdGridCap;
+}
 constexpr int kLnFwdPBlocks = 1536;   // persistent LayerNorm forward: 6 waves per SIMD (768 / 1024 / 2048: slower)
 
 int status() {
@@ -372,7 +485,7 @@ int status() {
 
 extern "C" {
 
-int hsg_ln_bwd_blocks(int n) { return grid_rows(n, kLnBwdGridCap); }
+int hsg_ln_bwd_blocks(int n) { return grid_rows(n, ln_bwd_cap()); }
 
 int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma, const float *beta, float eps,
                float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
@@ -442,9 +555,17 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
         (p_drop > 0.f && (long)n * d >= (1L << 32)))
         return HSG_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    dim3 grid(grid_rows(n, kLnBwdGridCap)), block(256);
+    dim3 grid(grid_rows(n, ln_bwd_cap())), block(256);
     if (n == 0) return (int)hipMemsetAsync(part, 0, sizeof(float) * 3 * d * grid.x, st);
     const int npl = (d + 63) / 64;
+    bool vec = kLnBwdVec;
+    if (const char *e = HSG_DEV_ENV("HSG_LN_BWDP")) vec = atoi(e) != 0;            // dev A/B
+    const auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    if (vec && d % 4 == 0 && (d + 255) / 256 == 2 && al(dout) && al(y) && al(x) && al(gamma) && al(dy) && al(dx)) {
+        hipLaunchKernelGGL((k_ln_bwd4p<2>), grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, seed,
+                           offset, dy, dx, part);
+        return status();
+    }
 #define HSG_LNB(K)                                                                                       \
     case K:                                                                                              \
         hipLaunchKernelGGL(k_ln_bwd<K>, grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, \

@@ -170,3 +170,43 @@ def test_ln_fwd_persistent_variant_bitwise(monkeypatch, variant, n, p):
     torch.cuda.synchronize()
     for a, c in zip(res["0,1"], res[variant]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("cap", ["512", "1024", "3"])
+@pytest.mark.parametrize("n,p", [(3000, 0.1), (77, 0.0), (1, 0.1), (4097, 0.1)])
+def test_ln_bwd_vector_variant(monkeypatch, cap, n, p):
+    """k_ln_bwd4p (the product default for 257..512 columns: float4 columns, next row's
+    loads ahead) against k_ln_bwd (HSG_LN_BWDP=0) on the same grid (HSG_LN_BWD_CAP): dgamma / dbeta partials bitwise
+    (same rows per block, same per-column order), dx / dy / db2 partials to fp32 noise
+    (the row sums add a lane's columns in another order); tiny caps walk many rows per
+    wave."""
+    from helpers import skip_unless_dev
+    from hetersumgraph_amd._lib import check, load
+    skip_unless_dev(False)
+    torch.manual_seed(n)
+    d = 300
+    dev = "cuda"
+    y, x, dout = (torch.randn(n, d, device=dev) for _ in range(3))
+    g = 1 + 0.1 * torch.randn(d, device=dev)
+    s = y + x
+    mean = s.mean(1)
+    rstd = torch.rsqrt(s.var(1, unbiased=False) + 1e-5)
+    seed = torch.tensor([91], dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    monkeypatch.setenv("HSG_LN_BWD_CAP", cap)
+    lib = load()
+    res = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("HSG_LN_BWDP", v)
+        nb = lib.hsg_ln_bwd_blocks(n)
+        dy, dx = torch.empty_like(y), torch.empty_like(y)
+        part = torch.empty(nb, 3, d, device=dev)
+        check(lib.hsg_ln_bwd(n, d, dout.data_ptr(), y.data_ptr(), x.data_ptr(), g.data_ptr(), mean.data_ptr(),
+                             rstd.data_ptr(), p, seed.data_ptr(), 5, dy.data_ptr(), dx.data_ptr(), part.data_ptr(), st),
+              "hsg_ln_bwd")
+        res[v] = (dx, dy, part)
+    torch.cuda.synchronize()
+    a, b = res["0"], res["1"]
+    assert torch.equal(a[2][:, :2], b[2][:, :2])
+    for u, w in ((a[0], b[0]), (a[1], b[1]), (a[2][:, 2], b[2][:, 2])):
+        assert (u - w).abs().max().item() <= 2e-6 * max(1.0, u.abs().max().item())
