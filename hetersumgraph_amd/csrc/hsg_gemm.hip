@@ -2305,7 +2305,7 @@ struct RedJobs {
 // scalar (V = 1: 32 columns per block) and the float4 (V = 4: 128 columns per block,
 // 512-B row pieces) form, so both give bitwise equal sums.
 extern "C++" {
-template <int V>
+template <int V, bool PRED = false>
 __device__ __forceinline__ void slab_reduce_job(const RedJobs &j, int q, int blk) {
     typedef float vec_t __attribute__((ext_vector_type(V)));
     __shared__ __attribute__((aligned(16))) float red[8][32 * V];
@@ -2322,16 +2322,24 @@ __device__ __forceinline__ void slab_reduce_job(const RedJobs &j, int q, int blk
             const float *P = j.seg[q][sg] + coff + c;
             const int rows = j.rows[q][sg], per = (rows + orows - 1) / orows;
             const int r1 = min(rows, (ob + 1) * per);
-            // up to 16 rows in flight per thread, ALL requested before any is added: rows
-            // past the range load a clamped (valid) row and add 0, so a segment of <= 128
+            // up to 16 rows in flight per thread, ALL requested before any is added (PRED,
+            // the default: rows past the range are not loaded and add 0; 25.2 -> 23.4 us per
+            // cfg2 step, profiles/r04_dev/slab_pred/; dev HSG_SLAB_PRED=0: they load a
+            // clamped valid row, as before), so a segment of <= 128
             // rows is one round trip (the ragged 4-row / 1-row tail loops made the 100-row
             // head-projection segments ~4 dependent round trips each); rows go into the
             // four partial sums in row order
             for (int r = ob * per + g; r < r1; r += 128) {
                 vec_t v[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u)
-                    v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)min(r + 8 * u, r1 - 1) * pitch);
+                for (int u = 0; u < 16; ++u) {
+                    if constexpr (PRED) {       // rows past the range not loaded at all (round 4)
+                        v[u] = vec_t(0.f);
+                        if (r + 8 * u < r1) v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)(r + 8 * u) * pitch);
+                    } else {
+                        v[u] = *reinterpret_cast<const vec_t *>(P + (size_t)min(r + 8 * u, r1 - 1) * pitch);
+                    }
+                }
 #pragma unroll
                 for (int u = 0; u < 16; ++u) s[u & 3] += r + 8 * u < r1 ? v[u] : vec_t(0.f);
             }
@@ -2348,15 +2356,16 @@ __device__ __forceinline__ void slab_reduce_job(const RedJobs &j, int q, int blk
         *o = j.acc[q] ? *o + j.scale[q] * a : j.scale[q] * a;
     }
 }
-}  // extern "C++"
 
+template <bool PRED = false>
 __global__ __launch_bounds__(256) void k_slab_reduce(RedJobs j) {
     int q = 0;
     while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
     const int blk = (int)blockIdx.x - j.start[q];
-    if (j.vec[q] == 4) slab_reduce_job<4>(j, q, blk);
-    else slab_reduce_job<1>(j, q, blk);
+    if (j.vec[q] == 4) slab_reduce_job<4, PRED>(j, q, blk);
+    else slab_reduce_job<1, PRED>(j, q, blk);
 }
+}  // extern "C++"
 
 int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *out_rows, const int *pitch,
                     const int *coff, const float *scale, const int *accumulate, const int *nseg,
@@ -2387,7 +2396,13 @@ int hsg_slab_reduce(int njobs, float *const *out, const int *cols, const int *ou
         j.start[q + 1] = j.start[q] + (cols[q] + 32 * j.vec[q] - 1) / (32 * j.vec[q]) * out_rows[q];
     }
     if (j.start[njobs] == 0) return 0;
-    hipLaunchKernelGGL(k_slab_reduce, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
+#ifdef HSG_DEV
+    if (const char *e = HSG_DEV_ENV("HSG_SLAB_PRED"); e && atoi(e) == 0) {
+        hipLaunchKernelGGL(k_slab_reduce<false>, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
+        return hipGetLastError() == hipSuccess ? 0 : HSG_EINVAL;
+    }
+#endif
+    hipLaunchKernelGGL(k_slab_reduce<true>, dim3(j.start[njobs]), dim3(256), 0, (hipStream_t)stream, j);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

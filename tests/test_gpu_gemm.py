@@ -334,9 +334,12 @@ def test_slab_reduce_float4_columns_bitwise_equal_scalar(cols, pitch, coff, out_
         return out
 
     vec = run()
+    monkeypatch.setenv("HSG_SLAB_PRED", "0")        # dev: clamped loads of rows past a range
+    pred = run()
     monkeypatch.setenv("HSG_SLAB_VEC", "1")
     scalar = run()
     assert torch.equal(vec, scalar)
+    assert torch.equal(vec, pred)
     per = [(sg.shape[0] + out_rows - 1) // out_rows for sg in segs]
     ref = torch.full((out_rows, cols), 3.0, dtype=torch.float64, device="cuda")
     for sg, pr in zip(segs, per):
