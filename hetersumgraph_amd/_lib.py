@@ -177,6 +177,48 @@ def version() -> str:
     return load().hsg_version().decode()
 
 
+_is_dev = None
+_OPTIONS = {}
+
+
+def is_dev() -> bool:
+    """True when the loaded library is the dev build (libhsg_dev.so via HSG_LIB_PATH)."""
+    global _is_dev
+    if _is_dev is None:
+        _is_dev = version().endswith(" dev")
+    return _is_dev
+
+
+def path_option(name: str, default: str) -> str:
+    """A Python-side path switch (e.g. ``HSG_FUSED_STACK``): an explicit selection made
+    with :func:`path_options` first; the environment variable of the same name only
+    when the dev library is loaded (the A/B tools); otherwise the measured default.
+    The product path therefore never changes algorithm or precision because of the
+    environment (the C library's switches follow the same rule, csrc/hsg_dev.h)."""
+    if name in _OPTIONS:
+        return _OPTIONS[name]
+    if is_dev():
+        return os.environ.get(name, default)
+    return default
+
+
+class path_options:
+    """``with path_options(HSG_FUSED_STACK="0"): ...`` -- explicit, scoped path
+    selections for tests and tools (values are strings, as the environment's)."""
+
+    def __init__(self, **kw):
+        self.kw = {k: str(v) for k, v in kw.items()}
+
+    def __enter__(self):
+        self.prev = dict(_OPTIONS)
+        _OPTIONS.update(self.kw)
+        return self
+
+    def __exit__(self, *exc):
+        _OPTIONS.clear()
+        _OPTIONS.update(self.prev)
+
+
 class KernelClock:
     """In-step kernel timing for bench.py: while a clock is active (``with
     KernelClock() as clk``), tagged edge launches are timed inside an ordinary

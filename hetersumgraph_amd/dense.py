@@ -6,7 +6,7 @@ projection need (bias, ReLU, ReLU-backward mask, accumulate).  Everything is
 enqueued on the current stream; no host synchronisation.
 
 Operand precision, chosen process-wide with :func:`set_gemm_dtype` /
-:func:`gemm_dtype` or ``HSG_GEMM_DTYPE``:
+:func:`gemm_dtype` (never from the environment):
 * 'f32' (default, the parity contract): hsg_gemm_f32 -- fp32 operands and
   fp32-accurate products from three bf16 limbs per operand (six limb products on
   the bf16 matrix cores, fp32 accumulation; include/hsg.h);
@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
-import os
 
 import torch
 
@@ -27,7 +26,7 @@ from . import _lib
 from ._lib import HSG_EINVAL, HSG_EPI_ADD, HSG_EPI_RELU_BWD, HSG_EPI_STORE, check, load, ptr, stream_of
 
 
-_GEMM_DTYPE = os.environ.get("HSG_GEMM_DTYPE", "f32")
+_GEMM_DTYPE = "f32"             # explicit only (set_gemm_dtype / gemm_dtype / bench --dtype)
 _FNS = {"f32": "hsg_gemm_f32", "f32mfma": "hsg_gemm_f32_mfma", "bf16": "hsg_gemm_bf16"}
 
 
@@ -187,7 +186,7 @@ def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out
     GATLayer.py:40-42 in its epilogue, the dropout stream of hsg_ln_fwd).  Returns
     False (nothing launched) when the shape has no such plan; the caller then runs
     gemm_psw + hsg_ln_fwd."""
-    if os.environ.get("HSG_FFN_LN_EPI", "0") != "1":                 # opt-in (dev library): break-even
+    if _lib.path_option("HSG_FFN_LN_EPI", "0") != "1":                 # opt-in (dev library): break-even
         return False
     lib = load()
     M, K = A.shape
@@ -245,8 +244,8 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     # and the smaller slices keep each slice's operand rows L2-resident (cfg2 step
     # -17..-21 us against the 32 of hsg_gemm_f32's own plan; 24 / 48 / 96 / 128 are
     # slower, tools/ab.py)
-    splits = int(os.environ.get("HSG_DW_SPLITS", "64"))          # dev A/B
-    minrows = int(os.environ.get("HSG_DW_MINROWS", "0"))         # dev A/B: rows per K slice
+    splits = int(_lib.path_option("HSG_DW_SPLITS", "64"))          # dev A/B
+    minrows = int(_lib.path_option("HSG_DW_MINROWS", "0"))         # dev A/B: rows per K slice
     if minrows > 0:
         splits = min(splits, K // minrows)
     splits = max(2, min(splits, (K + 31) // 32))
@@ -279,7 +278,7 @@ def gemm_dw_slabs(pairs, splits=None):
     kt = (K + 31) // 32
     if splits is None:
         tiles = sum(lib.hsg_gemm_dw_tiles(A.shape[1], B.shape[1]) for A, B in pairs)
-        splits = int(os.environ.get("HSG_DW2_SPLITS", "0")) or max(1, (2 * 256) // max(tiles, 1))   # dev A/B
+        splits = int(_lib.path_option("HSG_DW2_SPLITS", "0")) or max(1, (2 * 256) // max(tiles, 1))   # dev A/B
         splits = max(1, min(splits, kt // 4))
     # every K slice non-empty (the kernel's slice length is ceil(kt / splits) tiles)
     per = (kt + splits - 1) // splits

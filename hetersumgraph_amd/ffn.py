@@ -20,10 +20,10 @@ whose backward writes the parameter gradients straight into their destination
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from . import _lib
 from . import rng as hsg_rng
 from ._lib import HSG_EINVAL, check, load, ptr, stream_of
 from .dense import (gemm, gemm_psw, gemm_psw_elug, gemm_psw_ln, get_gemm_dtype, psw_row_tiles, row_tiles,
@@ -37,7 +37,7 @@ def _fused_ok(lib, x, w1, w2):
     d=64, d_hid=512) cover this call: contiguous operands.  They compute in fp32 in
     either GEMM mode (in the bf16 mode this small FFN simply stays exact).
     HSG_FFN_FUSED=0 selects the split path (A/B tests)."""
-    if os.environ.get("HSG_FFN_FUSED", "1") == "0":
+    if _lib.path_option("HSG_FFN_FUSED", "1") == "0":
         return False
     d_hid, d = w1.shape
     return (bool(lib.hsg_ffn_small_supported(d, d_hid)) and x.is_contiguous() and w1.is_contiguous()
@@ -61,7 +61,7 @@ def ffn_wsplit(x, w1, b1, w2, b2, launch=True):
     lib = load()
     if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
         return None
-    if get_gemm_dtype() not in ("f32", "bf16") or os.environ.get("HSG_GEMM_PSW", "1") == "0":
+    if get_gemm_dtype() not in ("f32", "bf16") or _lib.path_option("HSG_GEMM_PSW", "1") == "0":
         return None
     d_hid, d = w1.shape
     if d % 4 or d_hid % 4 or not (w1.is_contiguous() and w2.is_contiguous()):

@@ -12,10 +12,10 @@ fused stack (:mod:`hetersumgraph_amd.stack`).
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
+from . import _lib
 from . import rng as hsg_rng
 import ctypes
 
@@ -67,7 +67,7 @@ def dropmasks(jobs, device, stream_of_t, wt=None, wsplit_job=None):
 def narrow_heads(d_in, H, D):
     """Whether the VALU projection (hsg_hproj_fwd_t8, D = 8) takes (d_in, H, D);
     HSG_HPROJ_FWDV=0 keeps the MFMA kernel (dev A/B)."""
-    return os.environ.get("HSG_HPROJ_FWDV", "1") != "0" and bool(load().hsg_hproj_fwd_t8_supported(d_in, H, D))
+    return _lib.path_option("HSG_HPROJ_FWDV", "1") != "0" and bool(load().hsg_hproj_fwd_t8_supported(d_in, H, D))
 
 
 def transposed_weight(W, H, D):

@@ -16,7 +16,6 @@ training step can be captured into a HIP graph.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -166,7 +165,7 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         sigma = Z.new_empty(n_src, H)
         check(lib.hsg_attn_src_logits(n_src, H, D, ptr(Z), ptr(a1), ptr(sigma), st), "hsg_attn_src_logits")
     relp = ctypes.byref(rel.cstruct())
-    no_h = ((no_h or (not keep_h and os.environ.get("HSG_GAT_NOH", "0") == "1")) and origin is not None
+    no_h = ((no_h or (not keep_h and _lib.path_option("HSG_GAT_NOH", "0") == "1")) and origin is not None
             and bool(lib.hsg_gat_bwd_dst_noh_supported(relp, H, D)))
     h = None if no_h else Z.new_empty(n_dst, HD)
     if origin is None:

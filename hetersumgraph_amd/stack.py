@@ -31,10 +31,10 @@ HSG_CHECK_NAN=1).
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
+from . import _lib
 from . import rng as hsg_rng
 from ._lib import load, stream_of
 from .dense import gemm, gemm_dw_slabs, gemm_slabs
@@ -145,7 +145,7 @@ def _apply_fwd(lay, rel, T, neighbor, origin, tables=None, x_out=None, H_out=Non
     # with the FFN on the pre-split-weight GEMMs, its backward's last GEMM also makes the
     # edge layer's G rows (hsg_gemm_f32_psw_elug), so the forward need not store h
     # (HSG_GAT_GEPI=0: h stored and G made in the dst pass, for A/B tests)
-    g_epi = wsplit is not None and not isinstance(wsplit, str) and os.environ.get("HSG_GAT_GEPI", "1") != "0"
+    g_epi = wsplit is not None and not isinstance(wsplit, str) and _lib.path_option("HSG_GAT_GEPI", "1") != "0"
     x, gsaved = gat_table_fwd(Z, lay.attn, T, lay.wf, lay.bf, origin, rel, H, D, LEAKY_SLOPE, tables=tables,
                               out=x_out, sigma=sigma, keep_h=False, no_h=g_epi)
     d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
@@ -172,7 +172,7 @@ def _attn_dst(grads, lay, T):
 def _merged_bwd(gsaved):
     """The one-pass edge backward (hsg_gat_bwd_src_g) covers this application's
     relation and head shape (HSG_GAT_MERGED=0: the dst + src pair, for A/B tests)."""
-    if os.environ.get("HSG_GAT_MERGED", "1") == "0":
+    if _lib.path_option("HSG_GAT_MERGED", "1") == "0":
         return False
     rel, H, D = gsaved[11], gsaved[12], gsaved[13]
     return bool(load().hsg_gat_bwd_src_g_supported(ctypes.byref(rel.cstruct()), H, D))
@@ -266,7 +266,7 @@ class _GatStack(torch.autograd.Function):
         # the narrow-head (VALU) projection's transposed weight comes out of the same
         # launch as the masks (hsg_dropmask_multi_wt; HSG_WT_FOLD=0: its own launch)
         narrow = [lay for lay in (w2s, s2w) if lay.p_attn > 0 and narrow_heads(lay.W.shape[1], lay.H, lay.D)]
-        fold = narrow[0] if narrow and jobs and os.environ.get("HSG_WT_FOLD", "1") != "0" else None
+        fold = narrow[0] if narrow and jobs and _lib.path_option("HSG_WT_FOLD", "1") != "0" else None
         # ... and so are the wide FFN's weight limb planes (hsg_step_prologue: one launch
         # for masks, transpose and split; HSG_WT_FOLD=0: separate launches)
         wsplits, split_job = {}, None
@@ -312,7 +312,7 @@ class _GatStack(torch.autograd.Function):
             apps.append((lay, saved, nb, org, a))
 
         # the attention tables depend on the parameters only: once per layer
-        if os.environ.get("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
+        if _lib.path_option("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
             tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T)))
         else:
             tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
@@ -384,7 +384,7 @@ class _GatStack(torch.autograd.Function):
                 if dw is not None:
                     todo.append((p, A, B, m, n, dw, a_w))
             pair = gemm_dw_slabs([(A, B) for _, A, B, *_ in todo]) \
-                if todo and os.environ.get("HSG_DW_PAIR", "1") != "0" else None
+                if todo and _lib.path_option("HSG_DW_PAIR", "1") != "0" else None
             for k, (p, A, B, m, n, dw, a_w) in enumerate(todo):
                 sl = pair[k] if pair is not None else gemm_slabs(A, B, a_t=True)   # split-K slabs
                 if sl is not None:
@@ -394,7 +394,7 @@ class _GatStack(torch.autograd.Function):
         batch.flush()
         fin = [(ws, lay, _attn_dst(pgrads, lay, T)) for lay, ws in stages.values()]   # in order (dT flags)
         fin = [f for f in fin if f[2] is not None]
-        if len(fin) == 2 and os.environ.get("HSG_ATTN_PAIR", "1") != "0":
+        if len(fin) == 2 and _lib.path_option("HSG_ATTN_PAIR", "1") != "0":
             attn_params_finish_pair(fin[0], fin[1], T)                # both layers in one launch
         else:
             for ws, lay, dst in fin:
@@ -412,7 +412,7 @@ class _GatStack(torch.autograd.Function):
 def fused_stack_ok(G, word2sent, sent2word, T, w, s):
     """Whether :func:`gat_stack` covers this call (else use the per-layer path)."""
     from .module.GATLayer import CHECK_NAN, table_weight
-    if os.environ.get("HSG_FUSED_STACK", "1") == "0":   # per-layer path (A/B tests)
+    if _lib.path_option("HSG_FUSED_STACK", "1") == "0":   # per-layer path (A/B tests)
         return False
     if CHECK_NAN or not (w.is_cuda and s.is_cuda) or w.dtype != torch.float32 or s.dtype != torch.float32:
         return False

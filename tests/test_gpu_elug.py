@@ -194,6 +194,37 @@ def test_psw_elug_rho_partials(M, mode):
     assert (err <= bound).all()
 
 
+@pytest.mark.parametrize("mode", ["f32", "bf16"])
+def test_psw_elug_rho_under_big_tile_switch(mode, monkeypatch):
+    """the dev library's HSG_GEMM11=1 routes the psw GEMMs to k_gemm11,
+    whose epilogue writes C and G but no rho.  The rho GEMM must decline it and run on
+    k_gemm7: rho fully written (no NaN left from the prefill) and bitwise equal to the
+    run without the switch, C and G too.  Dev library only."""
+    from helpers import skip_unless_dev
+    skip_unless_dev(False)
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    M, N, K, D = 19200, 300, 512, 50
+    torch.manual_seed(5)
+    dH = torch.randn(M, K, device="cuda")
+    W1 = torch.randn(K, N, device="cuda") / K ** 0.5
+    with gemm_dtype(mode):
+        (S,) = split_weights((W1, True))
+    ds = torch.randn(M, N, device="cuda")
+    origin = torch.randn(M, N, device="cuda")
+    x = torch.nn.functional.elu(2 * torch.randn(M, N, device="cuda")) + origin
+    outs = []
+    for switch in ("0", "1"):
+        monkeypatch.setenv("HSG_GEMM11", switch)
+        out, G = ds.clone(), torch.empty_like(ds)
+        rho = torch.full((M, (N + 63) // 64, 3), float("nan"), device="cuda")
+        assert gemm_psw_elug(dH, S, out, x, origin, G, rho, D)
+        outs.append((out, G, rho))
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[1][2]).all()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_psw_elug_rho_declines_bad_head_dim():
     from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
     W1 = torch.randn(64, 300, device="cuda")

@@ -4,6 +4,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from hetersumgraph_amd import _lib
+
 pytestmark = pytest.mark.gpu
 
 
@@ -121,7 +123,7 @@ def test_one_launch_narrow_ffn_matches_split_path(monkeypatch, n, p):
     dout = torch.randn(n, 64, device=dev)
     res = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("HSG_FFN_FUSED", flag)
+        monkeypatch.setitem(_lib._OPTIONS, "HSG_FFN_FUSED", flag)
         rng.manual_seed(5)
         out, saved = ffn_fwd(x, w1, b1, w2, b2, g, bt, p)
         grads = [torch.empty_like(t) for t in (w1, w2, b1, b2, g, bt)]

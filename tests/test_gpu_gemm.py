@@ -478,7 +478,6 @@ def test_psw_ln_epilogue_equals_gemm_plus_ln(M, p_drop, dtype):
     the arithmetic of k_ln_fwd4).  Dev library (measured break-even: the product
     library declines and the FFN runs the GEMM and hsg_ln_fwd)."""
     skip_unless_dev(False)
-    import os
     from hetersumgraph_amd import rng as hsg_rng
     from hetersumgraph_amd._lib import load, ptr, stream_of
     from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, gemm_psw_ln, split_weights
@@ -494,11 +493,9 @@ def test_psw_ln_epilogue_equals_gemm_plus_ln(M, p_drop, dtype):
     seed_t, off = hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0)
     y1, out1 = torch.empty(M, N, device="cuda"), torch.empty(M, N, device="cuda")
     mean1, rstd1 = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
-    os.environ["HSG_FFN_LN_EPI"] = "1"
-    try:
+    from hetersumgraph_amd._lib import path_options
+    with path_options(HSG_FFN_LN_EPI="1"):
         assert gemm_psw_ln(Hm, S, b2, x, gamma, beta, 1e-5, p_drop, seed_t, off, y1, out1, mean1, rstd1)
-    finally:
-        del os.environ["HSG_FFN_LN_EPI"]
     y2 = gemm_psw(Hm, S, bias=b2)
     out2, mean2, rstd2 = torch.empty_like(out1), torch.empty_like(mean1), torch.empty_like(rstd1)
     lib = load()

@@ -12,6 +12,8 @@ import numpy as np
 import pytest
 import torch
 
+from hetersumgraph_amd import _lib
+
 pytestmark = pytest.mark.gpu
 
 
@@ -81,8 +83,8 @@ def _zero(mods, T, Xw, Xs):
     ("hsg", True, True, 2, 2, 0), ("hsg", True, False, 1, 2, 0),
     ("hsg", True, True, 2, 2, 1), ("hdsg", True, True, 1, 2, 1), ("hsg", False, True, 1, 1, 1)])
 def test_fused_stack_matches_layerwise(monkeypatch, kind, train, word_grad, reps, n_iter, noh):
-    monkeypatch.setenv("HSG_GAT_NOH", str(int(noh == 1)))
-    monkeypatch.setenv("HSG_GAT_GEPI", str(int(noh == 2)))
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_GAT_NOH", str(int(noh == 1)))
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_GAT_GEPI", str(int(noh == 2)))
     G = _graph(kind, 3)
     w2s, s2w, T = _modules(7, 0.1)
     for m in (w2s, s2w):
@@ -92,7 +94,7 @@ def test_fused_stack_matches_layerwise(monkeypatch, kind, train, word_grad, reps
     Xw = (0.4 * torch.randn(rel_s.n_dst, 300, device="cuda", generator=gen)).requires_grad_(word_grad)
     Xs = torch.randn(rel_w.n_dst, 64, device="cuda", generator=gen).requires_grad_()
     R = torch.randn(rel_w.n_dst, 64, device="cuda", generator=gen)
-    monkeypatch.setenv("HSG_FUSED_STACK", "1")
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_FUSED_STACK", "1")
     fo, fg, fx = _run(G, w2s, s2w, T, Xw, Xs, R, n_iter, fused=True, reps=reps)
     _zero((w2s, s2w), T, Xw, Xs)
     lo, lg, lx = _run(G, w2s, s2w, T, Xw, Xs, R, n_iter, fused=False, reps=reps)
@@ -134,7 +136,7 @@ def test_fused_stack_is_used_by_hsumgraph(monkeypatch):
     Xs = torch.randn(rel_w.n_dst, 64, device="cuda", requires_grad=True)
     s = HSumGraph.gat_stack(m, G, Xw, Xs)
     assert type(s.grad_fn).__name__.startswith("_GatStack")
-    monkeypatch.setenv("HSG_FUSED_STACK", "0")
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_FUSED_STACK", "0")
     s = HSumGraph.gat_stack(m, G, Xw, Xs)
     assert not type(s.grad_fn).__name__.startswith("_GatStack")
 
@@ -165,7 +167,7 @@ def test_fused_stack_is_an_ordinary_autograd_node(monkeypatch):
     s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
     got = torch.autograd.grad((s * R).sum(), want)
     assert all(p.grad is None for p in params) and Xw.grad is None and Xs.grad is None
-    monkeypatch.setenv("HSG_FUSED_STACK", "0")
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_FUSED_STACK", "0")
     w, s = Xw, w2s(G, Xw, Xs)
     for _ in range(2):
         w = s2w(G, w, s)
@@ -173,7 +175,7 @@ def test_fused_stack_is_an_ordinary_autograd_node(monkeypatch):
     ref = torch.autograd.grad((s * R).sum(), want)
     for a, b in zip(got, ref):
         assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1.0)
-    monkeypatch.setenv("HSG_FUSED_STACK", "1")
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_FUSED_STACK", "1")
     s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
     s.backward(R, inputs=[Xs])
     assert Xs.grad is not None and all(p.grad is None for p in params) and Xw.grad is None
