@@ -234,7 +234,7 @@ def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False, issued=False):
         peak = FP32_MFMA_PEAK_TFLOPS if kind == "W2S" else dense_peak
         ffn = 2.0 * m * d * dh
         items.append((f"ffn_{kind}", 4.0 * (m * d + m * dh) * 2 * 3, 6 * ffn, peak))
-    # the deferred FFN weight gradients' split-K partial slabs (dense.gemm_slabs): each
+    # the deferred FFN weight gradients' split-K partial slabs (dense.gemm_dw_slabs): each
     # of dW1, dW2 of a layer writes and re-reads `splits` [d x 512] fp32 slabs, summed
     # by hsg_slab_reduce (these bytes belong to the step's dense work)
     for kind, (rel, d_in, H, D, d) in layers.items():
@@ -245,12 +245,23 @@ def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False, issued=False):
 
 
 def dw_slab_splits(K, d, dh):
-    """Split-K factor dense.gemm_slabs uses for an FFN weight gradient of K rows
-    (1: not split), mirrored on the host for the byte count."""
+    """K slices of a layer's FFN weight-gradient pair over K rows, mirrored on the host
+    for the byte count: the product backward runs both gradients in one
+    hsg_gemm_dw_slabs launch with dense.gemm_dw_slabs' rule -- two blocks per CU over
+    the pair's tiles, at least 4 K tiles per slice, every slice non-empty -- and
+    falls back to dense.gemm_slabs' 64 slices only when that declines (1: not split)."""
+    from hetersumgraph_amd._lib import load
+    kt = (K + 31) // 32
+    tiles = load().hsg_gemm_dw_tiles(d, dh) + load().hsg_gemm_dw_tiles(dh, d)
+    splits = max(1, min(max(1, (2 * 256) // max(tiles, 1)), kt // 4))
+    per = (kt + splits - 1) // splits
+    splits = (kt + per - 1) // per
+    if splits >= 2:
+        return splits
     from hetersumgraph_amd.dense import auto_splits
     if auto_splits(d, dh, K) < 2:
         return 1
-    return max(2, min(int(os.environ.get("HSG_DW_SPLITS", "64")), (K + 31) // 32))
+    return max(2, min(64, kt))
 
 
 def full_stack_floor(items):
@@ -406,102 +417,73 @@ def cpu_baseline(docs, args, stack):
             "ms_per_step": dt * 1e3, "step_ms_all": [t * 1e3 for t in times]}
 
 
-def main():
-    args = parse()
-    # stdout carries exactly ONE JSON line (rank 0): anything libraries print there
-    # (RCCL's version banner at communicator init, for one) goes to stderr instead
-    sys.stdout.flush()
-    json_fd = os.dup(1)
-    os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # one rank per GPU; ranks beyond the visible devices share them (only for the
-    # single-GPU rehearsal of the multi-rank path with HSG_DIST_BACKEND=gloo)
-    ndev = max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local % ndev)
-    dev = torch.device("cuda", local % ndev)
-    # the data-parallel exchange runs whenever there is more than one rank; at one rank
-    # HSG_DP_REHEARSAL=1 runs it anyway over a world-size-1 group (the driver's N-GPU
-    # code path -- RCCL communicator, doc-weighted in-place all-reduce captured in the
-    # step graph -- exercised on one GPU; tests/test_gpu_rccl.py)
-    dp = world > 1 or os.environ.get("HSG_DP_REHEARSAL", "0") == "1"
-    backend = None
-    if dp:
-        import torch.distributed as dist
-        backend = os.environ.get("HSG_DIST_BACKEND", "nccl")       # nccl = RCCL over xGMI
-        kw = {"device_id": dev} if backend == "nccl" else {}
-        if world > 1:
-            dist.init_process_group(backend, **kw)
-        else:
-            import tempfile
-            fd, rdv = tempfile.mkstemp(prefix="hsg_rdv_")
-            os.close(fd)
-            os.unlink(rdv)
-            dist.init_process_group(backend, init_method=f"file://{rdv}", rank=0, world_size=1, **kw)
-    from hetersumgraph_amd import _lib
-    _lib.load()
-    from hetersumgraph_amd.dense import set_gemm_dtype
-    set_gemm_dtype(args.dtype)
+class HipBench:
+    """The measured path: the fused WSWGAT stack of libhsg.so on this rank's ROCm
+    device, captured into a HIP graph.  ``main`` drives it through these seams --
+    device, synchronisation, per-step events, the step itself and the in-step
+    kernel measurements -- so that the multi-rank driver logic (barriers, max over
+    ranks, the exchange, the JSON line, the CPU baseline on rank 0) is one code path
+    for every world size; tests/bench_cpu_worker.py replays that logic over gloo on
+    CPU with a stand-in step (test infrastructure, not a product path)."""
 
-    docs, G, E_global, frac = make_shard(args.config, rank, world, args.seed)
-    E_total = G.number_of_edges()
-    G.to(dev)
-    torch.manual_seed(args.seed)                       # identical replicas on every rank
-    stack = Stack(args.dropout, args.n_iter).to(dev).train()
-    rel_w, rel_s = G.relation("W2S"), G.relation("S2W")
-    gen = torch.Generator(device=dev).manual_seed(args.seed * 7 + rank)
-    Xw = 0.4 * torch.randn(rel_s.n_dst, 300, device=dev, generator=gen)      # word embeddings (frozen)
-    Xs = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen).requires_grad_()   # encoder output
-    R = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen)
-    params = [p for p in stack.parameters() if p.requires_grad]
+    graphs = True
+    data = "synthetic (seeded CNN/DM-shaped graphs, random-init weights of the reference architecture)"
 
-    from hetersumgraph_amd import rng as hsg_rng
+    def __init__(self, args, rank, world, local):
+        self.args, self.rank, self.world = args, rank, world
+        # one rank per GPU; ranks beyond the visible devices share them (only for the
+        # single-GPU rehearsal of the multi-rank path with HSG_DIST_BACKEND=gloo)
+        ndev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local % ndev)
+        self.dev = torch.device("cuda", local % ndev)
 
-    def step():
-        hsg_rng.advance_all()          # fresh dropout masks every step (device-side: replays too)
-        s = stack(G, Xw, Xs)
-        s.backward(R)                  # d/ds of sum(s * R): the upstream gradient of the stack output
+    def dist_kwargs(self, backend):
+        return {"device_id": self.dev} if backend == "nccl" else {}
 
-    def allreduce():
-        # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL.
-        # After the backward every gradient is final at once, so there is nothing to
-        # overlap with: ONE flat bucket (7 MB at cfg2) pays one collective latency
-        # instead of one per 2 MiB bucket (the eager train step overlaps its buckets
-        # with the backward instead: parallel.GradientReducer).  The fused stack writes
-        # every gradient into one flat buffer (stack._Grads), which is reduced in place:
-        # one scale pass + one all-reduce, no concatenation or copy-back -- and no host
-        # sync, so on RCCL it is captured into the step's graph
-        from hetersumgraph_amd.parallel import allreduce_gradients, flat_gradients, reduce_flat
-        flat = flat_gradients(params)
-        if flat is not None:
-            reduce_flat(flat, scale=frac)
-        else:
-            allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
+    def load(self):
+        from hetersumgraph_amd import _lib
+        _lib.load()
+        from hetersumgraph_amd.dense import set_gemm_dtype
+        set_gemm_dtype(self.args.dtype)
 
-    def zero():
-        # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
-        for p in params:
-            p.grad = None
-        Xs.grad = None
+    def synchronize(self):
+        torch.cuda.synchronize()
 
-    # eager warm-up (builds relation caches, allocator pools)
-    for _ in range(max(args.warmup, 2)):
-        zero()
-        step()
-        if dp:
-            allreduce()                # also the communicator's first collective, before any capture
-    torch.cuda.synchronize()
+    def events(self, n):
+        st = torch.cuda.current_stream(self.dev)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+        return lambda i: evs[i].record(st), lambda i, j: evs[i].elapsed_time(evs[j])
 
-    use_graph = not args.no_graph
-    graph = None
-    # RCCL collectives are capturable: the exchange joins the step's graph (one replay
-    # = step + exchange); gloo's are not, so a gloo rehearsal runs it eagerly after it
-    capture_exchange = dp and backend == "nccl" and os.environ.get("HSG_CAPTURE_EXCHANGE", "1") != "0"
+    def build(self, G, docs):
+        """(stack, step, zero, params): the timed unit on this rank's batch."""
+        args, dev = self.args, self.dev
+        G.to(dev)
+        torch.manual_seed(args.seed)                       # identical replicas on every rank
+        stack = Stack(args.dropout, args.n_iter).to(dev).train()
+        rel_w, rel_s = G.relation("W2S"), G.relation("S2W")
+        gen = torch.Generator(device=dev).manual_seed(args.seed * 7 + self.rank)
+        Xw = 0.4 * torch.randn(rel_s.n_dst, 300, device=dev, generator=gen)      # word embeddings (frozen)
+        Xs = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen).requires_grad_()   # encoder output
+        R = torch.randn(rel_w.n_dst, 64, device=dev, generator=gen)
+        params = [p for p in stack.parameters() if p.requires_grad]
+        from hetersumgraph_amd import rng as hsg_rng
 
-    def capture(with_exchange):
+        def step():
+            hsg_rng.advance_all()          # fresh dropout masks every step (device-side: replays too)
+            s = stack(G, Xw, Xs)
+            s.backward(R)                  # d/ds of sum(s * R): the upstream gradient of the stack output
+
+        def zero():
+            # optimizer.zero_grad() (set_to_none): backward then writes fresh gradients
+            for p in params:
+                p.grad = None
+            Xs.grad = None
+
+        self.rel_w, self.rel_s, self.n_typed = rel_w, rel_s, rel_w.n_typed
+        return stack, step, zero, params
+
+    def capture(self, step, zero, allreduce, with_exchange):
+        dev = self.dev
         s_side = torch.cuda.Stream(dev)
         s_side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s_side):
@@ -520,10 +502,148 @@ def main():
         torch.cuda.synchronize()
         return g
 
+    def kernel_report(self, stack, step, zero, ms_per_step):
+        """The roofline objects of the JSON line: the S2W edge forward (the north-star
+        kernel), every edge kernel of the step, the full-stack floor and the S2W FFN
+        GEMM, all timed after the timed region."""
+        args = self.args
+        rel_w, rel_s = self.rel_w, self.rel_s
+        # edge kernels timed inside eager steps (HIP events of their dispatches), after the
+        # timed region so they cannot perturb it
+        kt = time_edge_kernels_in_step(step, zero, args.kernel_steps)
+        Hs, Ds = stack.sent2word.layer.num_heads, stack.sent2word.layer.head_dim
+        Hw, Dw = stack.word2sent.layer.num_heads, stack.word2sent.layer.head_dim
+        shapes = {"S2W": (rel_s, Hs, Ds), "W2S": (rel_w, Hw, Dw)}
+        k_ms = kt[("gat_fwd", "S2W")][0]
+        k_bytes = edge_bytes_fwd(rel_s, Hs, Ds)
+        achieved = k_bytes / (k_ms * 1e-3) / 1e9
+        e_bytes = e_ms = 0.0
+        edge_rows = {}
+        for (what, kind), (ms, per_step) in sorted(kt.items()):
+            rel, H, D = shapes[kind]
+            b = (edge_bytes_fwd if what == "gat_fwd" else edge_bytes_bwd)(rel, H, D)
+            e_bytes += b * per_step
+            e_ms += ms * per_step
+            edge_rows[f"{what}_{kind}"] = {"avg_launch_us": ms * 1e3, "launches_per_step": per_step,
+                                           "bytes_per_launch": b, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        traffic, traffic_src, traffic_rec = pmc_traffic() if args.config == "cfg2" else (None, None, None)
+        items = step_work(rel_w, rel_s, args.n_iter, args.dtype)
+        floor_s, edge_floor_s, dense_floor_s, gflop = full_stack_floor(items)
+        floor_i, _, dense_floor_i, _ = full_stack_floor(step_work(rel_w, rel_s, args.n_iter, args.dtype, issued=True))
+        d_ms, d_flops, d_name = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
+        d_tf = d_flops / (d_ms * 1e-3) / 1e12
+        rep = {
+            "roofline": {"kernel": "hsg_gat_fwd (S2W: sentence->word, H=6 x D=50)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": k_bytes,
+                         "bytes_formula": "SURVEY 8(d) B_f = 4 n_src (HD+H) + 8 n_dst + 4 + 5 E_T + 4 n_dst (HD+2H)",
+                         "epilogue_bytes_per_launch": epilogue_bytes_fwd(rel_s, Hs, Ds),
+                         "avg_launch_us": k_ms * 1e3,
+                         "timing": f"HIP events recorded by the kernel's own dispatch packet on its stream "
+                                   f"(hipExtLaunchKernel) inside {args.kernel_steps} eager training steps "
+                                   "(in-step cache state); cross-check: rocprofv3 kernel trace of the same "
+                                   "command under profiles/"},
+            "edge_aggregate": {"bytes_per_step": e_bytes, "time_us_per_step": e_ms * 1e3,
+                               "achieved": e_bytes / (e_ms * 1e-3) / 1e9, "unit": "GB/s",
+                               "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernels": edge_rows},
+            "full_stack": {"floor_us": floor_s * 1e6, "edge_floor_us": edge_floor_s * 1e6,
+                           "dense_floor_us": dense_floor_s * 1e6, "dense_gflop_per_step": gflop,
+                           "frac": floor_s / (ms_per_step * 1e-3),
+                           "formula": "sum_k max(B_k/8 TB/s, F_k/peak_k) / t_step over the step's edge, head-"
+                                      "projection and FFN work (bench.step_work)",
+                           "floor_issued_us": floor_i * 1e6, "dense_floor_issued_us": dense_floor_i * 1e6,
+                           "frac_issued": floor_i / (ms_per_step * 1e-3),
+                           "frac_issued_is": "the same floor with the dense work priced at the rate the path issues "
+                                             "it: the fp32-accurate GEMMs as 6 bf16 limb products each at the bf16 "
+                                             "MFMA peak (2.5 PF/s), i.e. 417 TF/s fp32-equivalent, the exact-f32 "
+                                             "kernels (head projection, narrow FFN) at 157 TF/s"},
+            "roofline_dense": dense_roofline(d_name, rel_s.n_dst, d_tf, d_flops, d_ms, args.dtype),
+        }
+        if traffic_rec is not None:
+            rep["roofline"]["traffic_detail"] = {k: traffic_rec[k] for k in ("fetch_bytes", "write_bytes", "launches")
+                                                 if k in traffic_rec}
+        return rep
+
+    def e2e(self, G):
+        dt = time_train_step(G, self.args.config, self.args.n_iter, self.args.e2e_steps, 3, self.dev)
+        return {"value": G.number_of_edges() / dt, "unit": "graph-edges/s", "ms_per_step": dt * 1e3,
+                "steps": self.args.e2e_steps,
+                "what": "whole train.py iteration (HiGraph forward incl. CNN+LSTM sentence encoder, "
+                        "cross-entropy, backward, Adam; eager, 1 GPU)"}
+
+
+def main(backend_cls=HipBench):
+    args = parse()
+    # stdout carries exactly ONE JSON line (rank 0): anything libraries print there
+    # (RCCL's version banner at communicator init, for one) goes to stderr instead
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    be = backend_cls(args, rank, world, local)
+    # the data-parallel exchange runs whenever there is more than one rank; at one rank
+    # HSG_DP_REHEARSAL=1 runs it anyway over a world-size-1 group (the driver's N-GPU
+    # code path -- RCCL communicator, doc-weighted in-place all-reduce captured in the
+    # step graph -- exercised on one GPU; tests/test_gpu_rccl.py)
+    dp = world > 1 or os.environ.get("HSG_DP_REHEARSAL", "0") == "1"
+    backend = None
+    if dp:
+        import torch.distributed as dist
+        backend = os.environ.get("HSG_DIST_BACKEND", "nccl")       # nccl = RCCL over xGMI
+        kw = be.dist_kwargs(backend)
+        if world > 1:
+            dist.init_process_group(backend, **kw)
+        else:
+            import tempfile
+            fd, rdv = tempfile.mkstemp(prefix="hsg_rdv_")
+            os.close(fd)
+            os.unlink(rdv)
+            dist.init_process_group(backend, init_method=f"file://{rdv}", rank=0, world_size=1, **kw)
+    be.load()
+
+    docs, G, E_global, frac = make_shard(args.config, rank, world, args.seed)
+    E_total = G.number_of_edges()
+    stack, step, zero, params = be.build(G, docs)
+
+    def allreduce():
+        # the data-parallel exchange: the doc-weighted gradient all-reduce over RCCL.
+        # After the backward every gradient is final at once, so there is nothing to
+        # overlap with: ONE flat bucket (7 MB at cfg2) pays one collective latency
+        # instead of one per 2 MiB bucket (the eager train step overlaps its buckets
+        # with the backward instead: parallel.GradientReducer).  The fused stack writes
+        # every gradient into one flat buffer (stack._Grads), which is reduced in place:
+        # one scale pass + one all-reduce, no concatenation or copy-back -- and no host
+        # sync, so on RCCL it is captured into the step's graph
+        from hetersumgraph_amd.parallel import allreduce_gradients, flat_gradients, reduce_flat
+        flat = flat_gradients(params)
+        if flat is not None:
+            reduce_flat(flat, scale=frac)
+        else:
+            allreduce_gradients(params, scale=frac, bucket_bytes=1 << 30)
+
+    # eager warm-up (builds relation caches, allocator pools)
+    for _ in range(max(args.warmup, 2)):
+        zero()
+        step()
+        if dp:
+            allreduce()                # also the communicator's first collective, before any capture
+    be.synchronize()
+
+    use_graph = not args.no_graph and be.graphs
+    graph = None
+    # RCCL collectives are capturable: the exchange joins the step's graph (one replay
+    # = step + exchange); gloo's are not, so a gloo rehearsal runs it eagerly after it
+    capture_exchange = dp and backend == "nccl" and os.environ.get("HSG_CAPTURE_EXCHANGE", "1") != "0"
     if use_graph:
         for attempt in ((True, False) if capture_exchange else (False,)):
             try:
-                graph = capture(attempt)
+                graph = be.capture(step, zero, allreduce, attempt)
                 capture_exchange = attempt
                 break
             except Exception as exc:  # pragma: no cover - reported on stderr and in the JSON
@@ -551,25 +671,26 @@ def main():
     if dp:
         import torch.distributed as dist
         dist.barrier()
-    torch.cuda.synchronize()
-    # one HIP event after every step on the launching stream: the per-step times give
-    # the median (t_step is the median); the contract's value stays the
-    # timed region's mean (K steps between barrier + synchronize)
-    st_main = torch.cuda.current_stream(dev)
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    be.synchronize()
+    # one event after every step on the launching stream: the per-step times give the
+    # median (t_step is the median); the contract's value stays the timed
+    # region's mean (K steps between barrier + synchronize)
+    mark, between = be.events(args.steps + 1)
     t0 = time.perf_counter()
-    evs[0].record(st_main)
+    mark(0)
     for i in range(args.steps):
         run_one()
-        evs[i + 1].record(st_main)
-    torch.cuda.synchronize()
+        mark(i + 1)
+    be.synchronize()
     if dp:
         dist.barrier()
     dt = time.perf_counter() - t0
-    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    step_ms = [between(i, i + 1) for i in range(args.steps)]
     med_ms = float(np.median(step_ms))
     if dp:
-        t = torch.tensor([dt, med_ms], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt, med_ms], dtype=torch.float64)
+        if backend == "nccl":
+            t = t.to(be.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, med_ms = float(t[0].item()), float(t[1].item())
     ms_per_step = dt / args.steps * 1e3
@@ -580,31 +701,7 @@ def main():
                     else "bucketed all-reduce (concatenated copies)")
                    + (", captured in the step's HIP graph" if capture_exchange else ", eager after each step")
                    + f" ({backend}, world {world})")
-
-    # edge kernels timed inside eager steps (HIP events of their dispatches), after the
-    # timed region so they cannot perturb it
-    kt = time_edge_kernels_in_step(step, zero, args.kernel_steps)
-    Hs, Ds = stack.sent2word.layer.num_heads, stack.sent2word.layer.head_dim
-    Hw, Dw = stack.word2sent.layer.num_heads, stack.word2sent.layer.head_dim
-    shapes = {"S2W": (rel_s, Hs, Ds), "W2S": (rel_w, Hw, Dw)}
-    k_ms = kt[("gat_fwd", "S2W")][0]
-    k_bytes = edge_bytes_fwd(rel_s, Hs, Ds)
-    achieved = k_bytes / (k_ms * 1e-3) / 1e9
-    e_bytes = e_ms = 0.0
-    edge_rows = {}
-    for (what, kind), (ms, per_step) in sorted(kt.items()):
-        rel, H, D = shapes[kind]
-        b = (edge_bytes_fwd if what == "gat_fwd" else edge_bytes_bwd)(rel, H, D)
-        e_bytes += b * per_step
-        e_ms += ms * per_step
-        edge_rows[f"{what}_{kind}"] = {"avg_launch_us": ms * 1e3, "launches_per_step": per_step,
-                                       "bytes_per_launch": b, "frac": b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-    traffic, traffic_src, traffic_rec = pmc_traffic() if args.config == "cfg2" else (None, None, None)
-    items = step_work(rel_w, rel_s, args.n_iter, args.dtype)
-    floor_s, edge_floor_s, dense_floor_s, gflop = full_stack_floor(items)
-    floor_i, _, dense_floor_i, _ = full_stack_floor(step_work(rel_w, rel_s, args.n_iter, args.dtype, issued=True))
-    d_ms, d_flops, d_name = time_dense_kernel(stack, rel_s.n_dst, args.kernel_reps)
-    d_tf = d_flops / (d_ms * 1e-3) / 1e12
+    rep = be.kernel_report(stack, step, zero, ms_per_step)
 
     out = {
         "metric": "graph-edges/sec through WSWGAT fwd+bwd, CNN/DM-shaped batch; 1/2/4/8 GPU",
@@ -623,60 +720,36 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (seeded CNN/DM-shaped graphs, random-init weights of the reference architecture)",
+        "data": be.data,
         "config": {"workload": f"{args.config}: HSG WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) fwd+bwd, "
                                f"train mode, {workload_shape(args.config)}",
                    "gemm_operands": args.dtype,
                    "edge_kernels_ln_head_projection": "f32",
                    "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
-                   "typed_edges_per_direction": rel_w.n_typed,
+                   "typed_edges_per_direction": be.n_typed,
                    "dropout": args.dropout, "parallelism": f"dp{world}", "dp_exchange": dp_exchange,
                    "hip_graph": bool(use_graph)},
-        "roofline": {"kernel": "hsg_gat_fwd (S2W: sentence->word, H=6 x D=50)", "bound": "hbm",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": k_bytes,
-                     "bytes_formula": "SURVEY 8(d) B_f = 4 n_src (HD+H) + 8 n_dst + 4 + 5 E_T + 4 n_dst (HD+2H)",
-                     "epilogue_bytes_per_launch": epilogue_bytes_fwd(rel_s, Hs, Ds),
-                     "avg_launch_us": k_ms * 1e3,
-                     "timing": f"HIP events recorded by the kernel's own dispatch packet on its stream "
-                               f"(hipExtLaunchKernel) inside {args.kernel_steps} eager training steps "
-                               "(in-step cache state); cross-check: rocprofv3 kernel trace of the same "
-                               "command under profiles/"},
-        "edge_aggregate": {"bytes_per_step": e_bytes, "time_us_per_step": e_ms * 1e3,
-                           "achieved": e_bytes / (e_ms * 1e-3) / 1e9, "unit": "GB/s",
-                           "frac": e_bytes / (e_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "kernels": edge_rows},
-        "full_stack": {"floor_us": floor_s * 1e6, "edge_floor_us": edge_floor_s * 1e6,
-                       "dense_floor_us": dense_floor_s * 1e6, "dense_gflop_per_step": gflop,
-                       "frac": floor_s / (ms_per_step * 1e-3),
-                       "formula": "sum_k max(B_k/8 TB/s, F_k/peak_k) / t_step over the step's edge, head-"
-                                  "projection and FFN work (bench.step_work)",
-                       "floor_issued_us": floor_i * 1e6, "dense_floor_issued_us": dense_floor_i * 1e6,
-                       "frac_issued": floor_i / (ms_per_step * 1e-3),
-                       "frac_issued_is": "the same floor with the dense work priced at the rate the path issues "
-                                         "it: the fp32-accurate GEMMs as 6 bf16 limb products each at the bf16 "
-                                         "MFMA peak (2.5 PF/s), i.e. 417 TF/s fp32-equivalent, the exact-f32 "
-                                         "kernels (head projection, narrow FFN) at 157 TF/s"},
-        "roofline_dense": dense_roofline(d_name, rel_s.n_dst, d_tf, d_flops, d_ms, args.dtype),
     }
-    if traffic_rec is not None:
-        out["roofline"]["traffic_detail"] = {k: traffic_rec[k] for k in ("fetch_bytes", "write_bytes", "launches")
-                                             if k in traffic_rec}
+    out.update(rep)
     if world == 1 and not args.no_e2e:
         try:
-            dt = time_train_step(G, args.config, args.n_iter, args.e2e_steps, 3, dev)
-            out["e2e_train_step"] = {
-                "value": E_total / dt, "unit": "graph-edges/s", "ms_per_step": dt * 1e3, "steps": args.e2e_steps,
-                "what": "whole train.py iteration (HiGraph forward incl. CNN+LSTM sentence encoder, "
-                        "cross-entropy, backward, Adam; eager, 1 GPU)"}
+            out["e2e_train_step"] = be.e2e(G)
         except Exception as exc:  # pragma: no cover - reported in the JSON
             out["e2e_train_step"] = {"error": repr(exc)}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    # the CPU baseline (every GPU count beside the CPU number) on rank 0 only,
+    # after the timed region and the kernel timings, on rank 0's own shard -- the same
+    # per-GPU workload at every world size; the other ranks wait at a barrier
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(docs, args, stack)
         except Exception as exc:  # pragma: no cover
             out["cpu_baseline"] = {"error": repr(exc)}
+        if world > 1:
+            out["cpu_baseline"]["sample"] = out["cpu_baseline"].get("sample", "") + (
+                f"; rank 0's shard of the {world}-rank job, timed on rank 0's host cores after the timed "
+                "region while the other ranks waited at a barrier")
+    if dp:
+        dist.barrier()
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

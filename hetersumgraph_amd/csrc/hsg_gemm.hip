@@ -741,14 +741,18 @@ __device__ __forceinline__ void split_rne8(const f32x4 x, const f32x4 y, bf16x8 
     u32x4 w0, w1, w2;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
+        // the low element is unpacked by a byte permute, (a & 0xffff) << 16: written as a
+        // shift, the compiler saw through it and re-converted that element alone
+        // (v_cvt_pk_bf16_f32 x, 0) -- 16 extra VALU per k_gemm7 K tile beside 48 MFMAs
+        // that are vector-issue-bound already
         const unsigned a = __builtin_bit_cast(unsigned, bf16x2v{(__bf16)v[2 * p], (__bf16)v[2 * p + 1]});
         w0[p] = a;
         float ra, rb, sa, sb;
-        asm("v_sub_f32 %0, %1, %2" : "=v"(ra) : "v"(v[2 * p]), "v"(__uint_as_float(a << 16)));
+        asm("v_sub_f32 %0, %1, %2" : "=v"(ra) : "v"(v[2 * p]), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, a, 0x01000c0cu))));
         asm("v_sub_f32 %0, %1, %2" : "=v"(rb) : "v"(v[2 * p + 1]), "v"(__uint_as_float(a & 0xFFFF0000u)));
         const unsigned b = __builtin_bit_cast(unsigned, bf16x2v{(__bf16)ra, (__bf16)rb});
         w1[p] = b;
-        asm("v_sub_f32 %0, %1, %2" : "=v"(sa) : "v"(ra), "v"(__uint_as_float(b << 16)));
+        asm("v_sub_f32 %0, %1, %2" : "=v"(sa) : "v"(ra), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, b, 0x01000c0cu))));
         asm("v_sub_f32 %0, %1, %2" : "=v"(sb) : "v"(rb), "v"(__uint_as_float(b & 0xFFFF0000u)));
         w2[p] = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
     }
@@ -1273,7 +1277,11 @@ typedef float f32x4v7 __attribute__((ext_vector_type(4)));
 // PM: 0 = fp32-accurate (RNE 3-limb split, six products), 1 = the same with the
 // truncation split (dev), 2 = bf16 mode (hsg_gemm_bf16 semantics: A and the weight
 // rounded to bf16 RNE, ONE product: only limb plane 0 of the weight is staged)
-template <int BN, int S, int PM = 0, int OCC = 2>
+// SA: the DMA sources as a wave-uniform base pointer (advanced by 32 k per tile, SGPRs)
+// plus per-lane 32-bit byte offsets computed once (row clamps, swizzles, limb rows), so
+// the K loop issues the saddr form of global_load_lds with no per-tile address VALU;
+// only a tile reaching past K takes the per-chunk zero-page select.
+template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false>
 __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
     constexpr int A_FL = BM * 32;                          // floats of the A tile
@@ -1304,9 +1312,54 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
     EpiRows<BN> ep;
 
+    uint32_t aoff[BM / 32], boff[NBP];
+    if constexpr (SA) {
+#pragma unroll
+        for (int pc = 0; pc < BM / 32; ++pc) {
+            const int r = (pc * 4 + wid) * 8 + (lane >> 3);
+            aoff[pc] = ((uint32_t)min(m0 + r, p.M - 1) * (uint32_t)p.lda + 4u * ((lane & 7) ^ swz16(r))) * 4u;
+        }
+#pragma unroll
+        for (int pc = 0; pc < NBP; ++pc) {
+            const int piece = min(pc * 4 + wid, NL * BPC - 1);
+            const int limb = piece / BPC, r = (piece % BPC) * 16 + (lane >> 2);
+            boff[pc] = ((uint32_t)(limb * Np + n0 + r) * (uint32_t)Kp + 8u * ((lane & 3) ^ bswz16(r))) * 2u;
+        }
+    }
     auto issue = [&](int it) {
         float *st = lds + (it % S) * STAGE_FL;
         const int k0 = it * 32;
+        if constexpr (SA) {
+            const char *ab = reinterpret_cast<const char *>(p.A) + (size_t)k0 * 4;
+            const char *bb = reinterpret_cast<const char *>(planes) + (size_t)k0 * 2;
+            __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
+            if (k0 + 32 <= p.K) {                                 // wave-uniform: no K-tail chunk
+#pragma unroll
+                for (int pc = 0; pc < BM / 32; ++pc)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(ab + aoff[pc]),
+                                                     (__attribute__((address_space(3))) void *)(st + (pc * 4 + wid) * 256),
+                                                     16, 0, 0);
+            } else {
+#pragma unroll
+                for (int pc = 0; pc < BM / 32; ++pc) {
+                    const int r = (pc * 4 + wid) * 8 + (lane >> 3);
+                    const bool in = k0 + 4 * ((lane & 7) ^ swz16(r)) < p.K;
+                    const void *src = in ? (const void *)(ab + aoff[pc]) : (const void *)g_zero16;
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                     (__attribute__((address_space(3))) void *)(st + (pc * 4 + wid) * 256),
+                                                     16, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int pc = 0; pc < NBP; ++pc) {
+                const int piece = min(pc * 4 + wid, NL * BPC - 1);
+                const int limb = piece / BPC, prow = (piece % BPC) * 16;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(bb + boff[pc]),
+                                                 (__attribute__((address_space(3))) void *)(sb + limb * B_BF + prow * 32),
+                                                 16, 0, 0);
+            }
+            return;
+        }
         if constexpr (!NOA) glds_tile<BM, true>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
         __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
 #pragma unroll
@@ -1409,14 +1462,15 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     if (p.colpart) epi_rows_colpart<BN>(lds, cs, wid, lane, ty, n0, p);
 }
 
-template <int BN, int S, int PM = 0, int OCC = 2>
+template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false>
 int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
     p.k_tiles_per_split = Kp / 32;
     if ((p.N + BN - 1) / BN * BN > Np) return HSG_EINVAL;   // B tile rows must exist in the planes
     if (!epi_rows_ok(p)) return HSG_EINVAL;                 // the float4 epilogue needs whole aligned quads
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
-    hipLaunchKernelGGL((k_gemm7<BN, S, PM, OCC>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
+    if (SA && ((long)p.M * p.lda * 4 >= (1L << 32) || (long)3 * Np * Kp * 2 >= (1L << 32))) return HSG_EINVAL;
+    hipLaunchKernelGGL((k_gemm7<BN, S, PM, OCC, SA>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -2497,6 +2551,9 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 36 && epi_rows_ok(p)) return launch7<64, 2, 6>(p, pl, Np, Kp, st);   // dev: loads only
     if (plan == 37 && epi_rows_ok(p)) return launch7<64, 2, 7>(p, pl, Np, Kp, st);   // dev: A loads only
     if (plan == 38 && epi_rows_ok(p)) return launch7<64, 2, 8>(p, pl, Np, Kp, st);   // dev: B loads only
+    if (plan == 40 && epi_rows_ok(p)) return launch7<64, 2, 0, 2, true>(p, pl, Np, Kp, st);   // hoisted DMA offsets
+    if (plan == 41 && epi_rows_ok(p))                       // + 80-wide tiles for N <= 320
+        return N <= 320 ? launch7<80, 2, 0, 2, true>(p, pl, Np, Kp, st) : launch7<64, 2, 0, 2, true>(p, pl, Np, Kp, st);
     if (plan != 27) return launch5<64, 2>(p, pl, Np, Kp, st);
     if (gemm11_on()) {
         // one round of big tiles (k_gemm11, dev opt-in: measured slower)

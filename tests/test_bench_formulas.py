@@ -41,10 +41,14 @@ def test_full_stack_floor(cfg2_rels):
     assert 74 <= gflop <= 80
     assert 0.45e-3 <= dense <= 0.54e-3          # incl. the ~20 us of split-K slab bytes
     assert abs(edge - 207.1e6 / 8e12) < 1e-7
-    # the S2W weight gradients' split-K slabs: 64 x [300 x 512] fp32 per weight, each
-    # written and read once (dense.gemm_slabs)
+    # the weight gradients' split-K slabs, each written and read once, at the
+    # slice counts of the one-launch pair (dense.gemm_dw_slabs): S2W 32 x
+    # [300 x 512] per weight (16 tiles, two blocks per CU), W2S 21 x [64 x 512] (8 tiles:
+    # 64 slices capped at 4 K tiles each over its 105, then made non-empty)
     slabs = {n: b for n, b, _, _ in items if n.startswith("ffn_dw_slabs")}
-    assert round(slabs["ffn_dw_slabs_S2W"] / 1e6, 1) == round(2 * 2 * 4 * 64 * 300 * 512 / 1e6, 1)
+    assert bench.dw_slab_splits(38400, 300, 512) == 32 and bench.dw_slab_splits(3360, 64, 512) == 21
+    assert round(slabs["ffn_dw_slabs_S2W"] / 1e6, 1) == round(2 * 2 * 4 * 32 * 300 * 512 / 1e6, 1)
+    assert round(slabs["ffn_dw_slabs_W2S"] / 1e6, 1) == round(2 * 2 * 4 * 21 * 64 * 512 / 1e6, 1)
 
 
 def test_dense_roofline_peak_follows_the_path():

@@ -17,6 +17,7 @@
 #   benchprof               rocprofv3 --kernel-trace --stats over bench.py (trace/, bench_prof.json)
 #   bench                   the default bench line (bench.json)
 #   bench=<args>            bench.py with extra arguments, '+' for spaces (bench_<n>.json)
+#   cfgs                    bench lines of every single-GPU configuration, f32 and bf16 (cfgs/)
 set -e
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -78,6 +79,12 @@ for step in "$@"; do
     bench=*)
       nb=$((nb + 1))
       timeout -k 10 400 python -u bench.py $(echo ${step#bench=} | tr '+' ' ') > $OUT/bench_$nb.json 2> $OUT/bench_$nb.err ;;
+    cfgs)
+      mkdir -p $OUT/cfgs
+      for c in "cfg2 f32" "cfg2 bf16" "cfg4 f32" "cfg4 bf16" "cfg5 f32" "cfg5 bf16"; do
+        set -- $c
+        timeout -k 10 240 python -u bench.py --config $1 --dtype $2 --no-cpu-baseline > $OUT/cfgs/bench_$1_$2.json 2> $OUT/cfgs/bench_$1_$2.err
+      done ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
