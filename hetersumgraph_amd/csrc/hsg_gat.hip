@@ -1933,8 +1933,14 @@ int hsg_gat_bwd_src(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
 // the two shapes of the one-pass edge backward: wide heads over long CSC segments
 // (S2W; rho as 64-column-group partials) and D = 8 heads over short ones (W2S: the
 // head-lane kernel; rho per head)
+// the one-pass wide kernel splits each source's out-edges over a block's 4 waves; it
+// takes any segment length, so it stands in for the dst + src pair from a mean CSC
+// segment of 4 on (cfg5's 14 words per sentence ran the two-pass backward while the
+// condition was the 16 of the 4-wave forward / dst passes: 42 vs ~17 us per S2W
+// application)
 bool srcg_wide(const hsg_rel *rel, int H, int D) {
-    return D >= 32 && D <= 64 && src_wpn(rel) == 4 && (D + lanes_per_head(H) - 1) / lanes_per_head(H) <= 8;
+    return D >= 32 && D <= 64 && rel->n_src > 0 && rel->n_edges >= 4 * rel->n_src &&
+           (D + lanes_per_head(H) - 1) / lanes_per_head(H) <= 8;
 }
 bool srcg_narrow(const hsg_rel *rel, int H, int D) { return D == 8 && H <= 8 && src_wpn(rel) == 1; }
 
@@ -1954,7 +1960,7 @@ int hsg_gat_bwd_src_g_blocks(const hsg_rel *rel, int H, int D) {
         const int b = (groups + HSG_WAVES - 1) / HSG_WAVES;
         return b < 1 ? 1 : (b < kBwdSrcGridCap ? b : kBwdSrcGridCap);
     }
-    return hsg_gat_bwd_src_blocks(rel);
+    return grid_nodes(rel->n_src, 4, kBwdSrcGridCap);        // one source per block per iteration
 }
 
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,

@@ -896,17 +896,26 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
         stash();
         __syncthreads();
         if (r0 + 32 < rend) fetch(r0 + 32);
+        // the step's mask words in registers; the keep bit of row rr is one v_bfe_i32
+        // (0 or -1) and a v_and on the X value -- the select form cost a shift, an and,
+        // a compare and a v_cndmask per MFMA (plus s_nop pads before the MFMA reading it)
+        uint32_t mq[SL];
+#pragma unroll
+        for (int q = 0; q < SL; ++q) mq[q] = Ms[q][col];
 #pragma unroll
         for (int s4 = 0; s4 < 32; s4 += 4) {
             const int rr = s4 + lk;
-            const float xv = Xs[rr][col];
+            const uint32_t xv = __float_as_uint(Xs[rr][col]);
             // slots past NS were staged as zeros: no branch around the MFMAs (a
             // conditional MFMA makes the compiler shuffle accumulators)
+            float a[SL], b[SL];
 #pragma unroll
             for (int q = 0; q < SL; ++q) {
-                const float a = ((Ms[q][col] >> rr) & 1u) ? xv : 0.f;
-                acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Zs[rr][q * ZS + li], acc[q], 0, 0, 0);
+                a[q] = __uint_as_float(xv & (uint32_t)__builtin_amdgcn_sbfe((int)mq[q], rr, 1));
+                b[q] = Zs[rr][q * ZS + li];
             }
+#pragma unroll
+            for (int q = 0; q < SL; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[q], b[q], acc[q], 0, 0, 0);
         }
     }
     // D: col = lane & 15 -> slot output j, row = (lane >> 4) * 4 + r -> input column
@@ -921,6 +930,150 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
         for (int r = 0; r < 4; ++r) {
             const int gc = c0 + wv * 16 + lk * 4 + r;
             if (gc < in) part[base + (long)(k * D + j) * in + gc] = acc[q][r];
+        }
+    }
+}
+
+// ------------------------------------------------- dW, narrow heads, 4x4x1 ----
+// (round 5) Heads of D % 4 == 0 with H * D <= 64 (the W2S projection: 8 heads x 8) on
+// v_mfma_f32_4x4x1_16b_f32: 16 independent 4 x 4 outer products per instruction, K = 1
+// row.  Block b of the instruction is the output quad (W rows 4b .. 4b + 3, i.e. one
+// head k_b = 4b / D, columns c .. c + 3): A[i] at lane 4b + i = keep(r, k_b, c + i) *
+// X[r, c + i], B[j] at lane 4b + j = dZ[r, 4b + j] = dZ[r, lane], so one instruction
+// is 64 W rows x 4 columns x 1 row with nothing padded -- the 16x16x4 kernel above
+// pads each 8-wide head to a 16-wide slot (half its MFMA work is zeros) and spends
+// three VALU + two s_nop per MFMA on the mask.  Here the keep bit is one v_bfe_i32 +
+// v_and per MFMA lane value.  D[i][j] lands in register i of lane 4b + j: lane l
+// accumulates W row l, four columns per quad -> one 16-byte store per quad.
+// Per wave M4Q column quads; per block M4W waves (M4W * M4Q * 4 columns) and a chunk of
+// rows in 32-row steps (the keep-mask word granularity).  Per step the block stages
+// X[32 rows][block columns] transposed (Xt[column][row], 4-row groups XOR-swizzled by
+// the column quad so the transposing dword stores spread over the banks; a lane's
+// 4-row A values are one ds_read_b128) and dZ[32][64] (zero past H * D); the next
+// step's global loads are issued before this step's MFMAs.  The chunk's partial slab
+// part[chunk][H*D][in] is the contract of k_hproj_dw (hsg_slab_reduce / k_sum_parts).
+constexpr int M4Q = 5, M4W = 5;                   // 5 waves x 5 quads = 100 columns per block
+constexpr int M4C = M4W * M4Q * 4, M4XS = 36;     // block columns; Xt column stride (floats)
+
+struct DwM4Geom {
+    int ctiles, chunks, rows;
+};
+
+// measured slower than the 16x16x4 kernel (36.1 vs 25.2 us per cfg2 W2S launch in the
+// step): with the keep bit on the A value, each 4x4x1 MFMA (11 cycles alone) costs 27
+// cycles per wave (tools/census/mfma_rate_probe.hip), i.e. the two mask VALU per 256
+// MACs outweigh the padding the 16x16x4 form wastes.  Dev opt-in (HSG_HPROJ_DWM4=1).
+bool dw_m4_shape(int in, int H, int D) {
+    const char *e = HSG_DEV_ENV("HSG_HPROJ_DWM4");
+    return e && atoi(e) == 1 && D % 4 == 0 && H * D <= 64 && in % 4 == 0;
+}
+
+DwM4Geom dw_m4_geom(int n, int in) {
+    DwM4Geom g;
+    g.ctiles = (in + M4C - 1) / M4C;
+    int per = 4;                                          // 32-row steps per chunk (128 rows)
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_DWM4_STEPS")) per = atoi(e) > 0 ? atoi(e) : per;   // dev sweep
+    const int steps = (n + 31) / 32 > 0 ? (n + 31) / 32 : 1;
+    if (per > steps) per = steps;
+    g.rows = per * 32;
+    g.chunks = (steps + per - 1) / per;
+    return g;
+}
+
+__global__ __launch_bounds__(64 * M4W) void k_hproj_dw_m4(int n, int in, int H, int D, int rows_per_chunk,
+                                                        const float *__restrict__ dZ, int ldz,
+                                                        const float *__restrict__ X, int ldx,
+                                                        const uint32_t *__restrict__ bits, float *__restrict__ part) {
+    constexpr int NT = 64 * M4W;
+    constexpr int XQ = M4C / 4;                           // column quads per block row
+    constexpr int NXL = (32 * XQ + NT - 1) / NT;          // X float4 loads per thread per step
+    constexpr int NZL = (32 * 16 + NT - 1) / NT;          // dZ float4 loads per thread per step
+    __shared__ __attribute__((aligned(16))) float Xt[M4C][M4XS];
+    __shared__ __attribute__((aligned(16))) float Zs[32][64];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int HD = H * D, NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int cb = blockIdx.x * M4C, cw = wv * M4Q * 4;  // block / wave column offsets
+    const int rb = blockIdx.y * rows_per_chunk;
+    const int rend = min(rb + rows_per_chunk, n);
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    const int i4 = lane & 3, kb = min(lane & ~3, HD - 1) / D;   // A index, head of the lane's block
+    u32x4v xg[NXL], zg[NZL];
+    uint32_t mw[M4Q], mn[M4Q];
+    auto fetch = [&](int r0) {
+#pragma unroll
+        for (int v = 0; v < NXL; ++v) {
+            const int u = tid + NT * v, row = u / XQ, cq = u % XQ, col = cb + 4 * cq;
+            const bool ok = u < 32 * XQ && r0 + row < rend && col < in;
+            xg[v] = bld4(rX, ok ? (uint32_t)((r0 + row) * ldx + col) * 4 : kOOB);
+        }
+#pragma unroll
+        for (int v = 0; v < NZL; ++v) {
+            const int u = tid + NT * v, row = u >> 4, c4 = (u & 15) * 4;
+            const bool ok = u < 32 * 16 && r0 + row < rend && c4 < HD;
+            zg[v] = bld4(rZ, ok ? (uint32_t)((r0 + row) * ldz + c4) * 4 : kOOB);
+        }
+#pragma unroll
+        for (int q = 0; q < M4Q; ++q) {
+            const int col = cb + cw + 4 * q + i4;
+            mn[q] = bldu(rM, col < in ? (uint32_t)((kb * NWI + r0 / 32) * LDC + col) * 4 : kOOB);
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int v = 0; v < NXL; ++v) {
+            const int u = tid + NT * v, row = u / XQ, cq = u % XQ;
+            if (u < 32 * XQ) {
+                const int pos = (((row >> 2) ^ (cq & 7)) << 2) | (row & 3);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) Xt[4 * cq + e][pos] = __uint_as_float(xg[v][e]);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < NZL; ++v) {
+            const int u = tid + NT * v;
+            if (u < 32 * 16) *reinterpret_cast<u32x4v *>(&Zs[u >> 4][(u & 15) * 4]) = zg[v];
+        }
+    };
+    f32x4v acc[M4Q];
+#pragma unroll
+    for (int q = 0; q < M4Q; ++q) acc[q] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    if (rb < rend) fetch(rb);
+    for (int r0 = rb; r0 < rend; r0 += 32) {
+        __syncthreads();                                   // every wave is done with the last step
+        stash();
+#pragma unroll
+        for (int q = 0; q < M4Q; ++q) mw[q] = mn[q];
+        __syncthreads();
+        if (r0 + 32 < rend) fetch(r0 + 32);
+#pragma unroll
+        for (int g = 0; g < 8; ++g) {                      // 4-row groups
+            f32x4v xq[M4Q];
+#pragma unroll
+            for (int q = 0; q < M4Q; ++q) {
+                const int cl = cw + 4 * q + i4, cq = (cw >> 2) + q;
+                xq[q] = *reinterpret_cast<const f32x4v *>(&Xt[cl][(g ^ (cq & 7)) << 2]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int rr = 4 * g + e;
+                const float bz = Zs[rr][lane];
+#pragma unroll
+                for (int q = 0; q < M4Q; ++q) {
+                    const int keep = __builtin_amdgcn_sbfe((int)mw[q], rr, 1);   // 0 or -1
+                    const float a = __uint_as_float(__float_as_uint(xq[q][e]) & (uint32_t)keep);
+                    acc[q] = __builtin_amdgcn_mfma_f32_4x4x1f32(a, bz, acc[q], 0, 0, 0);
+                }
+            }
+        }
+    }
+    if (lane < HD) {
+        float *dst = part + (long)blockIdx.y * HD * in + (long)lane * in;
+#pragma unroll
+        for (int q = 0; q < M4Q; ++q) {
+            const int col = cb + cw + 4 * q;
+            if (col < in) *reinterpret_cast<f32x4v *>(dst + col) = acc[q];
         }
     }
 }
@@ -1187,7 +1340,7 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
 
 int hsg_hproj_dw_chunks(int n, int in, int H, int D) {
     if (n < 0 || in < 1 || H < 1 || D < 1) return 0;
-    return dw_geom(n, in, H, D).chunks;
+    return dw_m4_shape(in, H, D) ? dw_m4_geom(n, in).chunks : dw_geom(n, in, H, D).chunks;
 }
 
 int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const float *X, int ldx,
@@ -1196,8 +1349,26 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         !fits_buffers(n, in, H, D, ldx > ldz ? ldx : ldz))
         return HSG_EINVAL;
     hipStream_t st = (hipStream_t)stream;
-    const DwGeom g = dw_geom(n, in, H, D);
+    DwGeom g = dw_geom(n, in, H, D);
     const long total = (long)H * D * in;
+    if (dw_m4_shape(in, H, D)) {
+        // the chunking is the 4x4x1 kernel's (hsg_hproj_dw_chunks); operands it cannot
+        // take as 16-byte rows go to the 16x16x4 kernel on the same row chunks
+        const DwM4Geom m = dw_m4_geom(n, in);
+        if (n > 0 && ldx % 4 == 0 && ldz % 4 == 0 && aligned16(X) && aligned16(dZ)) {
+            hipLaunchKernelGGL(k_hproj_dw_m4, dim3(m.ctiles, m.chunks), dim3(64 * M4W), 0, st, n, in, H, D, m.rows,
+                               dZ, ldz, X, ldx, bits, part);
+            if (int rc = status()) return rc;
+            if (!dW) return 0;
+            int blocks = (int)((total + 255) / 256);
+            if (blocks > 2048) blocks = 2048;
+            hipLaunchKernelGGL(k_sum_parts, dim3(blocks), dim3(256), 0, st, total, m.chunks, drop_scale(p), part, dW,
+                               accumulate);
+            return status();
+        }
+        g.rows = m.rows;
+        g.chunks = m.chunks;
+    }
     if (n > 0) {
         const char *ve = HSG_DEV_ENV("HSG_HPROJ_DWVEC");                   // dev A/B: 0 = dword staging
         const bool vec = (!ve || atoi(ve) != 0) && dw_slots() == 4 && D == 8 && in % 4 == 0 && ldx % 4 == 0 &&

@@ -18,7 +18,8 @@ def unpack(bits, n):
 @pytest.mark.parametrize("n,d_in,H,D", [(19200 // 4, 300, 8, 8), (1120, 64, 6, 50), (333, 70, 3, 16),
                                          (65, 33, 1, 64), (200, 40, 3, 5), (130, 50, 2, 75),
                                          (97, 300, 16, 25), (1000, 64, 16, 4), (257, 128, 3, 16),
-                                         (70, 300, 8, 8)])
+                                         (70, 300, 8, 8), (19200, 300, 8, 8), (100, 20, 2, 8), (50, 304, 4, 12),
+                                         (33, 8, 16, 4)])
 def test_head_projection_matches_masked_reference(n, d_in, H, D):
     from hetersumgraph_amd import _lib, rng
     from hetersumgraph_amd.hproj import _HeadProj
@@ -106,3 +107,35 @@ def test_batched_dropmask_equals_single_launches():
         assert lib.hsg_dropmask(n, d_in, H, float(p), ptr(s), off, ptr(ref), None) == 0
         torch.cuda.synchronize()
         assert torch.equal(g, ref), (n, d_in, H, p, off)
+
+
+@pytest.mark.parametrize("n,d_in,H,D", [(19200, 300, 8, 8), (1000, 64, 16, 4), (257, 128, 3, 16), (70, 300, 8, 8)])
+def test_dw_4x4x1_equals_16x16x4_kernel(monkeypatch, n, d_in, H, D):
+    """The unpadded 4x4x1 dW kernel (k_hproj_dw_m4, round 5) against the 16x16x4 slot
+    kernel on the same keep bits and the same row chunks (HSG_HPROJ_DWM4=0, dev
+    library): fp32 summation-order noise only, relative to the summed magnitudes."""
+    from helpers import skip_unless_dev
+    skip_unless_dev(False)
+    from hetersumgraph_amd._lib import load, ptr
+    from hetersumgraph_amd.hproj import dropmask_bits
+    lib = load()
+    torch.manual_seed(n + d_in)
+    X = torch.randn(n, d_in, device="cuda")
+    dZ = torch.randn(n, H * D, device="cuda")
+    bits = dropmask_bits(X, H, 0.1)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HSG_HPROJ_DWM4", flag)
+        chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+        part = X.new_empty(chunks * H * D * d_in)
+        dW = X.new_empty(H * D, d_in)
+        assert lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), 0.1, ptr(part), ptr(dW), 0,
+                                None) == 0
+        outs.append(dW)
+    torch.cuda.synchronize()
+    keep = unpack(bits, n).double()
+    mag = torch.einsum("kic,ikd->kdc", keep * X.double().abs().unsqueeze(0),
+                       dZ.double().abs().view(n, H, D)).reshape(H * D, d_in)
+    err = ((outs[0].double() - outs[1].double()).abs() / mag.clamp_min(1e-30)).max().item()
+    print(f"4x4x1 vs 16x16x4 dW: max |diff| / sum|terms| = {err:.2e}")
+    assert err < 1e-6

@@ -7,7 +7,7 @@
 #   devtests=<file>[+...]   the same against the dev library (pytest_dev.log)
 #   smoke                   __graft_entry__.smoke() (smoke.log)
 #   trace                   rocprofv3 kernel trace of 100 replayed cfg2 steps (step_kernels.txt)
-#   trace=<cfg>             the same on another config
+#   trace=<cfg>[:<dtype>]   the same on another config / GEMM dtype (step_kernels_<cfg>_<dtype>.txt)
 #   ab=<v1>;<v2>;...        dev-library trace A/B of env variants ('' = defaults), alternated twice
 #   abstep=<v1>;<v2>;...    dev-library in-process step-time A/B (tools/ab.py)
 #   sq                      two SQ counter passes over in-step launches, incl. SQ_LDS_BANK_CONFLICT (pmc_kernels.txt)
@@ -39,11 +39,13 @@ for step in "$@"; do
     smoke)
       timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     trace|trace=*)
-      cfg=${step#trace}; cfg=${cfg#=}; cfg=${cfg:-cfg2}
+      spec=${step#trace}; spec=${spec#=}; spec=${spec:-cfg2}
+      cfg=${spec%%:*}; dt=f32; [ "$spec" != "$cfg" ] && dt=${spec#*:}
+      tg=${cfg}_$dt
       (cd /tmp && export TMPDIR=/tmp && cd $ROOT &&
-       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/step_$cfg -o step -- python tools/step_profile.py run $cfg > $OUT/step_run_$cfg.log 2>&1)
-      python tools/step_profile.py parse $(first $OUT/step_$cfg/*/step_kernel_trace.csv $OUT/step_$cfg/step_kernel_trace.csv) > $OUT/step_kernels_$cfg.txt
-      rm -rf $OUT/step_$cfg ;;
+       HSG_PROFILE_DTYPE=$dt timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/step_$tg -o step -- python tools/step_profile.py run $cfg > $OUT/step_run_$tg.log 2>&1)
+      python tools/step_profile.py parse $(first $OUT/step_$tg/*/step_kernel_trace.csv $OUT/step_$tg/step_kernel_trace.csv) > $OUT/step_kernels_$tg.txt
+      rm -rf $OUT/step_$tg ;;
     ab=*)
       IFS=';' read -ra VS <<< "${step#ab=}"
       bash tools/gpu_trace_ab.sh $TAG/ab "${VS[@]}" ;;
