@@ -23,6 +23,7 @@
 // layouts chosen so that every such read is bank-conflict-free (Img below).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "../../include/hsg.h"
 #include "hsg_dev.h"
@@ -65,20 +66,28 @@ struct Img {
 // One operand's K tile in registers: thread t of NT covers (k row, 4 consecutive
 // columns) units t, t + NT, ...; rows past the K slice and columns past M/N load
 // zeros; units past the tile (NT not dividing it) are idle.
-template <int ROWS, int NL, int NT = kNT>
+template <int ROWS, int NL, int NT = kNT, bool BF = false>
 struct Stage {
     static constexpr int UNITS = kBK * ROWS / 4;
     static constexpr int NU = (UNITS + NT - 1) / NT;
-    f32x4 v[NU];
+    // BF (the bf16 mode's bf16 activations, round 5): the operand is bf16 rows, read as
+    // 8-byte quads and kept as they are until the image store -- converting them in
+    // load() made every prefetch wait at once (k_dw 140 vs 58 us at cfg5); the image then
+    // holds the same values the fp32 path's RNE conversion would put there
+    typedef typename std::conditional<BF, bf16x4, f32x4>::type Unit;
+    typedef typename std::conditional<BF, __bf16, float>::type Elem;
+    Unit v[NU];
 
-    __device__ __forceinline__ void load(const float *__restrict__ g, int ld, int c0, int nc, int k0, int k1) {
+    __device__ __forceinline__ void load(const void *__restrict__ g, int ld, int c0, int nc, int k0, int k1) {
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
             const int idx = threadIdx.x + NT * i;
             const int kk = idx / (ROWS / 4), c = c0 + 4 * (idx % (ROWS / 4));
-            f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            Unit x;
+            if constexpr (BF) x = bf16x4{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
+            else x = f32x4{0.f, 0.f, 0.f, 0.f};
             if ((UNITS % NT == 0 || idx < UNITS) && k0 + kk < k1 && c < nc)
-                x = *reinterpret_cast<const f32x4 *>(g + (size_t)(k0 + kk) * ld + c);
+                x = *reinterpret_cast<const Unit *>(reinterpret_cast<const Elem *>(g) + (size_t)(k0 + kk) * ld + c);
             v[i] = x;                                  // nc % 4 == 0 (host-checked): whole quads
         }
     }
@@ -89,21 +98,26 @@ struct Stage {
             const int idx = threadIdx.x + NT * i;
             if (UNITS % NT != 0 && idx >= UNITS) continue;
             const int o = Img<ROWS>::off(idx / (ROWS / 4), 4 * (idx % (ROWS / 4)));
-            bf16x4 x0, x1, x2;
+            if constexpr (BF) {
+                static_assert(NL == 1, "bf16 operands: the bf16 mode's one product");
+                *reinterpret_cast<bf16x4 *>(&img[o]) = v[i];
+            } else {
+                bf16x4 x0, x1, x2;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if constexpr (NL == 3) {
-                    __bf16 a, b, c;
-                    hsg_split3(v[i][e], a, b, c);
-                    x0[e] = a; x1[e] = b; x2[e] = c;
-                } else {
-                    x0[e] = (__bf16)v[i][e];             // RNE: the bf16 mode's operand
+                for (int e = 0; e < 4; ++e) {
+                    if constexpr (NL == 3) {
+                        __bf16 a, b, c;
+                        hsg_split3(v[i][e], a, b, c);
+                        x0[e] = a; x1[e] = b; x2[e] = c;
+                    } else {
+                        x0[e] = (__bf16)v[i][e];             // RNE: the bf16 mode's operand
+                    }
                 }
-            }
-            *reinterpret_cast<bf16x4 *>(&img[o]) = x0;
-            if constexpr (NL == 3) {
-                *reinterpret_cast<bf16x4 *>(&img[Img<ROWS>::SIZE + o]) = x1;
-                *reinterpret_cast<bf16x4 *>(&img[2 * Img<ROWS>::SIZE + o]) = x2;
+                *reinterpret_cast<bf16x4 *>(&img[o]) = x0;
+                if constexpr (NL == 3) {
+                    *reinterpret_cast<bf16x4 *>(&img[Img<ROWS>::SIZE + o]) = x1;
+                    *reinterpret_cast<bf16x4 *>(&img[2 * Img<ROWS>::SIZE + o]) = x2;
+                }
             }
         }
     }
@@ -126,7 +140,8 @@ __device__ __forceinline__ bf16x8 frag(const __bf16 *plane, int c0, int lane) {
 }
 
 struct DwJob {
-    const float *A, *B;       // [K][M] (lda), [K][N] (ldb)
+    const void *A, *B;        // [K][M] (lda), [K][N] (ldb): fp32, or bf16 per abf / bbf
+    int abf, bbf;
     float *ws;                // [splits][M][N]
     int M, N, lda, ldb;
     int cfg;                  // tile: 0 = 160 x 128, 1 = 128 x 160, 2 = 128 x 128
@@ -146,7 +161,7 @@ __device__ __forceinline__ int xcd_order(int b, int total) {
     return x * per + min(x, rem) + j;
 }
 
-template <int BM, int BN, int NL>
+template <int BM, int BN, int NL, bool ABF = false, bool BBF = false>
 __device__ __forceinline__ void dw_tile(const DwJob &jb, int tz, int t, const DwJobs &J, __bf16 *sA, __bf16 *sB) {
     constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -162,8 +177,8 @@ __device__ __forceinline__ void dw_tile(const DwJob &jb, int tz, int t, const Dw
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    Stage<BM, NL> ra;
-    Stage<BN, NL> rb;
+    Stage<BM, NL, kNT, ABF> ra;
+    Stage<BN, NL, kNT, BBF> rb;
     if (kt0 < kt1) {
         ra.load(jb.A, jb.lda, m0, jb.M, kt0 * kBK, J.K);
         rb.load(jb.B, jb.ldb, n0, jb.N, kt0 * kBK, J.K);
@@ -227,6 +242,19 @@ __global__ __launch_bounds__(kNT, 2) void k_dw(DwJobs J) {
     const DwJob &jb = J.j[q];
     const int loc = L - jb.start, tiles = jb.tiles_m * jb.tiles_n;
     const int tz = loc / tiles, t = loc - tz * tiles;            // K slices outer: a slice's tiles adjacent
+    if constexpr (NL == 1) {              // the bf16 mode: operands fp32 or bf16 per job
+        const int f = jb.abf | (jb.bbf << 1);
+#define HSG_DWT(BM_, BN_)                                                                   \
+        if (f == 0) dw_tile<BM_, BN_, 1>(jb, tz, t, J, sA, sB);                             \
+        else if (f == 1) dw_tile<BM_, BN_, 1, true, false>(jb, tz, t, J, sA, sB);           \
+        else if (f == 2) dw_tile<BM_, BN_, 1, false, true>(jb, tz, t, J, sA, sB);           \
+        else dw_tile<BM_, BN_, 1, true, true>(jb, tz, t, J, sA, sB);
+        if (jb.cfg == 0) { HSG_DWT(160, 128) }
+        else if (jb.cfg == 1) { HSG_DWT(128, 160) }
+        else { HSG_DWT(128, 128) }
+#undef HSG_DWT
+        return;
+    }
     if (jb.cfg == 0) dw_tile<160, 128, NL>(jb, tz, t, J, sA, sB);
     else if (jb.cfg == 1) dw_tile<128, 160, NL>(jb, tz, t, J, sA, sB);
     else dw_tile<128, 128, NL>(jb, tz, t, J, sA, sB);
@@ -265,7 +293,7 @@ __device__ __forceinline__ void dw2_tile(const DwJob &jb, int tz, int t, const D
     Stage<BN, NL, kNT2> rb[2];
     auto load = [&](int s, int kt) {
         if (kt < kt1) {
-            ra[s].load(jb.A, jb.lda, m0, jb.M, kt * kBK, J.K);
+            ra[s].load(jb.A, jb.lda, m0, jb.M, kt * kBK, J.K);          // fp32 operands (dev kernel)
             rb[s].load(jb.B, jb.ldb, n0, jb.N, kt * kBK, J.K);
         }
     };
@@ -378,8 +406,9 @@ int hsg_gemm_dw_tiles(int M, int N) {
     return ((M + kTileM[c] - 1) / kTileM[c]) * ((N + kTileN[c] - 1) / kTileN[c]);
 }
 
-int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float *const *A, const int *lda,
-                      const float *const *B, const int *ldb, int splits, int bf16, float *const *ws, void *stream) {
+static int dw_slabs(int njobs, const int *M, const int *N, int K, const void *const *A, const int *lda,
+                    const void *const *B, const int *ldb, const int *io, int splits, int bf16, float *const *ws,
+                    void *stream) {
     if (njobs < 1 || njobs > 2 || K < 1 || splits < 1 || !M || !N || !A || !B || !lda || !ldb || !ws)
         return HSG_EINVAL;
     DwJobs J{};
@@ -396,7 +425,11 @@ int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float 
         if (M[q] < 1 || N[q] < 1 || (M[q] & 3) || (N[q] & 3) || lda[q] < M[q] || ldb[q] < N[q] || (lda[q] & 3) ||
             (ldb[q] & 3) || !A[q] || !B[q] || !ws[q] || !al16(A[q]) || !al16(B[q]))
             return HSG_EINVAL;
+        const int iq = io ? io[q] : 0;
+        if (iq && (!bf16 || (iq & ~3))) return HSG_EINVAL;      // bf16 operands: the bf16 mode only
         jb.A = A[q]; jb.B = B[q]; jb.ws = ws[q];
+        jb.abf = iq & 1;
+        jb.bbf = (iq >> 1) & 1;
         jb.M = M[q]; jb.N = N[q]; jb.lda = lda[q]; jb.ldb = ldb[q];
         jb.cfg = pick_cfg(M[q], N[q]);
         jb.tiles_m = (M[q] + kTileM[jb.cfg] - 1) / kTileM[jb.cfg];
@@ -406,13 +439,25 @@ int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float 
     }
     J.total = start;
     hipStream_t st = (hipStream_t)stream;
-    if (dw_v2()) {
+    if (dw_v2() && !(J.j[0].abf | J.j[0].bbf | (njobs > 1 ? J.j[1].abf | J.j[1].bbf : 0))) {
         if (bf16) hipLaunchKernelGGL(k_dw2<1>, dim3((unsigned)J.total), dim3(kNT2), 0, st, J);
         else hipLaunchKernelGGL(k_dw2<3>, dim3((unsigned)J.total), dim3(kNT2), 0, st, J);
     } else if (bf16) hipLaunchKernelGGL(k_dw<1>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
     else hipLaunchKernelGGL(k_dw<3>, dim3((unsigned)J.total), dim3(kNT), 0, st, J);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float *const *A, const int *lda,
+                      const float *const *B, const int *ldb, int splits, int bf16, float *const *ws, void *stream) {
+    return dw_slabs(njobs, M, N, K, reinterpret_cast<const void *const *>(A), lda,
+                    reinterpret_cast<const void *const *>(B), ldb, nullptr, splits, bf16, ws, stream);
+}
+
+int hsg_gemm_dw_slabs_io(int njobs, const int *M, const int *N, int K, const void *const *A, const int *lda,
+                         const void *const *B, const int *ldb, const int *io, int splits, float *const *ws,
+                         void *stream) {
+    return dw_slabs(njobs, M, N, K, A, lda, B, ldb, io, splits, 1, ws, stream);
 }
 
 }  // extern "C"

@@ -358,6 +358,93 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     }
 }
 
+// ------------------------------------------------ forward, single pass (round 5) ----
+// Narrow rows (H * D <= 64: the W2S sentence destinations, ~36 word in-edges each at
+// cfg2).  k_gat_fwd runs a destination as two phases -- the scores' online (max, sum)
+// over the lanes of each head, merged across the block's 4 waves through LDS and a
+// barrier, then the alphas staged in LDS and the Z rows gathered -- i.e. four dependent
+// memory round trips and two block barriers per destination.  Here one wave owns a
+// destination and lane f its feature f (head f / D) end to end: lane j < EB loads edge
+// j's (source, box) once, the wave broadcasts them by readlane, and every lane requests
+// its own head's (sigma, tau) and its Z feature for all EB edges at once; the softmax
+// is online per lane over the batch (one rescale per batch), so h = sum_e p_e Z_u / l
+// needs no alpha staging and no cross-lane reduction.  Chain: indptr -> (src, box) ->
+// (sigma, tau, Z) -> stores.  Same numbers as k_gat_fwd up to fp32 summation order
+// (the per-edge exp and the accumulation order differ); m, l as it writes them.
+template <int TAU_MODE, int EB>
+__global__ __launch_bounds__(256) void k_gat_fwd_sp(RelPtrs R, int H, int D, float slope,
+                                                    const float *__restrict__ Z,
+                                                    const float *__restrict__ sigma,
+                                                    const float *__restrict__ tau,
+                                                    const float *__restrict__ origin,
+                                                    float *__restrict__ hout, float *__restrict__ out,
+                                                    float *__restrict__ mout, float *__restrict__ lout) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const bool fok = lane < HD;
+    const int f = fok ? lane : HD - 1;
+    const int kf = div_small(f, 1.f / (float)D);
+    const WorkRange wr = work_range(R.n_dst, HSG_WAVES, wid, R.xcd);
+    for (int v_ = wr.first; v_ < wr.end; v_ += wr.stride) {
+        const int v = __builtin_amdgcn_readfirstlane(v_);
+        const int beg = R.indptr[v], end = R.indptr[v + 1], c = R.phantom[v];
+        const float org = origin ? origin[(size_t)v * HD + f] : 0.f;
+        float m = -INFINITY, l = 0.f, acc = 0.f;
+        for (int e0 = beg; e0 < end; e0 += EB) {
+            const int nb = min(EB, end - e0);
+            int uj = 0, tj = 0;
+            if (lane < nb) {
+                uj = R.src[e0 + lane];
+                tj = tau_row<TAU_MODE>(R, e0 + lane);
+            }
+            float sc[EB], zz[EB];
+#pragma unroll
+            for (int j = 0; j < EB; ++j) {
+                if (j < nb) {                                    // wave-uniform
+                    const int u = __builtin_amdgcn_readlane(uj, j), t = __builtin_amdgcn_readlane(tj, j);
+                    sc[j] = sigma[u * H + kf] + tau[t * H + kf];
+                    zz[j] = Z[(size_t)u * HD + f];
+                }
+            }
+            float bm = m;
+#pragma unroll
+            for (int j = 0; j < EB; ++j)
+                if (j < nb) {
+                    sc[j] = leaky(sc[j], slope);
+                    bm = fmaxf(bm, sc[j]);
+                }
+            const float r = __expf(m - bm);                     // m = -inf on the first batch: 0
+            acc *= r;
+            l *= r;
+#pragma unroll
+            for (int j = 0; j < EB; ++j)
+                if (j < nb) {
+                    const float pj = __expf(sc[j] - bm);
+                    l += pj;
+                    acc = fmaf(pj, zz[j], acc);
+                }
+            m = bm;
+        }
+        if (c > 0) {                                             // phantom in-edges: e = 0, no message
+            const float bm = fmaxf(m, 0.f), r = __expf(m - bm);
+            acc *= r;
+            l = l * r + (float)c * __expf(-bm);
+            m = bm;
+        }
+        const bool any = end > beg;
+        const float hv = any ? acc / l : 0.f;
+        if (fok) {
+            const size_t o = (size_t)v * HD + f;
+            if (hout) hout[o] = hv;
+            if (origin) out[o] = elu1(hv) + org;
+        }
+        if (fok && f - kf * D == 0) {
+            mout[v * H + kf] = any ? m : 0.f;
+            lout[v * H + kf] = any ? l : 1.f;
+        }
+    }
+}
+
 // Grouped forward for short segments and wide rows (S2W: ~2 in-edges per word,
 // H*D = 300): a wave carries 64/LPN destinations at once, one per LPN-lane group,
 // so each wave has that many independent index -> score -> gather chains in flight
@@ -1684,6 +1771,14 @@ int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
 
 // dst-side launch shape (fwd and bwd_dst share it; the d tau slab has one row per block)
 int dst_wpn(const hsg_rel *r) { return wpn_for(r->n_dst, r->n_edges); }
+// single-pass narrow-row forward (k_gat_fwd_sp): its edge batch, 0 = off.  Measured
+// slower than the 4-wave k_gat_fwd on the cfg2 W2S destinations (17.4 / 16.2 us with
+// 64- / 32-edge batches against 7.8 us, profiles/r05/): dev opt-in (HSG_GAT_FWD_SP=32|64)
+int fwd_sp() {
+    const char *e = HSG_DEV_ENV("HSG_GAT_FWD_SP");
+    const int eb = e ? atoi(e) : 0;
+    return eb == 0 ? 0 : (eb == 32 ? 32 : 64);
+}
 int src_wpn(const hsg_rel *r) { return wpn_for(r->n_src, r->n_edges); }
 
 }  // namespace
@@ -1713,6 +1808,21 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
 #endif
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
+    if (nf == 1 && fwd_sp()) {                      // narrow rows: one single-pass wave per destination
+        const dim3 g(grid_nodes(rel->n_dst, 1, kFwdGridCap));
+        const int eb = fwd_sp();
+#define HSG_SP(TAU, EB_) HSG_KLAUNCH(true, true, (k_gat_fwd_sp<TAU, EB_>), g, dim3(256), st, R, H, D, slope, Z, sigma, \
+                                     tau, origin, h, out, m, l)
+        if (tau_mode == HSG_TAU_TABLE) {
+            if (eb == 64) HSG_SP(HSG_TAU_TABLE, 64);
+            else HSG_SP(HSG_TAU_TABLE, 32);
+        } else {
+            if (eb == 64) HSG_SP(HSG_TAU_PER_EDGE, 64);
+            else HSG_SP(HSG_TAU_PER_EDGE, 32);
+        }
+#undef HSG_SP
+        return launch_status();
+    }
 #ifdef HSG_DEV
     if (wpn == 1) {                      // short segments: row-tile float4 kernel
         const bool al = aligned16p(Z) && aligned16p(h) && (!origin || (aligned16p(origin) && aligned16p(out)));

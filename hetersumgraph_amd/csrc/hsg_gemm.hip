@@ -955,11 +955,17 @@ __device__ __forceinline__ void epi_store(const f32x16 (&acc)[TN], int row0, int
 // __shfl_xor lowers to a chain of ds_bpermute round trips through the LDS path
 __device__ __forceinline__ float row16_sum(float x) { return hsg_group_sum<16>(x); }
 
-template <int BN>
+typedef float f32x4v7 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4v7 __attribute__((ext_vector_type(4)));
+
+// CBF / AUXBF (the bf16 mode's bf16 activations, round 5): C is stored and the aux
+// operand (the relu' mask H) read as bf16 quads (8 B) at the same element offsets
+template <int BN, bool CBF = false, bool AUXBF = false>
 struct EpiRows {
     static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
     static constexpr int STEPS = (32 + RPS - 1) / RPS;
     f32x4 bn, aux[STEPS], ex[STEPS];
+    bf16x4v7 auxb[AUXBF ? STEPS : 1];
 
     // the epilogue's global operands (bias, aux, and for HSG_EPI_ADD_ELUG x - origin),
     // requested together; k_gemm7 issues this before its last K tile's MFMAs so the
@@ -974,7 +980,12 @@ struct EpiRows {
 #pragma unroll
             for (int t = 0; t < STEPS; ++t) {
                 const int m = min(row0 + min(t * RPS + rs, 31), p.M - 1);
-                aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + nc);
+                if constexpr (AUXBF) {      // kept raw until finish(): a conversion here would wait
+                    auxb[t] = *reinterpret_cast<const bf16x4v7 *>(      // for the load at once
+                        reinterpret_cast<const __bf16 *>(p.aux) + (size_t)m * p.ldaux + nc);
+                } else {
+                    aux[t] = *reinterpret_cast<const f32x4 *>(p.aux + (size_t)m * p.ldaux + nc);
+                }
             }
         }
         if (p.epi == HSG_EPI_ADD_ELUG) {                   // e = x - origin = elu(h)
@@ -1014,8 +1025,13 @@ struct EpiRows {
             if (qok && rok) {
                 f32x4 v = *reinterpret_cast<const f32x4 *>(&wl[r * LDW + 4 * q]);
                 if (p.epi == HSG_EPI_RELU_BWD) {
+                    if constexpr (AUXBF) {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
+                        for (int e = 0; e < 4; ++e) v[e] = (float)auxb[t][e] > 0.f ? v[e] : 0.f;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = aux[t][e] > 0.f ? v[e] : 0.f;
+                    }
                 } else {
                     v += bn;
                     if (p.epi == HSG_EPI_ADD || p.epi == HSG_EPI_ADD_ELUG) v += aux[t];
@@ -1024,7 +1040,12 @@ struct EpiRows {
                         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
                     }
                 }
-                if (!NS || v[0] == 1234.5f) *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+                if constexpr (CBF) {
+                    *reinterpret_cast<bf16x4v7 *>(reinterpret_cast<__bf16 *>(p.C) + (size_t)m * p.ldc + n) =
+                        bf16x4v7{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};   // RNE
+                } else if (!NS || v[0] == 1234.5f) {
+                    *reinterpret_cast<f32x4 *>(p.C + (size_t)m * p.ldc + n) = v;
+                }
                 if (p.epi == HSG_EPI_ADD_ELUG) {
                     // G = dOut * elu'(h): 1 for e = elu(h) > 0, else e + 1 = exp(h) (continuous at 0)
                     f32x4 g;
@@ -1273,7 +1294,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm5(GemmArgs p, const __bf16 *__re
 // (tools/gemm5_sweep.py, 5 interleaved rounds): BN = 64 is the fastest tile on all
 // four cfg2 S2W FFN shapes; the wide tiles (80 | 128) were not faster.
 // ---------------------------------------------------------------------------------
-typedef float f32x4v7 __attribute__((ext_vector_type(4)));
+
 // PM: 0 = fp32-accurate (RNE 3-limb split, six products), 1 = the same with the
 // truncation split (dev), 2 = bf16 mode (hsg_gemm_bf16 semantics: A and the weight
 // rounded to bf16 RNE, ONE product: only limb plane 0 of the weight is staged)
@@ -1281,10 +1302,19 @@ typedef float f32x4v7 __attribute__((ext_vector_type(4)));
 // plus per-lane 32-bit byte offsets computed once (row clamps, swizzles, limb rows), so
 // the K loop issues the saddr form of global_load_lds with no per-tile address VALU;
 // only a tile reaching past K takes the per-chunk zero-page select.
-template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false>
+// IO (round 5, bf16 mode only, PM = 2): bit 0 -- A is bf16 (the FFN's bf16 H / dY /
+// dH rows: lda % 8 == 0, 16-byte rows, columns K .. ceil8(K) - 1 zero): the A tile is
+// staged as bf16 rows of 64 B (the weight planes' image and swizzle, bswz16) and a
+// fragment is one ds_read_b128, no conversion; bit 1 -- C is stored as bf16; bit 2 --
+// the aux operand (relu' mask) is bf16.  The products are those of the fp32-A path
+// (which rounds A to bf16 at fragment read): the bf16 mode's numbers are unchanged, its
+// bytes halved.
+template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false, int IO = 0>
 __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
-    constexpr int A_FL = BM * 32;                          // floats of the A tile
+    constexpr bool ABF = (IO & 1) != 0, CBF = (IO & 2) != 0, AUXBF = (IO & 4) != 0;
+    static_assert(!ABF || (PM == 2 && !SA), "bf16 A: the bf16 mode's one-product path");
+    constexpr int A_FL = ABF ? BM * 16 : BM * 32;          // floats of the A tile
     constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
     constexpr int NL = PM == 2 ? 1 : 3;                    // weight limb planes staged
     constexpr bool NOMFMA = PM >= 5;                       // dev diagnostics (plans 34-38)
@@ -1292,7 +1322,8 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     constexpr int STAGE_FL = A_FL + NL * B_BF / 2;         // stage size in floats
     constexpr int BPC = BN / 16;                           // 1-KB pieces (16 rows) per limb plane tile
     constexpr int NBP = (NL * BPC + 3) / 4;                // B DMA instructions per wave per K tile
-    constexpr int NLD = BM / 32 + NBP;                     // all DMA instructions per wave per K tile
+    constexpr int NLA = ABF ? BM / 64 : BM / 32;           // A DMA instructions per wave per K tile
+    constexpr int NLD = NLA + NBP;                         // all DMA instructions per wave per K tile
     constexpr int EPI_FL = BM * (BN + 4);                  // the epilogue's row images reuse the stages
     static_assert(BN % 16 == 0, "BN must be a multiple of 16");
     __shared__ __attribute__((aligned(16))) float lds[S * STAGE_FL > EPI_FL ? S * STAGE_FL : EPI_FL];
@@ -1310,7 +1341,7 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
-    EpiRows<BN> ep;
+    EpiRows<BN, CBF, AUXBF> ep;
 
     uint32_t aoff[BM / 32], boff[NBP];
     if constexpr (SA) {
@@ -1360,7 +1391,23 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
             }
             return;
         }
-        if constexpr (!NOA) glds_tile<BM, true>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
+        if constexpr (ABF) {
+            // 16 rows of 64 B per 1-KB piece, BM / 16 pieces over 4 waves
+            const __bf16 *Ab = reinterpret_cast<const __bf16 *>(p.A);
+#pragma unroll
+            for (int pc = 0; pc < NLA; ++pc) {
+                const int piece = pc * 4 + wid;
+                const int r = piece * 16 + (lane >> 2);
+                const int c = (lane & 3) ^ bswz16(r);
+                const int k = k0 + 8 * c;
+                const void *src = k < p.K ? (const void *)(Ab + (size_t)min(m0 + r, p.M - 1) * p.lda + k)
+                                          : (const void *)g_zero16;
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                                 (__attribute__((address_space(3))) void *)(st + piece * 256), 16, 0, 0);
+            }
+        } else if constexpr (!NOA) {
+            glds_tile<BM, true>(st, p.A, p.lda, m0, p.M, k0, p.K, wid, lane);
+        }
         __bf16 *sb = reinterpret_cast<__bf16 *>(st + A_FL);
 #pragma unroll
         for (int pc = 0; pc < (NOB ? 0 : NBP); ++pc) {
@@ -1397,6 +1444,12 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
         bf16x8 a[2][3];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
+            if constexpr (ABF) {
+                const int r = wid * 32 + 16 * i + li;
+                a[i][0] = *reinterpret_cast<const bf16x8 *>(reinterpret_cast<const __bf16 *>(sa) + r * 32 +
+                                                            8 * (kb ^ bswz16(r)));
+                continue;
+            }
             const int r = wid * 32 + 16 * i + li, sw = swz16(r);
             const f32x4 x = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb) ^ sw)]);
             const f32x4 y = *reinterpret_cast<const f32x4 *>(&sa[r * 32 + 4 * ((2 * kb + 1) ^ sw)]);
@@ -1462,7 +1515,7 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     if (p.colpart) epi_rows_colpart<BN>(lds, cs, wid, lane, ty, n0, p);
 }
 
-template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false>
+template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false, int IO = 0>
 int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
     p.k_tiles_per_split = Kp / 32;
@@ -1470,7 +1523,7 @@ int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     if (!epi_rows_ok(p)) return HSG_EINVAL;                 // the float4 epilogue needs whole aligned quads
     const long g = (long)((p.N + BN - 1) / BN) * ((p.M + 127) / 128);
     if (SA && ((long)p.M * p.lda * 4 >= (1L << 32) || (long)3 * Np * Kp * 2 >= (1L << 32))) return HSG_EINVAL;
-    hipLaunchKernelGGL((k_gemm7<BN, S, PM, OCC, SA>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
+    hipLaunchKernelGGL((k_gemm7<BN, S, PM, OCC, SA, IO>), dim3((unsigned)g), dim3(256), 0, st, p, planes, Np, Kp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -2569,6 +2622,37 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
 }
 
 // bf16-mode k_gemm7 (one product per tile): dev plans for the tile / depth / occupancy sweep
+// the bf16 mode with bf16 activations (io: HSG_IO_* bits): the FFN's four GEMMs take
+// io 2 (x W1^T -> H), 1 (H W2^T), 7 (dY W2 with the H mask -> dH) and 1 (dH W1, ELU
+// gate); tiles as launch7b's default
+extern "C++" {
+template <int IO>
+static int launch7io_narrow(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
+#ifdef HSG_DEV
+    if (const char *e = HSG_DEV_ENV("HSG_GEMM7IO")) {         // dev sweep of the N <= 320 tile
+        const int v = atoi(e);
+        if (v == 1) return launch7<128, 2, 2, 2, false, IO>(p, pl, Np, Kp, st);
+        if (v == 3) return launch7<64, 2, 2, 3, false, IO>(p, pl, Np, Kp, st);
+        if (v == 4) return launch7<64, 2, 2, 2, false, IO>(p, pl, Np, Kp, st);
+    }
+#endif
+    // cfg5 in-step (profiles/r05/): 3 stages at 3 blocks per CU 42.7 us against 45.0
+    // (2 stages, 2 blocks), 44.9 (2 stages, 3 blocks) and 58.2 (128-wide tiles)
+    return launch7<64, 3, 2, 3, false, IO>(p, pl, Np, Kp, st);
+}
+}  // extern "C++"
+
+static int launch7io(GemmArgs p, const __bf16 *pl, int Np, int Kp, int io, hipStream_t st) {
+    const bool wide = p.N > 320;
+    switch (io) {
+    case 0: return wide ? launch7<128, 2, 2>(p, pl, Np, Kp, st) : launch7<64, 2, 2>(p, pl, Np, Kp, st);
+    case 1: return wide ? launch7<128, 2, 2, 2, false, 1>(p, pl, Np, Kp, st) : launch7io_narrow<1>(p, pl, Np, Kp, st);
+    case 2: return wide ? launch7<128, 2, 2, 2, false, 2>(p, pl, Np, Kp, st) : launch7io_narrow<2>(p, pl, Np, Kp, st);
+    case 7: return wide ? launch7<128, 2, 2, 2, false, 7>(p, pl, Np, Kp, st) : launch7io_narrow<7>(p, pl, Np, Kp, st);
+    default: return HSG_EINVAL;
+    }
+}
+
 static int launch7b(GemmArgs p, const __bf16 *pl, int Np, int Kp, hipStream_t st) {
     int plan = 0;
 #ifdef HSG_DEV
@@ -2641,6 +2725,30 @@ int hsg_gemm_psw_ln(int M, int N, int K, const float *A, int lda, const void *pl
 #endif
 }
 
+// bf16-mode GEMM on bf16 activations (round 5): A / C / aux given as bf16 rows per
+// io (HSG_IO_A_BF16 | HSG_IO_C_BF16 | HSG_IO_AUX_BF16; element strides lda / ldc /
+// ldaux).  bf16 A: lda % 8 == 0, 16-byte aligned, columns K .. ceil8(K) - 1 zero.
+int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void *planes, void *C, int ldc,
+                         const float *bias, const void *aux, int ldaux, int epi, int relu, float *colsum_part,
+                         int io, void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A) return HSG_EINVAL;
+    if (io != 0 && io != 1 && io != 2 && io != 7) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
+    if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
+    if ((io & 4) && epi != HSG_EPI_RELU_BWD) return HSG_EINVAL;           // a bf16 aux is a relu' mask
+    if ((io & 2) && epi == HSG_EPI_ADD) return HSG_EINVAL;                 // accumulate: fp32 C
+    const bool abf = io & 1;
+    if ((((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || (abf ? (lda & 7) : ((lda & 3) || (K & 3))))
+        return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, reinterpret_cast<const float *>(A), lda, nullptr, 0, reinterpret_cast<float *>(C), ldc, bias,
+               reinterpret_cast<const float *>(aux), ldaux, epi, relu, Kp / 32, nullptr, colsum_part, 1, 1};
+    if (!epi_rows_ok(p)) return HSG_EINVAL;
+    return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, io, (hipStream_t)stream);
+}
+
 int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     (void)K; (void)bf16;
     if (M < 0 || N < 1) return 0;
@@ -2671,6 +2779,25 @@ int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const vo
     // dev library's k_gemm11 declines a rho GEMM (try11), so it falls through to k_gemm7
     if (bf16) return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
     return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
+// hsg_gemm_psw_elug_rho in the bf16 mode on a bf16 A (the FFN's bf16 dH rows; lda %
+// 8 == 0, 16-byte aligned, columns K .. ceil8(K) - 1 zero)
+int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
+                                   int ldc, const float *aux, const float *x, const float *origin, float *G, int ld,
+                                   float *rho, int head_dim, void *stream) {
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G) return HSG_EINVAL;
+    if ((lda & 7) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N) return HSG_EINVAL;
+    if (rho && (head_dim < 32 || N % head_dim)) return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, reinterpret_cast<const float *>(A), lda, nullptr, 0, C, ldc, nullptr, aux, ld,
+               HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr, 1, 1, x, origin, G};
+    p.rho = rho;
+    p.rho_d = head_dim;
+    if (!epi_rows_ok(p)) return HSG_EINVAL;
+    return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, 1, (hipStream_t)stream);
 }
 
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,

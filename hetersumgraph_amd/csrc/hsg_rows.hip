@@ -74,6 +74,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd(int n, int d, const float *__res
 // 4*lane + 256*i, i < NV, and each wave takes RPW rows whose loads are issued
 // together (float4 loads: a quarter of the load instructions of k_ln_fwd).
 typedef float f32x4r __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x4r __attribute__((ext_vector_type(4)));
 template <int NV, int RPW>
 __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__restrict__ y,
                                                  const float *__restrict__ x, const float *__restrict__ gamma,
@@ -324,14 +325,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
 // block partials go to the same part[block][3][d] layout.  cfg2 in-step: 23.0-23.1 vs
 // 24.6 us per launch at the 512-block cap (1,024 / 1,536 blocks: 25.3 / 24.0 us and
 // larger partial slabs; profiles/r04_dev/ln_bwdp/).
-template <int NV>
+// DYBF (round 5, the bf16 GEMM mode): dy -- a pure GEMM operand there (dH = dy W2,
+// dW2 = dy^T H, both on bf16-rounded operands) -- is stored as bf16 rows of pitch ld_dy
+// (>= ceil8(d)), the pad columns d .. ceil8(d) - 1 zero (the bf16-A contract of
+// hsg_gemm_bf16_psw_io); db2 still sums the fp32 values.
+template <int NV, bool DYBF = false>
 __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__restrict__ dout,
                                                   const float *__restrict__ y, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ mean,
                                                   const float *__restrict__ rstd, float p_drop,
                                                   const int64_t *__restrict__ seedp, uint32_t offset,
                                                   float *__restrict__ dy, float *__restrict__ dx,
-                                                  float *__restrict__ part) {
+                                                  float *__restrict__ part, int ld_dy = 0) {
     __shared__ __attribute__((aligned(16))) float s_red[4][kMaxPerLane * 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
@@ -403,8 +408,16 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
                     dyv[e] = (keep >> (4 * i + e)) & 1u ? ds[e] * scale : 0.f;
                 }
                 *reinterpret_cast<f32x4r *>(dx + rb + cq[i]) = ds;
-                *reinterpret_cast<f32x4r *>(dy + rb + cq[i]) = dyv;
+                if constexpr (DYBF) {
+                    *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)r * ld_dy + cq[i]) =
+                        bf16x4r{(__bf16)dyv[0], (__bf16)dyv[1], (__bf16)dyv[2], (__bf16)dyv[3]};
+                } else {
+                    *reinterpret_cast<f32x4r *>(dy + rb + cq[i]) = dyv;
+                }
                 dyb[i] += dyv;
+            } else if (DYBF && 4 * lane + 256 * i == d && d + 4 <= ld_dy) {   // the zero pad quad
+                *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)r * ld_dy + d) =
+                    bf16x4r{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
             }
         }
     }
@@ -573,6 +586,25 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
         break;
     switch (npl) { HSG_LNB(1) HSG_LNB(2) HSG_LNB(3) HSG_LNB(4) HSG_LNB(5) HSG_LNB(6) HSG_LNB(7) HSG_LNB(8) }
 #undef HSG_LNB
+    return status();
+}
+
+// hsg_ln_bwd with dy stored as bf16 rows (the bf16 GEMM mode's bf16 activations): the
+// vector kernel's shapes only (d % 4 == 0, 257..512 columns, 16-byte aligned fp32 rows,
+// ld_dy % 8 == 0 and >= ceil8(d), 16-byte aligned dy), HSG_EINVAL otherwise.
+int hsg_ln_bwd_dy16(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+                    const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
+                    void *dy, int ld_dy, float *dx, float *part, void *stream) {
+    const auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
+    if (d % 4 || (d + 255) / 256 != 2 || d <= 256 || (ld_dy & 7) || ld_dy < (d + 7) / 8 * 8 || p_drop < 0.f ||
+        p_drop >= 1.f || (p_drop > 0.f && !seed) || !part || (p_drop > 0.f && (long)n * d >= (1L << 32)) ||
+        !al(dout) || !al(y) || !al(x) || !al(gamma) || !al(dy) || !al(dx))
+        return HSG_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(grid_rows(n, ln_bwd_cap())), block(256);
+    if (n == 0) return (int)hipMemsetAsync(part, 0, sizeof(float) * 3 * d * grid.x, st);
+    hipLaunchKernelGGL((k_ln_bwd4p<2, true>), grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, seed,
+                       offset, reinterpret_cast<float *>(dy), dx, part, ld_dy);
     return status();
 }
 

@@ -144,25 +144,43 @@ def split_weights(*specs, launch=True):
     return out
 
 
+def _io(A, out, aux):
+    """HSG_IO_* bits of a bf16-mode GEMM's bf16 operands (hsg_gemm_bf16_psw_io)."""
+    bf = torch.bfloat16
+    return ((_lib.HSG_IO_A_BF16 if A.dtype == bf else 0) | (_lib.HSG_IO_C_BF16 if out.dtype == bf else 0)
+            | (_lib.HSG_IO_AUX_BF16 if aux is not None and aux.dtype == bf else 0))
+
+
 def gemm_psw(A, Bs, out=None, bias=None, relu=False, relu_mask=None, add=None, colsum_part=None):
     """C = A @ B^T [+ bias] [relu] | * (relu_mask > 0) | + add, with B a SplitWeight
     (hsg_gemm_f32_psw: fp32-accurate as gemm(..., dtype='f32'); a weight split in the
     'bf16' mode runs hsg_gemm_bf16_psw: its plane 0 = RNE(W), one bf16 product, as
-    gemm(..., dtype='bf16'))."""
+    gemm(..., dtype='bf16')).  In the 'bf16' mode A, ``out`` and ``relu_mask`` may be
+    bf16 tensors (the FFN's bf16 activations, hsg_gemm_bf16_psw_io): the same products,
+    since that mode rounds A to bf16 anyway; a bf16 A carries zeros in its columns K ..
+    ceil8(K) - 1 (row pitch a multiple of 8)."""
     lib = load()
-    if not A.is_cuda or A.dtype != torch.float32:
+    if not A.is_cuda or A.dtype not in (torch.float32, torch.bfloat16):
         raise RuntimeError("hsg gemm: fp32 ROCm tensors only (no CPU fallback)")
     M, K = A.shape
     if K != Bs.K:
         raise ValueError(f"gemm_psw: inner dims {K} != {Bs.K}")
     N = Bs.N
     if out is None:
-        out = A.new_empty(M, N)
+        out = A.new_empty(M, N, dtype=torch.float32)
     epi, aux = HSG_EPI_STORE, None
     if relu_mask is not None:
         epi, aux = HSG_EPI_RELU_BWD, relu_mask
     elif add is not None:
         epi, aux = HSG_EPI_ADD, add
+    io = _io(A, out, aux)
+    if io:
+        if Bs.mode != "bf16":
+            raise RuntimeError("gemm_psw: bf16 activations belong to the 'bf16' GEMM mode")
+        check(lib.hsg_gemm_bf16_psw_io(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias),
+                                       ptr(aux), _ld(aux) if aux is not None else 0, epi, int(relu),
+                                       ptr(colsum_part), io, stream_of(A)), "hsg_gemm_bf16_psw_io")
+        return out
     if Bs.mode == "bf16":
         rc = lib.hsg_gemm_bf16_psw(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), _ld(out), ptr(bias), ptr(aux),
                                    _ld(aux) if aux is not None else 0, epi, int(relu), ptr(colsum_part), stream_of(A))
@@ -217,9 +235,16 @@ def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
         return False
     if rho is not None and (rho.shape != (M, (N + 63) // 64, 3) or not rho.is_contiguous()):
         return False
-    rc = lib.hsg_gemm_psw_elug_rho(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
-                                   ptr(origin), ptr(G), N, ptr(rho), int(head_dim), int(Bs.mode == "bf16"),
-                                   stream_of(A))
+    if A.dtype == torch.bfloat16:                # the bf16 mode's bf16 dH rows
+        if Bs.mode != "bf16":
+            raise RuntimeError("gemm_psw_elug: bf16 activations belong to the 'bf16' GEMM mode")
+        rc = lib.hsg_gemm_bf16_psw_elug_rho_a16(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out),
+                                                ptr(x), ptr(origin), ptr(G), N, ptr(rho), int(head_dim),
+                                                stream_of(A))
+    else:
+        rc = lib.hsg_gemm_psw_elug_rho(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
+                                       ptr(origin), ptr(G), N, ptr(rho), int(head_dim), int(Bs.mode == "bf16"),
+                                       stream_of(A))
     if rc == HSG_EINVAL:
         return False
     check(rc, "hsg_gemm_psw_elug_rho")
@@ -269,8 +294,9 @@ def gemm_dw_slabs(pairs, splits=None):
     if _GEMM_DTYPE not in ("f32", "bf16") or not pairs or len(pairs) > 2:
         return None
     K = pairs[0][0].shape[0]
+    okt = (torch.float32, torch.bfloat16) if _GEMM_DTYPE == "bf16" else (torch.float32,)
     for A, B in pairs:
-        if (not A.is_cuda or A.dtype != torch.float32 or B.dtype != torch.float32 or A.dim() != 2 or B.dim() != 2
+        if (not A.is_cuda or A.dtype not in okt or B.dtype not in okt or A.dim() != 2 or B.dim() != 2
                 or A.shape[0] != K or B.shape[0] != K or A.stride(1) != 1 or B.stride(1) != 1
                 or A.shape[1] % 4 or B.shape[1] % 4 or _ld(A) % 4 or _ld(B) % 4
                 or A.data_ptr() % 16 or B.data_ptr() % 16):
@@ -287,13 +313,21 @@ def gemm_dw_slabs(pairs, splits=None):
         return None
     n = len(pairs)
     arr = lambda t, xs: (t * n)(*xs)
-    ws = [pairs[q][0].new_empty(splits * pairs[q][0].shape[1] * pairs[q][1].shape[1]) for q in range(n)]
+    # fp32 slabs whatever the operands' dtype (a bf16 operand's new_empty would be bf16:
+    # half the bytes the kernel writes)
+    ws = [pairs[q][0].new_empty(splits * pairs[q][0].shape[1] * pairs[q][1].shape[1], dtype=torch.float32)
+          for q in range(n)]
     c_i, c_p = ctypes.c_int, ctypes.c_void_p
-    rc = lib.hsg_gemm_dw_slabs(n, arr(c_i, [A.shape[1] for A, _ in pairs]), arr(c_i, [B.shape[1] for _, B in pairs]),
-                               K, arr(c_p, [A.data_ptr() for A, _ in pairs]), arr(c_i, [_ld(A) for A, _ in pairs]),
-                               arr(c_p, [B.data_ptr() for _, B in pairs]), arr(c_i, [_ld(B) for _, B in pairs]),
-                               splits, int(_GEMM_DTYPE == "bf16"), arr(c_p, [w.data_ptr() for w in ws]),
-                               stream_of(pairs[0][0]))
+    io = [int(A.dtype == torch.bfloat16) | (2 * int(B.dtype == torch.bfloat16)) for A, B in pairs]
+    dims = (arr(c_i, [A.shape[1] for A, _ in pairs]), arr(c_i, [B.shape[1] for _, B in pairs]), K,
+            arr(c_p, [A.data_ptr() for A, _ in pairs]), arr(c_i, [_ld(A) for A, _ in pairs]),
+            arr(c_p, [B.data_ptr() for _, B in pairs]), arr(c_i, [_ld(B) for _, B in pairs]))
+    if any(io):                              # the bf16 mode's bf16 activations
+        rc = lib.hsg_gemm_dw_slabs_io(n, *dims, arr(c_i, io), splits, arr(c_p, [w.data_ptr() for w in ws]),
+                                      stream_of(pairs[0][0]))
+    else:
+        rc = lib.hsg_gemm_dw_slabs(n, *dims, splits, int(_GEMM_DTYPE == "bf16"), arr(c_p, [w.data_ptr() for w in ws]),
+                                   stream_of(pairs[0][0]))
     if rc == HSG_EINVAL:
         return None
     check(rc, "hsg_gemm_dw_slabs")

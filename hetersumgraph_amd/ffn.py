@@ -161,8 +161,13 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
     else:
         nb = lib.hsg_ln_bwd_blocks(n)
         part = x.new_empty(nb, 3, d)
-        check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
-                             ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
+        if dy.dtype == torch.bfloat16:       # the bf16 mode's bf16 dy rows (zero pad to ceil8(d))
+            check(lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                                      ptr(seed_t), off, ptr(dy), dy.stride(0), ptr(dx), ptr(part), st),
+                  "hsg_ln_bwd_dy16")
+        else:
+            check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                                 ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
         rt = psw_row_tiles(n, d_hid, d, wsplit[2].mode) if wsplit is not None else row_tiles(n, d_hid, d)
         hpart = x.new_empty(rt, d_hid)
         dH_out = act_grads[1] if act_grads is not None else None

@@ -295,13 +295,19 @@ class _GatStack(torch.autograd.Function):
             key = id(lay)
             if key not in bufs:
                 d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
-                bufs[key] = (states[org].new_empty(n_app[key], rel.n_dst, d),
-                             states[org].new_empty(n_app[key], rel.n_dst, d_hid))
+                X = states[org].new_empty(n_app[key], rel.n_dst, d)
                 # the FFN weights split into limb planes once per forward (hsg_wsplit),
                 # unless the prologue launch already did
                 if key not in wsplits:
-                    wsplits[key] = ffn_wsplit(bufs[key][0][0], lay.w1.view(d_hid, d), lay.b1,
-                                              lay.w2.view(d, d_hid), lay.b2)
+                    wsplits[key] = ffn_wsplit(X[0], lay.w1.view(d_hid, d), lay.b1, lay.w2.view(d, d_hid), lay.b2)
+                # the bf16 GEMM mode keeps the wide FFN's hidden activations H as bf16
+                # (with dY and dH in the backward): they are only GEMM operands there,
+                # rounded to bf16 by the GEMM anyway -- half their bytes, the same numbers
+                # (HSG_FFN_BF16_ACT=0: fp32 buffers, for the bitwise A/B test)
+                bf = (wsplits[key] is not None and wsplits[key][0].mode == "bf16"
+                      and _lib.path_option("HSG_FFN_BF16_ACT", "1") != "0")
+                bufs[key] = (X, X.new_empty(n_app[key], rel.n_dst, d_hid,
+                                            dtype=torch.bfloat16 if bf else torch.float32))
             a = slot[key]
             slot[key] += 1
             out, saved = _apply_fwd(lay, rel, T, states[nb], states[org], tables[key], x_out=bufs[key][0][a],
@@ -360,7 +366,12 @@ class _GatStack(torch.autograd.Function):
             stage = (batch, id(lay), stages[id(lay)][1])
             if id(lay) not in gbufs:
                 X, Hh = ctx.bufs[id(lay)]
-                gbufs[id(lay)] = (lay, torch.empty_like(X), torch.empty_like(Hh))
+                if Hh.dtype == torch.bfloat16:       # bf16 dY rows padded to a multiple of 8 (zeros)
+                    d = X.shape[2]
+                    DY = X.new_empty(X.shape[0], X.shape[1], (d + 7) // 8 * 8, dtype=torch.bfloat16)[:, :, :d]
+                else:
+                    DY = torch.empty_like(X)
+                gbufs[id(lay)] = (lay, DY, torch.empty_like(Hh))
             _, DY, DH = gbufs[id(lay)]
             dx = _apply_bwd(pgrads, lay, T, saved, dout, nb_grad, nb_acc, stage, act_grads=(DY[a], DH[a]),
                             batch=batch)
@@ -378,7 +389,9 @@ class _GatStack(torch.autograd.Function):
             X, Hh = ctx.bufs[id(lay)]
             d_hid, d = lay.w1.shape[0], lay.w1.shape[1]
             todo = []
-            for p, A, B, (m, n) in ((lay.w2, DY.view(-1, d), Hh.view(-1, d_hid), (d, d_hid)),
+            DYf = DY.reshape(-1, DY.shape[2]) if DY.is_contiguous() else \
+                DY.as_strided((DY.shape[0] * DY.shape[1], DY.shape[2]), (DY.stride(1), 1))
+            for p, A, B, (m, n) in ((lay.w2, DYf, Hh.view(-1, d_hid), (d, d_hid)),
                                     (lay.w1, DH.view(-1, d_hid), X.view(-1, d), (d_hid, d))):
                 dw, a_w = pgrads.dst(p)
                 if dw is not None:

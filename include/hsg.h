@@ -279,6 +279,24 @@ int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const vo
 int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
                       const float *bias, const float *aux, int ldaux, int epi, int relu, float *colsum_part,
                       void *stream);
+/* The bf16 mode's FFN GEMMs on bf16 activations (round 5): hsg_gemm_bf16_psw with A,
+ * C and the relu' mask aux given as bf16 rows per io = HSG_IO_A_BF16 | HSG_IO_C_BF16 |
+ * HSG_IO_AUX_BF16 (io in {0, 1, 2, 7}; element strides lda / ldc / ldaux).  A bf16 A
+ * needs lda % 8 == 0, 16-byte alignment and zeros in its columns K .. ceil8(K) - 1; a
+ * bf16 C takes no accumulate epilogue, a bf16 aux only the relu' mask.  The bf16 mode
+ * rounds A to bf16 at fragment read anyway, so the products equal hsg_gemm_bf16_psw's on
+ * the same values; a bf16 C is the fp32 result rounded to nearest even. */
+#define HSG_IO_A_BF16 1
+#define HSG_IO_C_BF16 2
+#define HSG_IO_AUX_BF16 4
+int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void *planes, void *C, int ldc,
+                         const float *bias, const void *aux, int ldaux, int epi, int relu, float *colsum_part,
+                         int io, void *stream);
+/* hsg_gemm_psw_elug_rho in the bf16 mode with a bf16 A (the FFN's bf16 dH rows; the
+ * bf16 A contract above). */
+int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
+                                   int ldc, const float *aux, const float *x, const float *origin, float *G, int ld,
+                                   float *rho, int head_dim, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
@@ -318,6 +336,13 @@ int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16);
  * slice non-empty (ceil(ceil(K/32) / ceil(ceil(K/32)/splits)) == splits). */
 int hsg_gemm_dw_slabs(int njobs, const int *M, const int *N, int K, const float *const *A, const int *lda,
                       const float *const *B, const int *ldb, int splits, int bf16, float *const *ws, void *stream);
+/* hsg_gemm_dw_slabs in the bf16 mode with bf16 operands (round 5): io[q] bit 0 -- A_q is
+ * bf16 rows, bit 1 -- B_q is bf16 rows (element strides; 8-byte quads, M / N / ld
+ * multiples of 4, 16-byte aligned).  The products equal the bf16 mode's on the same
+ * values. */
+int hsg_gemm_dw_slabs_io(int njobs, const int *M, const int *N, int K, const void *const *A, const int *lda,
+                         const void *const *B, const int *ldb, const int *io, int splits, float *const *ws,
+                         void *stream);
 /* Output tiles of one hsg_gemm_dw_slabs job of shape M x N (blocks = tiles x splits). */
 int hsg_gemm_dw_tiles(int M, int N);
 /* Deferred column sums of partial slabs, njobs (1..24) outputs in one deterministic
@@ -393,6 +418,13 @@ int hsg_ln_fwd(int n, int d, const float *y, const float *x, const float *gamma,
 int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                float *dy, float *dx, float *part, void *stream);
+/* hsg_ln_bwd with dy stored as bf16 rows of pitch ld_dy (the bf16 GEMM mode, where dy is
+ * only a GEMM operand): zeros in its columns d .. ceil8(d) - 1; the vector kernel's
+ * shapes only (d % 4 == 0, 257..512 columns, 16-byte aligned rows, ld_dy % 8 == 0),
+ * HSG_EINVAL otherwise.  dx and the partials as hsg_ln_bwd (db2 sums the fp32 dy). */
+int hsg_ln_bwd_dy16(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+                    const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
+                    void *dy, int ld_dy, float *dx, float *part, void *stream);
 
 /* ---- head projection with per-head input dropout (GATStackLayer.py:56) ----------
  * Training-mode  z_k = fc_k(dropout_k(h))  for all heads without materialising the

@@ -516,3 +516,118 @@ def test_psw_ln_declines_without_plan():
     v = torch.ones(N, device="cuda")
     assert not gemm_psw_ln(A, S, v, t, v, v, 1e-5, 0.0, None, 0, t.clone(), t.clone(), torch.empty(M, device="cuda"),
                            torch.empty(M, device="cuda"))
+
+
+# ---- the bf16 mode on bf16 activations (round 5) -----------------------------------
+def _bf16_rows(t, pad_to=8):
+    """t as bf16 rows with the pitch rounded up to ``pad_to`` (zeros in the pad)."""
+    n, d = t.shape
+    ld = (d + pad_to - 1) // pad_to * pad_to
+    buf = torch.zeros(n, ld, dtype=torch.bfloat16, device=t.device)
+    buf[:, :d] = t.bfloat16()
+    return buf[:, :d]
+
+
+@pytest.mark.parametrize("M,N,K", [(28800, 512, 300), (28800, 300, 512), (777, 512, 300), (130, 64, 96)])
+def test_bf16_io_gemms_bitwise_equal_fp32_io(M, N, K):
+    """hsg_gemm_bf16_psw_io against hsg_gemm_bf16_psw on the same values: a bf16 A
+    (io 1) holds exactly what the fp32-A path rounds at fragment read, a bf16 C (io 2)
+    is the fp32 result rounded to nearest even, a bf16 relu' mask (io 4) gates as the
+    fp32 one (RNE keeps the sign): bitwise equal, column partials too."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw, psw_row_tiles, split_weights
+    torch.manual_seed(M + N + K)
+    A = mk(M, K)
+    Ab = _bf16_rows(A)
+    A_r = Ab.float().contiguous()                       # the same values as fp32 rows
+    W = mk(N, K) * 0.5
+    with gemm_dtype("bf16"):
+        (S,) = split_weights((W, False))
+    bias = torch.randn(N, device="cuda")
+    # io 2: x W^T + b, relu -> bf16 C
+    ref = gemm_psw(A, S, bias=bias, relu=True)
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    gemm_psw(A, S, bias=bias, relu=True, out=Cb)
+    assert torch.equal(Cb, ref.bfloat16())
+    # io 1: bf16 A -> fp32 C
+    assert torch.equal(gemm_psw(Ab, S, bias=bias), gemm_psw(A_r, S, bias=bias))
+    # io 7: bf16 A, bf16 relu' mask, bf16 C, column partials
+    Hm = torch.randn(M, N, device="cuda")
+    rt = psw_row_tiles(M, N, K, "bf16")
+    p1, p2 = torch.empty(rt, N, device="cuda"), torch.empty(rt, N, device="cuda")
+    ref = gemm_psw(A_r, S, relu_mask=Hm.bfloat16().float(), colsum_part=p1)
+    Cb = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    gemm_psw(Ab, S, relu_mask=Hm.bfloat16(), colsum_part=p2, out=Cb)
+    torch.cuda.synchronize()
+    assert torch.equal(Cb, ref.bfloat16()) and torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("M", [28800, 777])
+def test_bf16_io_elug_rho_bitwise(M):
+    """The dx GEMM with the ELU gate and rho on a bf16 dH (hsg_gemm_bf16_psw_elug_rho_a16)
+    against the fp32-A call on the same values: bitwise equal dx, G and rho."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    N, K, D = 300, 512, 50
+    torch.manual_seed(M)
+    dH = torch.randn(M, K, device="cuda")
+    dHb = _bf16_rows(dH)
+    W1 = torch.randn(K, N, device="cuda") / K ** 0.5
+    with gemm_dtype("bf16"):
+        (S,) = split_weights((W1, True))
+    ds = torch.randn(M, N, device="cuda")
+    origin = torch.randn(M, N, device="cuda")
+    x = torch.nn.functional.elu(2 * torch.randn(M, N, device="cuda")) + origin
+    outs = []
+    for A in (dHb.float().contiguous(), dHb):
+        out, G = ds.clone(), torch.empty_like(ds)
+        rho = torch.empty(M, (N + 63) // 64, 3, device="cuda")
+        assert gemm_psw_elug(A, S, out, x, origin, G, rho, D)
+        outs.append((out, G, rho))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,p_drop", [(28800, 0.1), (1001, 0.0)])
+def test_ln_bwd_bf16_dy_bitwise(n, p_drop):
+    """hsg_ln_bwd_dy16: dy stored as bf16 rows (pitch 304, zero pad) = RNE of
+    hsg_ln_bwd's fp32 dy; dx and the dgamma / dbeta / db2 partials bitwise equal."""
+    from hetersumgraph_amd import rng as hsg_rng
+    from hetersumgraph_amd._lib import load, ptr
+    lib = load()
+    d = 300
+    torch.manual_seed(n)
+    dout, y, x = (torch.randn(n, d, device="cuda") for _ in range(3))
+    gamma = 1 + 0.1 * torch.randn(d, device="cuda")
+    mean, rstd = torch.randn(n, device="cuda"), torch.rand(n, device="cuda") + 0.5
+    hsg_rng.manual_seed(5)
+    seed_t, off = hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0)
+    nb = lib.hsg_ln_bwd_blocks(n)
+    dy, dx, part = torch.empty_like(x), torch.empty_like(x), x.new_empty(nb, 3, d)
+    assert lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop, ptr(seed_t),
+                          off, ptr(dy), ptr(dx), ptr(part), None) == 0
+    dyb = torch.full((n, 304), float("nan"), device="cuda").bfloat16()
+    dx2, part2 = torch.empty_like(x), torch.empty_like(part)
+    assert lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                               ptr(seed_t), off, ptr(dyb), 304, ptr(dx2), ptr(part2), None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dyb[:, :d], dy.bfloat16()) and torch.equal(dyb[:, d:].float(), torch.zeros(n, 4, device="cuda"))
+    assert torch.equal(dx, dx2) and torch.equal(part, part2)
+
+
+def test_dw_pair_bf16_operands_bitwise():
+    """hsg_gemm_dw_slabs_io (bf16 dY, H, dH; fp32 X) against hsg_gemm_dw_slabs in the
+    bf16 mode on the same values: bitwise equal partial slabs."""
+    from hetersumgraph_amd.dense import gemm_dtype, gemm_dw_slabs
+    K, d, dh = 38400, 300, 512
+    torch.manual_seed(3)
+    DY = _bf16_rows(torch.randn(K, d, device="cuda"))
+    Hh = torch.randn(K, dh, device="cuda").bfloat16()
+    DH = torch.randn(K, dh, device="cuda").bfloat16()
+    X = torch.randn(K, d, device="cuda")
+    with gemm_dtype("bf16"):
+        a = gemm_dw_slabs([(DY, Hh), (DH, X)])
+        b = gemm_dw_slabs([(DY.float().contiguous(), Hh.float()), (DH.float(), X)])
+    torch.cuda.synchronize()
+    assert a is not None and b is not None
+    for (wa, sa), (wb, sb) in zip(a, b):
+        assert sa == sb and torch.equal(wa, wb)
