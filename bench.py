@@ -724,7 +724,12 @@ def main(backend_cls=HipBench):
         "config": {"workload": f"{args.config}: HSG WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) fwd+bwd, "
                                f"train mode, {workload_shape(args.config)}",
                    "gemm_operands": args.dtype,
-                   "edge_kernels_ln_head_projection": "f32",
+                   "bf16_rows": ("wide (S2W) FFN hidden H, its output y (LayerNorm input), dY, dH and the "
+                                 "edge gate G rows; one RNE rounding each, GEMM operands rounded anyway"
+                                 if args.dtype == "bf16" else "none"),
+                   "f32_rows": ("node states, edge softmax state (sigma, m, l), head projection, narrow "
+                                "(W2S) FFN, LayerNorm statistics, parameters and gradients"
+                                if args.dtype == "bf16" else "all"),
                    "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
                    "typed_edges_per_direction": be.n_typed,
                    "dropout": args.dropout, "parallelism": f"dp{world}", "dp_exchange": dp_exchange,

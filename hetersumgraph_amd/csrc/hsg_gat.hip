@@ -1167,7 +1167,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
 // dsigma_u,k and (one lane) the box's d tau.  The waves' partials are combined in wave
 // order; d tau and d a1 leave as per-block partials: deterministic.  Replaces the
 // hsg_gat_bwd_dst_g + hsg_gat_bwd_src pair (G read once, no dpre round trip).
-template <int NE, int OCC = 1, int EQ = 4>
+// GBF (round 5, the bf16 GEMM mode): G comes as bf16 rows (hsg_gemm_bf16_psw_elug_rho_a16
+// with g_bf16), held raw until the edge uses them.
+template <int NE, int OCC = 1, int EQ = 4, bool GBF = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, int D, int lph, float slope,
                                                       const float *__restrict__ sigma,
                                                       const float *__restrict__ tau,
@@ -1241,19 +1243,30 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
             #pragma unroll 1
             for (int j0 = 0; j0 < nb; j0 += EQ) {
                 float gv[EQ][NE];
+                __bf16 gb[GBF ? EQ : 1][GBF ? NE : 1];
 #pragma unroll
                 for (int q = 0; q < EQ; ++q) {
                     // lane j = (head 0, l = j) holds edge j's destination; scalar row base,
                     // per-lane feature offsets shared by every row (saddr + voffset loads)
                     const int v = __builtin_amdgcn_readfirstlane(__shfl(vA, min(j0 + q, nb - 1)));
-                    const float *gr = G + (size_t)v * HD;
+                    if constexpr (GBF) {
+                        const __bf16 *gr = reinterpret_cast<const __bf16 *>(G) + (size_t)v * HD;
 #pragma unroll
-                    for (int i = 0; i < NE; ++i) gv[q][i] = gr[fo[i]];
+                        for (int i = 0; i < NE; ++i) gb[q][i] = gr[fo[i]];
+                    } else {
+                        const float *gr = G + (size_t)v * HD;
+#pragma unroll
+                        for (int i = 0; i < NE; ++i) gv[q][i] = gr[fo[i]];
+                    }
                 }
 #pragma unroll
                 for (int q = 0; q < EQ; ++q) {
                     const int j = j0 + q;
                     if (j >= nb) break;                        // wave-uniform
+                    if constexpr (GBF) {
+#pragma unroll
+                        for (int i = 0; i < NE; ++i) gv[q][i] = (float)gb[q][i];
+                    }
                     float dot = 0.f;
 #pragma unroll
                     for (int i = 0; i < NE; ++i) dot = fmaf(gv[q][i], zk[i], dot);     // zk = 0 past D
@@ -2073,10 +2086,27 @@ int hsg_gat_bwd_src_g_blocks(const hsg_rel *rel, int H, int D) {
     return grid_nodes(rel->n_src, 4, kBwdSrcGridCap);        // one source per block per iteration
 }
 
+// the wide one-pass kernel on bf16 G rows (the bf16 GEMM mode): g_bf16 != 0 needs the
+// wide form (rho_groups > 0); HSG_EINVAL otherwise
+int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                         const float *m, const float *l, const void *G, int g_bf16, const float *rho, int rho_groups,
+                         const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                         float *dtau_part, void *stream);
+
 int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
                       const float *m, const float *l, const float *G, const float *rho, int rho_groups,
                       const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                       float *dtau_part, void *stream) {
+    return hsg_gat_bwd_src_g_io(rel, H, D, slope, sigma, tau, m, l, G, 0, rho, rho_groups, a1, Z, dZ, dsigma,
+                                da1_part, dtau_part, stream);
+}
+
+int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                         const float *m, const float *l, const void *Gv, int g_bf16, const float *rho, int rho_groups,
+                         const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                         float *dtau_part, void *stream) {
+    const float *G = reinterpret_cast<const float *>(Gv);
+    if (g_bf16 && rho_groups == 0) return HSG_EINVAL;
     if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !G || !rho || !Z || !dZ || !dtau_part) return HSG_EINVAL;
     const RelPtrs R = rel_ptrs(rel);
     const dim3 grid(hsg_gat_bwd_src_g_blocks(rel, H, D));
@@ -2096,8 +2126,12 @@ int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float
     if (!srcg_wide(rel, H, D) || rho_groups != (H * D + 63) / 64) return HSG_EINVAL;
     const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;
 #define HSG_SG(NE_, OCC_, EQ_)                                                                               \
-    HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope, sigma,   \
-                tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part)
+    if (g_bf16)                                                                                              \
+        HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_, true>), grid, dim3(256), st, R, H, D, lph,   \
+                    slope, sigma, tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part);    \
+    else                                                                                                     \
+        HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope,  \
+                    sigma, tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part)
     // EQ: destination rows in flight per wave, as many as fit 5 blocks per CU unspilled
 #ifdef HSG_DEV
     const char *eq = HSG_DEV_ENV("HSG_SRCG_EQ");                               // dev A/B

@@ -960,7 +960,9 @@ typedef __bf16 bf16x4v7 __attribute__((ext_vector_type(4)));
 
 // CBF / AUXBF (the bf16 mode's bf16 activations, round 5): C is stored and the aux
 // operand (the relu' mask H) read as bf16 quads (8 B) at the same element offsets
-template <int BN, bool CBF = false, bool AUXBF = false>
+// GBF: the ELU-gate epilogue's G rows stored as bf16 (the bf16 mode; rho is summed from
+// the fp32 G before the rounding)
+template <int BN, bool CBF = false, bool AUXBF = false, bool GBF = false>
 struct EpiRows {
     static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
     static constexpr int STEPS = (32 + RPS - 1) / RPS;
@@ -1051,7 +1053,11 @@ struct EpiRows {
                     f32x4 g;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) g[e] = ex[t][e] > 0.f ? v[e] : v[e] * (ex[t][e] + 1.f);
-                    *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
+                    if constexpr (GBF)
+                        *reinterpret_cast<bf16x4v7 *>(reinterpret_cast<__bf16 *>(p.C2) + (size_t)m * p.ldaux + n) =
+                            bf16x4v7{(__bf16)g[0], (__bf16)g[1], (__bf16)g[2], (__bf16)g[3]};
+                    else
+                        *reinterpret_cast<f32x4 *>(p.C2 + (size_t)m * p.ldaux + n) = g;
                     if (rho) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
@@ -1312,7 +1318,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm5(GemmArgs p, const __bf16 *__re
 template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false, int IO = 0>
 __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
-    constexpr bool ABF = (IO & 1) != 0, CBF = (IO & 2) != 0, AUXBF = (IO & 4) != 0;
+    constexpr bool ABF = (IO & 1) != 0, CBF = (IO & 2) != 0, AUXBF = (IO & 4) != 0, GBF = (IO & 8) != 0;
     static_assert(!ABF || (PM == 2 && !SA), "bf16 A: the bf16 mode's one-product path");
     constexpr int A_FL = ABF ? BM * 16 : BM * 32;          // floats of the A tile
     constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
@@ -1341,7 +1347,7 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
-    EpiRows<BN, CBF, AUXBF> ep;
+    EpiRows<BN, CBF, AUXBF, GBF> ep;
 
     uint32_t aoff[BM / 32], boff[NBP];
     if constexpr (SA) {
@@ -2649,6 +2655,8 @@ static int launch7io(GemmArgs p, const __bf16 *pl, int Np, int Kp, int io, hipSt
     case 1: return wide ? launch7<128, 2, 2, 2, false, 1>(p, pl, Np, Kp, st) : launch7io_narrow<1>(p, pl, Np, Kp, st);
     case 2: return wide ? launch7<128, 2, 2, 2, false, 2>(p, pl, Np, Kp, st) : launch7io_narrow<2>(p, pl, Np, Kp, st);
     case 7: return wide ? launch7<128, 2, 2, 2, false, 7>(p, pl, Np, Kp, st) : launch7io_narrow<7>(p, pl, Np, Kp, st);
+    case 3: return wide ? launch7<128, 2, 2, 2, false, 3>(p, pl, Np, Kp, st) : launch7io_narrow<3>(p, pl, Np, Kp, st);
+    case 9: return wide ? launch7<128, 2, 2, 2, false, 9>(p, pl, Np, Kp, st) : launch7io_narrow<9>(p, pl, Np, Kp, st);
     default: return HSG_EINVAL;
     }
 }
@@ -2732,7 +2740,7 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
                          const float *bias, const void *aux, int ldaux, int epi, int relu, float *colsum_part,
                          int io, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C || !planes || !A) return HSG_EINVAL;
-    if (io != 0 && io != 1 && io != 2 && io != 7) return HSG_EINVAL;
+    if (io != 0 && io != 1 && io != 2 && io != 3 && io != 7) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && epi != HSG_EPI_RELU_BWD && epi != HSG_EPI_ADD) return HSG_EINVAL;
     if (epi != HSG_EPI_STORE && !aux) return HSG_EINVAL;
     if ((io & 4) && epi != HSG_EPI_RELU_BWD) return HSG_EINVAL;           // a bf16 aux is a relu' mask
@@ -2784,8 +2792,8 @@ int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const vo
 // hsg_gemm_psw_elug_rho in the bf16 mode on a bf16 A (the FFN's bf16 dH rows; lda %
 // 8 == 0, 16-byte aligned, columns K .. ceil8(K) - 1 zero)
 int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
-                                   int ldc, const float *aux, const float *x, const float *origin, float *G, int ld,
-                                   float *rho, int head_dim, void *stream) {
+                                   int ldc, const float *aux, const float *x, const float *origin, void *G, int ld,
+                                   float *rho, int head_dim, int g_bf16, void *stream) {
     if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G) return HSG_EINVAL;
     if ((lda & 7) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N) return HSG_EINVAL;
     if (rho && (head_dim < 32 || N % head_dim)) return HSG_EINVAL;
@@ -2793,11 +2801,11 @@ int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, 
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
     GemmArgs p{M, N, K, reinterpret_cast<const float *>(A), lda, nullptr, 0, C, ldc, nullptr, aux, ld,
-               HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr, 1, 1, x, origin, G};
+               HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr, 1, 1, x, origin, reinterpret_cast<float *>(G)};
     p.rho = rho;
     p.rho_d = head_dim;
     if (!epi_rows_ok(p)) return HSG_EINVAL;
-    return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, 1, (hipStream_t)stream);
+    return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, g_bf16 ? 9 : 1, (hipStream_t)stream);
 }
 
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,

@@ -142,7 +142,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__re
 // every load first, then every store).  Same arithmetic per row (bitwise equal,
 // tests/test_gpu_ffn.py).  cfg2 in-step at 1,536 blocks: 15.6-15.8 vs 17.7 us per launch
 // (profiles/r04_dev/ln_fwdp/); dev: HSG_LN_FWDP=<blocks> (0: k_ln_fwd4), HSG_LN_FWDP_R=2.
-template <int NV, int RPW>
+// YBF (round 5, the bf16 GEMM mode): y -- the wide FFN's output, the LayerNorm input --
+// comes as bf16 rows (pitch d), kept as raw quads until the row is consumed (a
+// conversion at the load would wait for the prefetch at once).
+template <int NV, int RPW, bool YBF = false>
 __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__restrict__ y,
                                                   const float *__restrict__ x, const float *__restrict__ gamma,
                                                   const float *__restrict__ beta, float eps, float p_drop,
@@ -157,6 +160,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     f32x4r yv[RPW][NV], xv[RPW][NV];
+    bf16x4r yb[YBF ? RPW : 1][YBF ? NV : 1];
     auto load = [&](int gg) {
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -164,7 +168,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
 #pragma unroll
             for (int i = 0; i < NV; ++i) {
                 const int c = min(4 * lane + 256 * i, d - 4);        // clamped: unused past d
-                yv[q][i] = *reinterpret_cast<const f32x4r *>(y + (size_t)r * d + c);
+                if constexpr (YBF)
+                    yb[q][i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + (size_t)r * d + c);
+                else
+                    yv[q][i] = *reinterpret_cast<const f32x4r *>(y + (size_t)r * d + c);
                 xv[q][i] = *reinterpret_cast<const f32x4r *>(x + (size_t)r * d + c);
             }
         }
@@ -183,7 +190,9 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
                 s[q][i] = f32x4r{0.f, 0.f, 0.f, 0.f};
                 if (c < d) {
                     const size_t o = (size_t)r * d + c;
-                    f32x4r v = yv[q][i];
+                    f32x4r v;
+                    if constexpr (YBF) v = f32x4r{(float)yb[q][i][0], (float)yb[q][i][1], (float)yb[q][i][2], (float)yb[q][i][3]};
+                    else v = yv[q][i];
                     if (p_drop > 0.f) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e)
@@ -329,7 +338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
 // dW2 = dy^T H, both on bf16-rounded operands) -- is stored as bf16 rows of pitch ld_dy
 // (>= ceil8(d)), the pad columns d .. ceil8(d) - 1 zero (the bf16-A contract of
 // hsg_gemm_bf16_psw_io); db2 still sums the fp32 values.
-template <int NV, bool DYBF = false>
+template <int NV, bool DYBF = false, bool YBF = false>
 __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__restrict__ dout,
                                                   const float *__restrict__ y, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ mean,
@@ -355,6 +364,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
     const int nw = gridDim.x * 4;
     int r = blockIdx.x * 4 + wid;
     f32x4r yv[NV], xv[NV], gv[NV];
+    bf16x4r yb[YBF ? NV : 1];                                        // YBF: bf16 y rows, raw until used
     float mu = 0.f, rs = 0.f;
     auto load = [&](int rr) {
         mu = mean[rr];
@@ -362,7 +372,8 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             const size_t o = (size_t)rr * d + cq[i];
-            yv[i] = *reinterpret_cast<const f32x4r *>(y + o);
+            if constexpr (YBF) yb[i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + o);
+            else yv[i] = *reinterpret_cast<const f32x4r *>(y + o);
             xv[i] = *reinterpret_cast<const f32x4r *>(x + o);
             gv[i] = *reinterpret_cast<const f32x4r *>(dout + o);
         }
@@ -380,7 +391,9 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
             if (cok[i]) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    float v = yv[i][e];
+                    float v;
+                    if constexpr (YBF) v = (float)yb[i][e];
+                    else v = yv[i][e];
                     if (p_drop > 0.f) {
                         const bool k = hsg_keep32(dkey, (uint32_t)(rb + cq[i] + e), thr);
                         if (!k) keep &= ~(1u << (4 * i + e));
@@ -592,7 +605,7 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
 // hsg_ln_bwd with dy stored as bf16 rows (the bf16 GEMM mode's bf16 activations): the
 // vector kernel's shapes only (d % 4 == 0, 257..512 columns, 16-byte aligned fp32 rows,
 // ld_dy % 8 == 0 and >= ceil8(d), 16-byte aligned dy), HSG_EINVAL otherwise.
-int hsg_ln_bwd_dy16(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+int hsg_ln_bwd_dy16(int n, int d, const float *dout, const void *y, int y_bf16, const float *x, const float *gamma,
                     const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                     void *dy, int ld_dy, float *dx, float *part, void *stream) {
     const auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
@@ -603,8 +616,32 @@ int hsg_ln_bwd_dy16(int n, int d, const float *dout, const float *y, const float
     hipStream_t st = (hipStream_t)stream;
     dim3 grid(grid_rows(n, ln_bwd_cap())), block(256);
     if (n == 0) return (int)hipMemsetAsync(part, 0, sizeof(float) * 3 * d * grid.x, st);
-    hipLaunchKernelGGL((k_ln_bwd4p<2, true>), grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, seed,
-                       offset, reinterpret_cast<float *>(dy), dx, part, ld_dy);
+    const float *yf = reinterpret_cast<const float *>(y);
+    if (y_bf16)
+        hipLaunchKernelGGL((k_ln_bwd4p<2, true, true>), grid, block, 0, st, n, d, dout, yf, x, gamma, mean, rstd,
+                           p_drop, seed, offset, reinterpret_cast<float *>(dy), dx, part, ld_dy);
+    else
+        hipLaunchKernelGGL((k_ln_bwd4p<2, true>), grid, block, 0, st, n, d, dout, yf, x, gamma, mean, rstd, p_drop,
+                           seed, offset, reinterpret_cast<float *>(dy), dx, part, ld_dy);
+    return status();
+}
+
+// hsg_ln_fwd with y given as bf16 rows (pitch d; the bf16 GEMM mode's FFN output): the
+// persistent vector kernel's shapes only (d % 4 == 0, 257..512 columns, 16-byte aligned
+// fp32 rows, 8-byte aligned y), HSG_EINVAL otherwise.  out, mean, rstd as hsg_ln_fwd on
+// the bf16 values of y.
+int hsg_ln_fwd_y16(int n, int d, const void *y, const float *x, const float *gamma, const float *beta, float eps,
+                   float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
+                   void *stream) {
+    const auto al = [](const void *q, uintptr_t a) { return ((uintptr_t)q & (a - 1)) == 0; };
+    if (d % 4 || (d + 255) / 256 != 2 || d <= 256 || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) ||
+        (p_drop > 0.f && (long)n * d >= (1L << 32)) || !al(y, 8) || !al(x, 16) || !al(out, 16) || !al(gamma, 16) ||
+        !al(beta, 16))
+        return HSG_EINVAL;
+    if (n == 0) return 0;
+    const int blocks = kLnFwdPBlocks < (n + 3) / 4 ? kLnFwdPBlocks : (n + 3) / 4;
+    hipLaunchKernelGGL((k_ln_fwd4p<2, 1, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, d,
+                       reinterpret_cast<const float *>(y), x, gamma, beta, eps, p_drop, seed, offset, out, mean, rstd);
     return status();
 }
 

@@ -235,12 +235,16 @@ def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
         return False
     if rho is not None and (rho.shape != (M, (N + 63) // 64, 3) or not rho.is_contiguous()):
         return False
+    if rho is not None and rho.dtype != torch.float32:
+        raise RuntimeError("gemm_psw_elug: rho partials are fp32")
+    if G.dtype == torch.bfloat16 and A.dtype != torch.bfloat16:
+        raise RuntimeError("gemm_psw_elug: bf16 G rows come with the bf16 mode's bf16 dH")
     if A.dtype == torch.bfloat16:                # the bf16 mode's bf16 dH rows
         if Bs.mode != "bf16":
             raise RuntimeError("gemm_psw_elug: bf16 activations belong to the 'bf16' GEMM mode")
         rc = lib.hsg_gemm_bf16_psw_elug_rho_a16(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out),
                                                 ptr(x), ptr(origin), ptr(G), N, ptr(rho), int(head_dim),
-                                                stream_of(A))
+                                                int(G.dtype == torch.bfloat16), stream_of(A))
     else:
         rc = lib.hsg_gemm_psw_elug_rho(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
                                        ptr(origin), ptr(G), N, ptr(rho), int(head_dim), int(Bs.mode == "bf16"),

@@ -102,6 +102,14 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
         if b2 is not None and gemm_psw_ln(H, wsplit[1], b2, x, gamma, beta, eps, p_drop, seed_t, off, y, out,
                                           mean, rstd):
             return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
+        if H.dtype == torch.bfloat16 and _lib.path_option("HSG_FFN_BF16_ROWS", "1") != "0":
+            # the bf16 GEMM mode's bf16 activations: the FFN output y (the LayerNorm
+            # input) as bf16 too -- rounded once, <= 2^-9 |y| per element
+            y = x.new_empty(n, d, dtype=torch.bfloat16)
+            gemm_psw(H, wsplit[1], bias=b2, out=y)
+            check(lib.hsg_ln_fwd_y16(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
+                                     ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd_y16")
+            return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
         gemm_psw(H, wsplit[1], bias=b2, out=y)                   # [n, d]
         check(lib.hsg_ln_fwd(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), float(eps), float(p_drop),
                              ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)), "hsg_ln_fwd")
@@ -162,9 +170,9 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
         nb = lib.hsg_ln_bwd_blocks(n)
         part = x.new_empty(nb, 3, d)
         if dy.dtype == torch.bfloat16:       # the bf16 mode's bf16 dy rows (zero pad to ceil8(d))
-            check(lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
-                                      ptr(seed_t), off, ptr(dy), dy.stride(0), ptr(dx), ptr(part), st),
-                  "hsg_ln_bwd_dy16")
+            check(lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), int(y.dtype == torch.bfloat16), ptr(x), ptr(gamma),
+                                      ptr(mean), ptr(rstd), p_drop, ptr(seed_t), off, ptr(dy), dy.stride(0), ptr(dx),
+                                      ptr(part), st), "hsg_ln_bwd_dy16")
         else:
             check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
                                  ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")

@@ -212,6 +212,10 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
     merged = rho is not None
     if merged and not g_given:
         raise ValueError("gat_table_bwd: rho partials without their G rows")
+    if merged and rho.dtype != torch.float32:
+        raise ValueError("gat_table_bwd: rho partials are fp32")
+    if G.dtype == torch.bfloat16 and not merged:
+        raise ValueError("gat_table_bwd: bf16 G rows are read by the one-pass backward only")
     nbs = lib.hsg_gat_bwd_src_g_blocks(relp, H, D) if merged else lib.hsg_gat_bwd_src_blocks(relp)
     nbd = nbs if merged else lib.hsg_gat_bwd_blocks(relp)
     dtp = Z.new_empty(nbd, N_BOX + 1, H)
@@ -224,9 +228,14 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
         if merged:                          # one source-centric pass (G and rho from the FFN epilogue)
             # rho [n_dst, groups, 3]: 64-column-group partials (wide heads); [n_dst, H]: per head
             groups = rho.shape[1] if rho.dim() == 3 else 0
-            check(lib.hsg_gat_bwd_src_g(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G), ptr(rho),
-                                        groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp), st),
-                  "hsg_gat_bwd_src_g")
+            if G.dtype == torch.bfloat16:   # the bf16 GEMM mode's bf16 G rows
+                check(lib.hsg_gat_bwd_src_g_io(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G), 1,
+                                               ptr(rho), groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p),
+                                               ptr(dtp), st), "hsg_gat_bwd_src_g_io")
+            else:
+                check(lib.hsg_gat_bwd_src_g(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G),
+                                            ptr(rho), groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp),
+                                            st), "hsg_gat_bwd_src_g")
         else:
             dpre = Z.new_empty(rel.n_typed, H)
             if g_given:                     # G from the FFN epilogue (forward without h)

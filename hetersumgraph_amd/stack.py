@@ -193,12 +193,17 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     # forward without h and the FFN on the pre-split path: the G rows of the edge
     # backward come out of the FFN's last GEMM (dx epilogue)
     G = rho = None
-    elug = (gsaved[16][1], torch.empty_like(fsaved[0])) if gsaved[16] is not None and fsaved[11] is not None \
-        else None
-    if elug is not None and _merged_bwd(gsaved):
+    # (the bf16 GEMM mode's bf16 activations, fsaved[4] = H bf16: G bf16 too when the one
+    # source-centric backward -- the only reader that takes bf16 G -- runs)
+    merged = gsaved[16] is not None and fsaved[11] is not None and _merged_bwd(gsaved)
+    gdt = torch.bfloat16 if (merged and fsaved[4].dtype == torch.bfloat16
+                             and _lib.path_option("HSG_FFN_BF16_ROWS", "1") != "0") else torch.float32
+    elug = (gsaved[16][1], torch.empty_like(fsaved[0], dtype=gdt)) \
+        if gsaved[16] is not None and fsaved[11] is not None else None
+    if elug is not None and merged:
         # ... and the rho partials, so the edge backward is one source-centric pass
         n_dst, HD = elug[1].shape
-        elug += (elug[1].new_empty(n_dst, (HD + 63) // 64, 3), gsaved[13])
+        elug += (elug[1].new_empty(n_dst, (HD + 63) // 64, 3, dtype=torch.float32), gsaved[13])
     # narrow heads (W2S) with h stored: the narrow FFN's backward epilogue makes G and the
     # per-head rho, and the edge backward is one head-lane pass over the words
     gate = None

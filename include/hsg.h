@@ -131,6 +131,12 @@ int hsg_gat_bwd_src_g(const hsg_rel *rel, int H, int D, float slope, const float
                       const float *m, const float *l, const float *G, const float *rho, int rho_groups,
                       const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                       float *dtau_part, void *stream);
+/* hsg_gat_bwd_src_g with G as bf16 rows when g_bf16 != 0 (the bf16 GEMM mode: the G
+ * hsg_gemm_bf16_psw_elug_rho_a16 writes with g_bf16; wide heads only, rho_groups > 0). */
+int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                         const float *m, const float *l, const void *G, int g_bf16, const float *rho, int rho_groups,
+                         const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                         float *dtau_part, void *stream);
 
 /* Measurement hook (bench.py's in-step kernel clock; not part of the reference
  * surface): the next hsg_gat_fwd launched FROM THE CALLING THREAD ON `stream` records
@@ -281,7 +287,7 @@ int hsg_gemm_bf16_psw(int M, int N, int K, const float *A, int lda, const void *
                       void *stream);
 /* The bf16 mode's FFN GEMMs on bf16 activations (round 5): hsg_gemm_bf16_psw with A,
  * C and the relu' mask aux given as bf16 rows per io = HSG_IO_A_BF16 | HSG_IO_C_BF16 |
- * HSG_IO_AUX_BF16 (io in {0, 1, 2, 7}; element strides lda / ldc / ldaux).  A bf16 A
+ * HSG_IO_AUX_BF16 (io in {0, 1, 2, 3, 7}; element strides lda / ldc / ldaux).  A bf16 A
  * needs lda % 8 == 0, 16-byte alignment and zeros in its columns K .. ceil8(K) - 1; a
  * bf16 C takes no accumulate epilogue, a bf16 aux only the relu' mask.  The bf16 mode
  * rounds A to bf16 at fragment read anyway, so the products equal hsg_gemm_bf16_psw's on
@@ -293,10 +299,11 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
                          const float *bias, const void *aux, int ldaux, int epi, int relu, float *colsum_part,
                          int io, void *stream);
 /* hsg_gemm_psw_elug_rho in the bf16 mode with a bf16 A (the FFN's bf16 dH rows; the
- * bf16 A contract above). */
+ * bf16 A contract above); g_bf16: G stored as bf16 rows (pitch ld; rho is summed from
+ * the fp32 G), for hsg_gat_bwd_src_g_io. */
 int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
-                                   int ldc, const float *aux, const float *x, const float *origin, float *G, int ld,
-                                   float *rho, int head_dim, void *stream);
+                                   int ldc, const float *aux, const float *x, const float *origin, void *G, int ld,
+                                   float *rho, int head_dim, int g_bf16, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
@@ -419,12 +426,20 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
                const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                float *dy, float *dx, float *part, void *stream);
 /* hsg_ln_bwd with dy stored as bf16 rows of pitch ld_dy (the bf16 GEMM mode, where dy is
- * only a GEMM operand): zeros in its columns d .. ceil8(d) - 1; the vector kernel's
+ * only a GEMM operand; y_bf16: y read as bf16 rows of pitch d, as hsg_ln_fwd_y16
+ * wrote it): zeros in its columns d .. ceil8(d) - 1; the vector kernel's
  * shapes only (d % 4 == 0, 257..512 columns, 16-byte aligned rows, ld_dy % 8 == 0),
  * HSG_EINVAL otherwise.  dx and the partials as hsg_ln_bwd (db2 sums the fp32 dy). */
-int hsg_ln_bwd_dy16(int n, int d, const float *dout, const float *y, const float *x, const float *gamma,
+int hsg_ln_bwd_dy16(int n, int d, const float *dout, const void *y, int y_bf16, const float *x, const float *gamma,
                     const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset,
                     void *dy, int ld_dy, float *dx, float *part, void *stream);
+/* hsg_ln_fwd with the FFN output y given as bf16 rows of pitch d (the bf16 GEMM mode:
+ * y is the GEMM's fp32 result rounded to nearest even, per-row error <= 2^-9 |y|); the
+ * persistent vector kernel's shapes only (d % 4 == 0, 257..512 columns), HSG_EINVAL
+ * otherwise.  hsg_ln_bwd_dy16 takes the same y with y_bf16 != 0. */
+int hsg_ln_fwd_y16(int n, int d, const void *y, const float *x, const float *gamma, const float *beta, float eps,
+                   float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
+                   void *stream);
 
 /* ---- head projection with per-head input dropout (GATStackLayer.py:56) ----------
  * Training-mode  z_k = fc_k(dropout_k(h))  for all heads without materialising the

@@ -282,6 +282,40 @@ def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k):
         assert err <= tol, name
 
 
+def test_one_pass_edge_bwd_bf16_G_rows_bitwise():
+    """hsg_gat_bwd_src_g_io with G as bf16 rows (the bf16 GEMM mode) against the fp32
+    call on the same values: the kernel widens each bf16 feature exactly, so dZ and
+    every attention-parameter gradient are bitwise equal."""
+    from hetersumgraph_amd import graph as hg
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.ops import LEAKY_SLOPE, gat_table_bwd, gat_table_fwd
+    rng = np.random.default_rng(11)
+    docs = [synth.make_hsg_doc(rng, N=35, W=600, k=36) for _ in range(4)]
+    Gr = hg.batch([synth.to_graph(d, hg.DGLGraph) for d in docs])
+    Gr.to(torch.device("cuda"))
+    rel = Gr.relation("S2W")
+    H, D = 6, 50
+    torch.manual_seed(2)
+    Z = torch.randn(rel.n_src, H * D, device="cuda")
+    attn = torch.randn(H, 3 * D, device="cuda") * 0.3
+    T = torch.randn(10, 50, device="cuda")
+    wf = torch.randn(H, D, 50, device="cuda") * 0.1
+    bf = torch.randn(H, D, device="cuda") * 0.1
+    org = torch.randn(rel.n_dst, H * D, device="cuda")
+    out, saved = gat_table_fwd(Z, attn, T, wf, bf, org, rel, H, D, LEAKY_SLOPE, no_h=True)
+    dout = torch.randn_like(out)
+    Gb = torch.randn_like(out).bfloat16()
+    rho = torch.randn(rel.n_dst, (H * D + 63) // 64, 3, device="cuda")
+    res = []
+    for G in (Gb.float().contiguous(), Gb):
+        dst = (torch.zeros_like(attn), torch.zeros_like(wf), torch.zeros_like(bf), torch.zeros_like(T), False, False)
+        dZ = gat_table_bwd(saved, dout, dst=dst, G=G, rho=rho)
+        res.append((dZ,) + dst[:4])
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("n", [1120, 37])
 def test_narrow_ffn_gate_epilogue(n):
     """hsg_ffn_small_bwd_gate: the same dx (bitwise) as hsg_ffn_small_bwd, and G =

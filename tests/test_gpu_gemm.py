@@ -577,14 +577,17 @@ def test_bf16_io_elug_rho_bitwise(M):
     origin = torch.randn(M, N, device="cuda")
     x = torch.nn.functional.elu(2 * torch.randn(M, N, device="cuda")) + origin
     outs = []
-    for A in (dHb.float().contiguous(), dHb):
-        out, G = ds.clone(), torch.empty_like(ds)
+    for A, gdt in ((dHb.float().contiguous(), torch.float32), (dHb, torch.float32), (dHb, torch.bfloat16)):
+        out, G = ds.clone(), torch.empty_like(ds, dtype=gdt)
         rho = torch.empty(M, (N + 63) // 64, 3, device="cuda")
         assert gemm_psw_elug(A, S, out, x, origin, G, rho, D)
         outs.append((out, G, rho))
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
+    for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+    # G as bf16 rows: the fp32 G rounded to nearest even; dx and rho (from the fp32 G) unchanged
+    assert torch.equal(outs[2][0], outs[0][0]) and torch.equal(outs[2][2], outs[0][2])
+    assert torch.equal(outs[2][1], outs[0][1].bfloat16())
 
 
 @pytest.mark.parametrize("n,p_drop", [(28800, 0.1), (1001, 0.0)])
@@ -607,7 +610,7 @@ def test_ln_bwd_bf16_dy_bitwise(n, p_drop):
                           off, ptr(dy), ptr(dx), ptr(part), None) == 0
     dyb = torch.full((n, 304), float("nan"), device="cuda").bfloat16()
     dx2, part2 = torch.empty_like(x), torch.empty_like(part)
-    assert lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+    assert lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), 0, ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
                                ptr(seed_t), off, ptr(dyb), 304, ptr(dx2), ptr(part2), None) == 0
     torch.cuda.synchronize()
     assert torch.equal(dyb[:, :d], dy.bfloat16()) and torch.equal(dyb[:, d:].float(), torch.zeros(n, 4, device="cuda"))
@@ -631,3 +634,43 @@ def test_dw_pair_bf16_operands_bitwise():
     assert a is not None and b is not None
     for (wa, sa), (wb, sb) in zip(a, b):
         assert sa == sb and torch.equal(wa, wb)
+
+
+@pytest.mark.parametrize("n,p_drop", [(28800, 0.1), (1001, 0.0)])
+def test_ln_fwd_bf16_y_equals_fp32_on_the_same_values(n, p_drop):
+    """hsg_ln_fwd_y16 (the bf16 mode's bf16 LayerNorm input y) against hsg_ln_fwd on
+    the same (bf16-rounded) y: out, mean, rstd bitwise equal; and hsg_ln_bwd_dy16 with
+    y_bf16 against y_bf16 = 0 on the fp32 copy of those values."""
+    from hetersumgraph_amd import rng as hsg_rng
+    from hetersumgraph_amd._lib import load, ptr
+    lib = load()
+    d = 300
+    torch.manual_seed(n + 1)
+    yb = torch.randn(n, d, device="cuda").bfloat16()
+    yf = yb.float().contiguous()
+    x = torch.randn(n, d, device="cuda")
+    gamma, beta = 1 + 0.1 * torch.randn(d, device="cuda"), 0.1 * torch.randn(d, device="cuda")
+    hsg_rng.manual_seed(9)
+    seed_t, off = hsg_rng.get(x.device).take() if p_drop > 0 else (None, 0)
+    outs = []
+    for y, f in ((yf, lib.hsg_ln_fwd), (yb, lib.hsg_ln_fwd_y16)):
+        out, mean, rstd = torch.empty_like(x), x.new_empty(n), x.new_empty(n)
+        assert f(n, d, ptr(y), ptr(x), ptr(gamma), ptr(beta), 1e-5, p_drop, ptr(seed_t), off, ptr(out), ptr(mean),
+                 ptr(rstd), None) == 0
+        outs.append((out, mean, rstd))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    mean, rstd = outs[0][1], outs[0][2]
+    dout = torch.randn(n, d, device="cuda")
+    nb = lib.hsg_ln_bwd_blocks(n)
+    res = []
+    for y, flag in ((yf, 0), (yb, 1)):
+        dy = torch.zeros(n, 304, device="cuda").bfloat16()
+        dx, part = torch.empty_like(x), x.new_empty(nb, 3, d)
+        assert lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), flag, ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
+                                   ptr(seed_t), off, ptr(dy), 304, ptr(dx), ptr(part), None) == 0
+        res.append((dy, dx, part))
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

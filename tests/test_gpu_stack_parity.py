@@ -253,6 +253,9 @@ def test_bf16_activations_bitwise_equal_fp32_buffers(train, monkeypatch):
     z = synth_fixture(docs)
     R = torch.from_numpy(np.random.default_rng(7).standard_normal((int(z["n_s"]), 64)))
     runs = []
+    # the bf16 LayerNorm input y and edge gate G rows (HSG_FFN_BF16_ROWS) round once more:
+    # off here, pinned against the fp64 oracle by the cfg5-bf16 cases above
+    monkeypatch.setitem(_lib._OPTIONS, "HSG_FFN_BF16_ROWS", "0")
     for flag in ("0", "1"):
         monkeypatch.setitem(_lib._OPTIONS, "HSG_FFN_BF16_ACT", flag)
         with gemm_dtype("bf16"):
