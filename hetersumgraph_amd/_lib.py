@@ -29,7 +29,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
            "hsg_hproj_fwd_logits", "hsg_wsplit_dims", "hsg_wsplit", "hsg_gemm_f32_psw", "hsg_dropmask_multi", "hsg_dropmask_multi_wt", "hsg_step_prologue", "hsg_gemm_f32_slabs", "hsg_slab_reduce",
-           "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_kclock_arm",
+           "hsg_hproj_wt", "hsg_hproj_fwd_t8_supported", "hsg_hproj_fwd_t8", "hsg_hproj_fwd_mf_supported", "hsg_hproj_fwd_mf", "hsg_kclock_arm",
            "hsg_kclock_pending", "hsg_seed_advance", "hsg_gat_bwd_dst_noh_supported", "hsg_gat_bwd_dst_noh",
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
            "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
@@ -100,6 +100,8 @@ _SIGS = {
     "hsg_hproj_wt": [_I, _I, _I, _P, _P, _P],
     "hsg_hproj_fwd_t8_supported": [_I, _I, _I],
     "hsg_hproj_fwd_t8": [_I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _P, _P, _P],
+    "hsg_hproj_fwd_mf_supported": [_I, _I, _I],
+    "hsg_hproj_fwd_mf": [_I, _I, _I, _P, _I, _P, _I, _I, _P, _F, _P, _I, _P, _P, _P],
     "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _I, _P],

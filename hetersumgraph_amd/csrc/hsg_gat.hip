@@ -42,6 +42,19 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Raw buffer access (k_gat_fwd_b): the row offset goes in soffset (wave-uniform), the
+// feature's byte offset in voffset; an offset past the descriptor's byte count reads 0
+// and drops the store.  Descriptors are built from kernel arguments (wave-uniform).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *p, long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff, float x) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), r, (int)voff, (int)soff, 0);
+}
+
 __device__ __forceinline__ float leaky(float x, float slope) { return x > 0.f ? x : x * slope; }
 
 // F.elu (GAT.py:56): x for x > 0, else exp(x) - 1 on v_exp_f32.  Absolute error
@@ -217,10 +230,16 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             ptu = tau[pt * H + k];
         }
     };
-    if constexpr (PF == 2) {
+    float org_next[PF == 3 ? NF : 1];                     // PF = 3: the next destination's residual row
+    if constexpr (PF >= 2) {
         if (wr.first < wr.end) {
             pf_edges(__builtin_amdgcn_readfirstlane(pf_beg), __builtin_amdgcn_readfirstlane(pf_end));
             pf_scores();
+            if constexpr (PF == 3) {
+                const int v0 = __builtin_amdgcn_readfirstlane(wr.first);
+#pragma unroll
+                for (int i = 0; i < NF; ++i) org_next[i] = origin ? origin[(size_t)v0 * HD + fo[i]] : 0.f;
+            }
         }
     }
     for (int v_ = wr.first; v_ < wr.end; v_ += vstride) {
@@ -235,7 +254,10 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             // requested after the score loads (cfg2 S2W, in-step), although vmcnt counts
             // in issue order and the score chain then also waits for this HBM row
 #pragma unroll
-            for (int i = 0; i < NF; ++i) org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
+            for (int i = 0; i < NF; ++i) {
+                if constexpr (PF == 3) org[i] = org_next[i];
+                else org[i] = origin ? origin[(size_t)v * HD + fo[i]] : 0.f;
+            }
             const int vn = v_ + vstride;
             if (vn < wr.end) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
         } else {
@@ -254,7 +276,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 const int e = eb + j;
                 int u;
                 float s;
-                if (PF == 2 && j == l && pok) {            // prefetched last iteration
+                if (PF >= 2 && j == l && pok) {            // prefetched last iteration
                     u = pu;
                     s = leaky(psg + ptu, slope);
                 } else {
@@ -284,7 +306,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             }
         }
         if (c > 0) lse_merge(mx, sm, 0.f, (float)c);     // phantom in-edges: e = 0
-        if constexpr (PF == 2) {                          // the next destination's (src, box)
+        if constexpr (PF >= 2) {                          // the next destination's (src, box)
             if (v_ + vstride < wr.end)
                 pf_edges(__builtin_amdgcn_readfirstlane(pf_beg), __builtin_amdgcn_readfirstlane(pf_end));
             else
@@ -298,6 +320,19 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
         }
 
+        // PF = 3: the next destination's (sigma, tau) and residual row, requested once
+        bool issued = false;
+        auto pf3_next = [&]() {
+            if constexpr (PF == 3) {
+                const int vn = v_ + vstride;
+                if (vn < wr.end) {
+                    pf_scores();
+                    const int vs = __builtin_amdgcn_readfirstlane(vn);
+#pragma unroll
+                    for (int i = 0; i < NF; ++i) org_next[i] = origin ? origin[(size_t)vs * HD + fo[i]] : 0.f;
+                }
+            }
+        };
         // phase 2: alphas per 64-edge chunk, then flat-mapped aggregation
         float acc[NF];
 #pragma unroll
@@ -319,8 +354,30 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 }
             }
             wave_lds_sync();
-            gather_rows<NF>(Z, HD, n, sn, sa, H, fh, fo, acc);
+            if constexpr (PF == 3) {
+                // after the first row's loads the next destination's (sigma, tau) and
+                // residual row are requested, so (vmcnt in issue order) the FMAs wait for
+                // the L2 rows only and the next destination's HBM residual row has a whole
+                // iteration to arrive
+                for (int j = 0; j < n; ++j) {
+                    float xv[NF];
+                    const float *xr = Z + (size_t)sn[j] * HD;
+#pragma unroll
+                    for (int i = 0; i < NF; ++i) xv[i] = xr[fo[i]];
+                    if (!issued) {
+                        issued = true;
+                        pf3_next();
+                    }
+#pragma unroll
+                    for (int i = 0; i < NF; ++i) acc[i] = fmaf(sa[j * H + fh[i]], xv[i], acc[i]);
+                }
+            } else {
+                gather_rows<NF>(Z, HD, n, sn, sa, H, fh, fo, acc);
+            }
             wave_lds_sync();
+        }
+        if constexpr (PF == 3) {
+            if (!issued) pf3_next();                        // no edges
         }
         if constexpr (WPN > 1) {
 #pragma unroll
@@ -441,6 +498,196 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sp(RelPtrs R, int H, int D, flo
         if (fok && f - kf * D == 0) {
             mout[v * H + kf] = any ? m : 0.f;
             lout[v * H + kf] = any ? l : 1.f;
+        }
+    }
+}
+
+// ---------------------------------------- forward, destination batches (round 5) ----
+// Short segments, wide rows (S2W at cfg2: ~2.1 in-edges per word, H*D = 300).
+// k_gat_fwd spends a wave on one destination: its (k, l) score lanes are mostly idle
+// at two edges, and the per-destination fixed work -- the butterfly (max, sum) merge,
+// one precise division per lane, the 64-bit address arithmetic of every gathered
+// row -- made it VALU-issue-heavy (SQ_INSTS_VALU 753 per wave, ~281 per destination;
+// the VALU was busy ~60 % of the kernel).  Here a wave takes a batch of up to DB
+// consecutive destinations whose edges fit one LDS chunk (CH edges; a destination
+// with more edges runs alone over several chunks):
+//   stage:   lane q loads edge q's (source, box) (one coalesced load of the batch's
+//            contiguous CSR range), then lanes p = (q, k) over all (edge, head) pairs
+//            load (sigma, tau) -> scores in LDS, pairs two at a time in flight;
+//   softmax: lane (d, k) walks destination d's scores of head k serially (online
+//            max / sum, no cross-lane merge), folds the phantom edges, writes m / l
+//            (coalesced over the batch) and turns its scores into alphas in place;
+//   gather:  per destination (wave-uniform loop) the source rows are scalar bases
+//            (readfirstlane of the staged index), so every row load is saddr + a
+//            per-lane feature offset, two rows in flight, alphas from LDS; then
+//            elu(h) + origin (the residual row requested with the rows).
+// Chain per batch: indptr -> (src, box) -> (sigma, tau) -> rows -> stores.  Same
+// arithmetic as k_gat_fwd (alpha = exp(s - m) / l, gathers in CSR order) up to the
+// summation order of (m, l).
+template <int NF, int TAU_MODE, int DB>
+__global__ __launch_bounds__(256, 7) void k_gat_fwd_b(RelPtrs R, int H, int D, float slope,
+                                                      const float *__restrict__ Z,
+                                                      const float *__restrict__ sigma,
+                                                      const float *__restrict__ tau,
+                                                      const float *__restrict__ origin,
+                                                      float *__restrict__ hout, float *__restrict__ out,
+                                                      float *__restrict__ mout, float *__restrict__ lout) {
+    constexpr int CH = HSG_CHUNK;
+    __shared__ float s_sc[HSG_WAVES][CH * HSG_HMAX];    // scores, then alphas: [edge][head]
+    __shared__ int s_u[HSG_WAVES][CH];                  // staged source rows
+    __shared__ int s_t[HSG_WAVES][CH];                  // staged tau rows
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const float invH = 1.f / (float)H;
+    // byte offset of feature f (clamped into the row) and its head.  Rows are read and
+    // written by buffer instructions: scalar row offset (soffset) + this per-lane byte
+    // offset, so a row access costs no VALU address arithmetic
+    unsigned fb[NF];
+    int fa[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        fb[i] = 4u * (unsigned)(f < HD ? f : HD - 1);
+        fa[i] = f < HD ? div_small(f, 1.f / (float)D) : 0;
+    }
+    const unsigned rowb = 4u * (unsigned)HD;
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(Z, (long)R.n_src * rowb);
+    const __amdgpu_buffer_rsrc_t orr = buf_rsrc(origin, origin ? (long)R.n_dst * rowb : 0);
+    const __amdgpu_buffer_rsrc_t outr = buf_rsrc(out, origin ? (long)R.n_dst * rowb : 0);
+    const __amdgpu_buffer_rsrc_t hr = buf_rsrc(hout, hout ? (long)R.n_dst * rowb : 0);
+    const int ndmax = min(DB, 64 / H);
+    const int sd = div_small(lane, invH), sk = lane - sd * H;    // softmax lane: (destination, head)
+    float *sc = s_sc[wid];
+    int *su = s_u[wid], *st = s_t[wid];
+
+    // scores of the chunk's edges [cb, cb + n) into sc[q * H + k]
+    auto stage = [&](int cb, int n) {
+        if (lane < n) {
+            su[lane] = R.src[cb + lane];
+            st[lane] = tau_row<TAU_MODE>(R, cb + lane);
+        }
+        wave_lds_sync();
+        const int np = n * H;
+        for (int p0 = 0; p0 < np; p0 += 128) {
+            const int pa = min(p0 + lane, np - 1), pb = min(p0 + 64 + lane, np - 1);
+            const int qa = div_small(pa, invH), qb = div_small(pb, invH);
+            const int ka = pa - qa * H, kb = pb - qb * H;
+            const float xa = sigma[su[qa] * H + ka] + tau[st[qa] * H + ka];
+            const float xb = sigma[su[qb] * H + kb] + tau[st[qb] * H + kb];
+            if (p0 + lane < np) sc[pa] = leaky(xa, slope);
+            if (p0 + 64 + lane < np) sc[pb] = leaky(xb, slope);
+        }
+        wave_lds_sync();
+    };
+
+    const int nbat = (R.n_dst + DB - 1) / DB;
+    const WorkRange wr = work_range(nbat, HSG_WAVES, wid, R.xcd);
+    for (int b = wr.first; b < wr.end; b += wr.stride) {
+        int v = __builtin_amdgcn_readfirstlane(b * DB);
+        const int bend = min(R.n_dst, v + DB);
+        while (v < bend) {
+            const int rem = min(bend - v, ndmax);
+            const int ip = R.indptr[v + min(lane, rem)];
+            const int beg0 = __builtin_amdgcn_readlane(ip, 0);
+            // destinations [v, v + nd) whose edges fit one chunk (ip is monotone: a prefix)
+            const bool fit = lane >= 1 && lane <= rem && ip - beg0 <= CH;
+            int nd = __builtin_popcountll(__ballot(fit));
+            nd = __builtin_amdgcn_readfirstlane(nd > 0 ? nd : 1);
+            const int endB = __builtin_amdgcn_readlane(ip, nd);
+            const bool multi = endB - beg0 > CH;        // one destination over several chunks
+            const bool sact = lane < nd * H;
+            const int dbeg = __shfl(ip, sd), dend = __shfl(ip, sd + 1);
+            const int c = sact ? R.phantom[v + sd] : 0;
+
+            // softmax state of (destination sd, head sk)
+            float mx = -INFINITY, sm = 0.f;
+            for (int cb = beg0; cb < endB; cb += CH) {
+                const int n = min(CH, endB - cb);
+                stage(cb, n);
+                if (sact) {
+                    const int e1 = min(dend, cb + n);
+                    for (int e = max(dbeg, cb); e < e1; ++e) {
+                        const float s = sc[(e - cb) * H + sk];
+                        if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
+                        else sm += __expf(s - mx);
+                    }
+                }
+                wave_lds_sync();
+            }
+            if (c > 0) lse_merge(mx, sm, 0.f, (float)c);     // phantom in-edges: e = 0
+            const bool any = dend > dbeg;
+            const float inv = any ? 1.f / sm : 0.f;
+            if (sact) {
+                mout[(v + sd) * H + sk] = any ? mx : 0.f;
+                lout[(v + sd) * H + sk] = any ? sm : 1.f;
+            }
+
+            float acc[NF];
+#pragma unroll
+            for (int i = 0; i < NF; ++i) acc[i] = 0.f;
+            int d = 0;
+            int cb = beg0;
+            do {                                   // at least once: a batch may have no edges
+                const int n = min(CH, endB - cb);
+                if (multi) stage(cb, n);
+                if (sact) {
+                    const int e1 = min(dend, cb + n);
+                    for (int e = max(dbeg, cb); e < e1; ++e) {
+                        float *p = sc + (e - cb) * H + sk;
+                        *p = __expf(*p - mx) * inv;
+                    }
+                }
+                wave_lds_sync();
+                for (; d < nd; ++d) {
+                    const int e0 = __builtin_amdgcn_readlane(ip, d), e1 = __builtin_amdgcn_readlane(ip, d + 1);
+                    const bool fin = e1 <= cb + n;              // the destination ends in this chunk
+                    const int vd = v + d;
+                    // rows two at a time; the residual row is requested right after the
+                    // first pair (vmcnt retires in issue order: the pair's FMAs then wait
+                    // for the L2 rows only, the HBM residual row just before the stores).
+                    // No branches around the loads: the first pair runs even for an empty
+                    // segment (weights 0, row 0), a null origin / out / h has a 0-byte
+                    // descriptor (loads read 0, stores are dropped)
+                    float org[NF];
+                    const int qe = min(e1, cb + n) - cb;
+                    auto pair = [&](int q, bool first) {
+                        const bool one = q < qe, two = q + 1 < qe;          // wave-uniform
+                        const int u0 = one ? __builtin_amdgcn_readfirstlane(su[q]) : 0;
+                        const int u1 = two ? __builtin_amdgcn_readfirstlane(su[q + 1]) : u0;
+                        float x0[NF], x1[NF];
+#pragma unroll
+                        for (int i = 0; i < NF; ++i) {
+                            x0[i] = buf_ld(zr, fb[i], u0 * rowb);
+                            x1[i] = buf_ld(zr, fb[i], u1 * rowb);
+                        }
+                        if (first) {
+#pragma unroll
+                            for (int i = 0; i < NF; ++i) org[i] = buf_ld(orr, fb[i], vd * rowb);
+                        }
+                        const float *a0 = sc + (one ? q : 0) * H, *a1 = sc + (two ? q + 1 : 0) * H;
+#pragma unroll
+                        for (int i = 0; i < NF; ++i) {
+                            acc[i] = fmaf(one ? a0[fa[i]] : 0.f, x0[i], acc[i]);
+                            acc[i] = fmaf(two ? a1[fa[i]] : 0.f, x1[i], acc[i]);
+                        }
+                    };
+                    const int q0 = max(e0, cb) - cb;
+                    pair(q0, true);
+                    for (int q = q0 + 2; q < qe; q += 2) pair(q, false);
+                    if (!fin) break;                            // continues in the next chunk
+#pragma unroll
+                    for (int i = 0; i < NF; ++i) {
+                        if (lane + 64 * i < HD) {
+                            buf_st(hr, fb[i], vd * rowb, acc[i]);
+                            buf_st(outr, fb[i], vd * rowb, elu1(acc[i]) + org[i]);
+                        }
+                        acc[i] = 0.f;
+                    }
+                }
+                wave_lds_sync();
+                cb += CH;
+            } while (cb < endB);
+            v += nd;
         }
     }
 }
@@ -1703,10 +1950,15 @@ bool bwd_occ() {
 // HSG_GAT_FWD_PF=0 drops it
 // round 4: two-level prefetch by default (S2W forward 16.53 / 16.59 -> 16.09 / 16.14 us
 // per launch in two alternations of rocprofv3 step traces, profiles/r04_dev/pf{1,2}_step_*.txt);
-// HSG_GAT_FWD_PF=1 / 0 (dev) restore one level / none
+// HSG_GAT_FWD_PF=1 / 0 (dev) restore one level / none.  Round 5, PF = 3 (dev): the next
+// destination's residual row requested right after this one's first gathered row, i.e.
+// a whole iteration ahead (6 waves per SIMD for its registers): 16.9 vs 16.0 us per
+// launch in step traces, 16.2 vs 16.0 back to back -- the residual row is not what the
+// forward waits on (without any residual read, h instead of out: 14.0 us).  The score
+// lanes per head (HSG_GAT_FWD_LPH, dev) at 8 / 4 / 2 / 1: 15.6 / 15.9 / 17.2 / 19.6 us.
 int fwd_pf() {
     const char *e = HSG_DEV_ENV("HSG_GAT_FWD_PF");
-    return e ? (atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : 2) : 2;
+    return e ? (atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : atoi(e) == 3 ? 3 : 2) : 2;
 }
 
 // occupancy hint of the one-destination-per-wave forward: 7 waves per SIMD (73 -> 64
@@ -1793,6 +2045,33 @@ int fwd_sp() {
     return eb == 0 ? 0 : (eb == 32 ? 32 : 64);
 }
 int src_wpn(const hsg_rel *r) { return wpn_for(r->n_src, r->n_edges); }
+// destinations per wave batch of the short-segment forward (k_gat_fwd_b, dev only); 0 =
+// the one-destination-per-wave k_gat_fwd.  Measured slower on the cfg2 S2W pass
+// (rocprofv3 step traces, two alternations: 17.3 / 17.3 / 21.0 us with 4 / 2 / 8
+// destinations per batch against 15.9 us; back to back 17.0 vs 16.0 us, gat_fwd_diag):
+// the wave walks its batch's destinations one gather round trip after another, and
+// fewer waves hide less.  HSG_GAT_FWD_B=2|4|8
+int fwd_batch() {
+    const char *e = HSG_DEV_ENV("HSG_GAT_FWD_B");
+    const int b = e ? atoi(e) : 0;
+    return b == 2 || b == 4 || b == 8 ? b : 0;
+}
+
+template <int TAU, int DB>
+int fwd_b_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, float slope, const float *Z,
+                   const float *sg, const float *tau, const float *org, float *h, float *out, float *m, float *l) {
+#define HSG_FB(NF_)                                                                                      \
+    case NF_:                                                                                            \
+        HSG_KLAUNCH(true, true, (k_gat_fwd_b<NF_, TAU, DB>), grid, dim3(256), st, R, H, D, slope, Z, sg, tau, \
+                    org, h, out, m, l);                                                                  \
+        break;
+    switch (nf) {
+        HSG_FB(1) HSG_FB(2) HSG_FB(3) HSG_FB(4) HSG_FB(5) HSG_FB(6) HSG_FB(7) HSG_FB(8)
+        default: return HSG_EINVAL;
+    }
+#undef HSG_FB
+    return launch_status();
+}
 
 }  // namespace
 
@@ -1837,6 +2116,21 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
         return launch_status();
     }
 #ifdef HSG_DEV
+    // (k_gat_fwd_b addresses rows by 32-bit buffer offsets)
+    const bool b32 = (long)rel->n_src * H * D * 4 < 0x7fffffffL && (long)rel->n_dst * H * D * 4 < 0x7fffffffL;
+    if (wpn == 1 && fwd_batch() && b32) {   // short segments: destination batches per wave (dev A/B)
+        const int db = fwd_batch();
+        const dim3 g(grid_nodes((rel->n_dst + db - 1) / db, 1, kFwdPersistentCap));
+#define HSG_B(DB_) (tau_mode == HSG_TAU_TABLE                                                                \
+                        ? fwd_b_dispatch<HSG_TAU_TABLE, DB_>(nf, g, st, R, H, D, slope, Z, sigma, tau, origin, h, \
+                                                             out, m, l)                                   \
+                        : fwd_b_dispatch<HSG_TAU_PER_EDGE, DB_>(nf, g, st, R, H, D, slope, Z, sigma, tau, origin, \
+                                                                h, out, m, l))
+        if (db == 2) return HSG_B(2);
+        if (db == 8) return HSG_B(8);
+        return HSG_B(4);
+#undef HSG_B
+    }
     if (wpn == 1) {                      // short segments: row-tile float4 kernel
         const bool al = aligned16p(Z) && aligned16p(h) && (!origin || (aligned16p(origin) && aligned16p(out)));
         const RowsPlan pl = rows_plan(H, D, al);
@@ -1852,12 +2146,25 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
     int fcap = wpn == 1 && fwd_occ() == 7 ? kFwdPersistentCap : kFwdGridCap;
     if (const char *e = HSG_DEV_ENV("HSG_GAT_FWD_CAP")) fcap = atoi(e) > 0 ? atoi(e) : fcap;   // dev sweep
     const dim3 grid(grid_nodes(rel->n_dst, wpn, fcap));
-    const int lph = lanes_per_head(H);
+    int lph = lanes_per_head(H);
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_FWD_LPH")) {      // dev sweep: score lanes per head (power of 2)
+        const int v = atoi(e);
+        if (v >= 1 && v <= lph && (v & (v - 1)) == 0 && wpn == 1) lph = v;
+    }
     const int occ = wpn == 1 ? fwd_occ() : 1;
     if (occ > 1) {
         const int pf = fwd_pf();
         if (pf != 0 || occ != 8) {
 #ifdef HSG_DEV
+            if (pf == 3) {                                 // residual row one destination ahead (dev A/B)
+                // 6 waves per SIMD (the next row's registers): one persistent wave of 1,536 blocks
+                const dim3 g6(grid_nodes(rel->n_dst, 1, 1536));
+                if (tau_mode == HSG_TAU_TABLE)
+                    return fwd_dispatch<HSG_TAU_TABLE, 1, 6, 3>(nf, g6, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                origin, h, out, m, l);
+                return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 6, 3>(nf, g6, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                               origin, h, out, m, l);
+            }
             if (pf == 1) {                                 // one-level prefetch (dev A/B)
                 if (tau_mode == HSG_TAU_TABLE)
                     return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,

@@ -729,33 +729,10 @@ __device__ __forceinline__ void split_trunc8(const f32x4 x, const f32x4 y, bf16x
     l2 = __builtin_bit_cast(bf16x8, w2);
 }
 
-// RNE split of 8 fp32 values, x = l0 + l1 + l2 exactly: l0 = RNE(x) and l1 = RNE(x - l0)
-// by v_cvt_pk_bf16_f32 (two values per instruction), l2 = x - l0 - l1 (at most 8
-// significant bits: exact in bf16, packed by v_perm_b32).  11 VALU per pair like
-// split_trunc8, with the limb magnitudes of split3 (|l1| <= 2^-9 |x|, |l2| <= 2^-18 |x|):
-// the dropped products a1 b2 + a2 b1 stay <= 2^-26 |ab|.  Subtractions pinned to
-// scalar v_sub_f32 as in split_trunc8.
-typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+// RNE split of 8 fp32 values, x = l0 + l1 + l2 exactly (hsg_split_rne8, hsg_wsplit.h)
 __device__ __forceinline__ void split_rne8(const f32x4 x, const f32x4 y, bf16x8 &l0, bf16x8 &l1, bf16x8 &l2) {
-    const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-    u32x4 w0, w1, w2;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        // the low element is unpacked by a byte permute, (a & 0xffff) << 16: written as a
-        // shift, the compiler saw through it and re-converted that element alone
-        // (v_cvt_pk_bf16_f32 x, 0) -- 16 extra VALU per k_gemm7 K tile beside 48 MFMAs
-        // that are vector-issue-bound already
-        const unsigned a = __builtin_bit_cast(unsigned, bf16x2v{(__bf16)v[2 * p], (__bf16)v[2 * p + 1]});
-        w0[p] = a;
-        float ra, rb, sa, sb;
-        asm("v_sub_f32 %0, %1, %2" : "=v"(ra) : "v"(v[2 * p]), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, a, 0x01000c0cu))));
-        asm("v_sub_f32 %0, %1, %2" : "=v"(rb) : "v"(v[2 * p + 1]), "v"(__uint_as_float(a & 0xFFFF0000u)));
-        const unsigned b = __builtin_bit_cast(unsigned, bf16x2v{(__bf16)ra, (__bf16)rb});
-        w1[p] = b;
-        asm("v_sub_f32 %0, %1, %2" : "=v"(sa) : "v"(ra), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, b, 0x01000c0cu))));
-        asm("v_sub_f32 %0, %1, %2" : "=v"(sb) : "v"(rb), "v"(__uint_as_float(b & 0xFFFF0000u)));
-        w2[p] = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
-    }
+    hsg_u32x4_t w0, w1, w2;
+    hsg_split_rne8(x, y, w0, w1, w2);
     l0 = __builtin_bit_cast(bf16x8, w0);
     l1 = __builtin_bit_cast(bf16x8, w1);
     l2 = __builtin_bit_cast(bf16x8, w2);

@@ -494,6 +494,162 @@ __global__ __launch_bounds__(64 * HB * KS) void k_hproj_fwd_v8(int n, int in, in
     }
 }
 
+// ------------------------------------------ forward on bf16 limb MFMAs (round 5) ----
+// D = 8 (the W2S projection): the VALU form above runs 8 fmac + 2 mask ops per (row,
+// column, head).  Here the products run on v_mfma_f32_16x16x32_bf16, fp32-accurate as
+// the FFN GEMMs (three RNE bf16 limbs per operand, six products).  A head's 8 outputs
+// take half of the 16 MFMA columns (the other half repeats them), because each head
+// masks the A rows with its own keep bits.
+// Block = one 32-row tile (one mask word per (head, column)) x all heads, wave w =
+// heads 2w, 2w + 1, the whole K.  Per 32-column step the block stages, double-buffered
+// in LDS with the next step's global loads in flight in registers: X split ONCE into
+// three limb planes (each thread splits one float4), the 8 heads' mask words, and the
+// W limb planes' 32-column slice (hsg_wsplit planes [3][Np][Kp], rows = outputs).  Per
+// head a wave then builds the 16-bit lane masks of its A fragments from the 8 words of
+// its columns (shifted so rows r and r + 16 sit at bits 15 / 31; v_perm_b32's sign-byte
+// selectors make a bf16 pair's mask in one instruction), ANDs them into the limbs and
+// runs 2 tiles x 6 MFMAs.  One barrier per step.  Epilogue: scale, Z, and the optional
+// source logits sigma[i, k] = <Z[i, 8k:8k+8], a1_k> (an 8-lane butterfly).
+__global__ __launch_bounds__(256) void k_hproj_fwd_mf(int n, int in, int H, const float *__restrict__ X, int ldx,
+                                                     const __bf16 *__restrict__ Wp, int Np, int Kp,
+                                                     const uint32_t *__restrict__ bits, float scale,
+                                                     float *__restrict__ Z, int ldz, const float *__restrict__ a1,
+                                                     float *__restrict__ sigma) {
+    constexpr int HM = 8;                                     // heads per block (max), 2 per wave
+    __shared__ __attribute__((aligned(16))) __bf16 sA[2][3][32 * 32];     // X limbs [row][col]
+    __shared__ __attribute__((aligned(16))) uint32_t sM[2][HM][32];       // keep words [head][col]
+    __shared__ __attribute__((aligned(16))) __bf16 sW[2][3][HM * 8 * 32]; // W limbs [out][col]
+    // LDS swizzles (bf16 rows of 32 columns = four 16-byte chunks): chunk j of X-limb row
+    // rr sits at j ^ hx(rr >> 2), of W-limb row o at j ^ 2 ((o >> 2) & 1), so that each
+    // 16-lane group of a ds_read_b128 fragment read ({0-3, 12-15, 20-27}, ... on gfx950)
+    // lands on 16 distinct 4-bank slots
+    auto ax = [](int rr, int j) { return rr * 32 + 8 * (j ^ ((0x78 >> (2 * ((rr >> 2) & 3))) & 3)); };
+    auto aw = [](int o, int j) { return o * 32 + 8 * (j ^ (2 * ((o >> 2) & 1))); };
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int rt = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, g = lane >> 4;
+    const int nst = Kp / 32;
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rW = rsrc(Wp, (long)3 * Np * Kp * 2);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    // staging units: X float4 (row xr, columns 4 xq..), mask word (head mk, column mc),
+    // W 16-byte pieces (limb, output row, 8 columns): HW * 3 per thread
+    const int xr = tid >> 3, xq = tid & 7;
+    const uint32_t xo = rt * 32 + xr < n ? (uint32_t)(rt * 32 + xr) * ldx * 4 : kOOB;
+    const int mk = tid >> 5, mc = tid & 31;
+    const uint32_t mo = mk < H ? (uint32_t)((mk * NWI + rt) * LDC) * 4 : kOOB;
+    const uint32_t plane = (uint32_t)Np * Kp * 2;
+    // two steps of global loads in flight (register sets R = 0, 1 for even / odd steps)
+    u32x4v rxs[2], rws[2][3];
+    uint32_t rms[2] = {0u, 0u};
+    auto gload = [&](int s, u32x4v &rx, uint32_t &rm, u32x4v (&rw)[3]) {
+        const int c = 32 * s + 4 * xq;
+        rx = bld4(rX, (xo == kOOB || c >= in) ? kOOB : xo + 4u * c);
+        const int cm = 32 * s + mc;
+        rm = bldu(rM, (mo == kOOB || cm >= LDC) ? kOOB : mo + 4u * cm);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {                             // piece u: limb u / 256, output (u / 4) % 64, 8 columns
+            const int u = tid + 256 * i, l = u >> 8, o = (u >> 2) & 63, q = u & 3;
+            rw[i] = bld4(rW, o < H * 8 ? l * plane + (uint32_t)o * Kp * 2 + 2u * (32 * s + 8 * q) : kOOB);
+        }
+    };
+    auto lstore = [&](int b, const u32x4v &rx, uint32_t rm, const u32x4v (&rw)[3]) {
+        typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+        u32x2v w0, w1, w2;
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            unsigned x0, x1, x2;
+            hsg_split_rne_pair(__uint_as_float(rx[2 * p]), __uint_as_float(rx[2 * p + 1]), x0, x1, x2);
+            w0[p] = x0; w1[p] = x1; w2[p] = x2;
+        }
+        const int xa = ax(xr, xq >> 1) + 4 * (xq & 1);
+        *reinterpret_cast<u32x2v *>(&sA[b][0][xa]) = w0;
+        *reinterpret_cast<u32x2v *>(&sA[b][1][xa]) = w1;
+        *reinterpret_cast<u32x2v *>(&sA[b][2][xa]) = w2;
+        sM[b][mk][mc] = rm;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int u = tid + 256 * i, l = u >> 8, o = (u >> 2) & 63, q = u & 3;
+            *reinterpret_cast<u32x4v *>(&sW[b][l][aw(o, q)]) = rw[i];
+        }
+    };
+    f32x4v acc[2][2];                                             // [row tile][head of the wave]
+#pragma unroll
+    for (int f = 0; f < 2; ++f) acc[f][0] = acc[f][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int sh = 15 - r;                                        // bit r -> 15, bit r + 16 -> 31
+    gload(0, rxs[0], rms[0], rws[0]);
+    if (nst > 1) gload(1, rxs[1], rms[1], rws[1]);
+    auto step = [&](int s, int b) {                              // b = s & 1 (compile-time in the caller)
+        lstore(b, rxs[b], rms[b], rws[b]);
+        __syncthreads();
+        if (s + 2 < nst) gload(s + 2, rxs[b], rms[b], rws[b]);
+        hsg_bf16x8_t a[2][3];
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int l = 0; l < 3; ++l)
+                a[f][l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sA[b][l][ax(16 * f + r, g)]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int k = 2 * w + h;
+            if (k >= H) break;                                    // wave-uniform
+            const u32x4v m0 = *reinterpret_cast<const u32x4v *>(&sM[b][k][8 * g]);
+            const u32x4v m1 = *reinterpret_cast<const u32x4v *>(&sM[b][k][8 * g + 4]);
+            hsg_bf16x8_t bb[3];
+#pragma unroll
+            for (int l = 0; l < 3; ++l)
+                bb[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sW[b][l][aw(k * 8 + (r & 7), g)]);
+            const uint32_t wd[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+            hsg_u32x4_t M[2];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t t0 = wd[2 * q] << sh, t1 = wd[2 * q + 1] << sh;
+                M[0][q] = __builtin_amdgcn_perm(t1, t0, 0x0A0A0808u);    // row r:      sign bytes of bit 15
+                M[1][q] = __builtin_amdgcn_perm(t1, t0, 0x0B0B0909u);    // row r + 16: sign bytes of bit 31
+            }
+#pragma unroll
+            for (int f = 0; f < 2; ++f) {
+                const hsg_bf16x8_t x0 = __builtin_bit_cast(hsg_bf16x8_t, __builtin_bit_cast(hsg_u32x4_t, a[f][0]) & M[f]);
+                const hsg_bf16x8_t x1 = __builtin_bit_cast(hsg_bf16x8_t, __builtin_bit_cast(hsg_u32x4_t, a[f][1]) & M[f]);
+                const hsg_bf16x8_t x2 = __builtin_bit_cast(hsg_bf16x8_t, __builtin_bit_cast(hsg_u32x4_t, a[f][2]) & M[f]);
+                f32x4v c = acc[f][h];                             // smallest limb products first
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x2, bb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, bb[1], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bb[2], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x1, bb[0], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bb[1], c, 0, 0, 0);
+                acc[f][h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x0, bb[0], c, 0, 0, 0);
+            }
+        }
+    };
+    for (int s = 0; s < nst; s += 2) {
+        step(s, 0);
+        if (s + 1 < nst) step(s + 1, 1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int k = 2 * w + h;
+        if (k >= H) break;
+        const float av = a1 ? a1[k * 8 + (r & 7)] : 0.f;
+#pragma unroll
+        for (int f = 0; f < 2; ++f)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = rt * 32 + 16 * f + 4 * g + e;
+                const float z = acc[f][h][e] * scale;
+                if (r < 8 && i < n) Z[(size_t)i * ldz + k * 8 + r] = z;
+                if (a1) {
+                    float sg = z * av;                            // lanes r = 0..7: one head's 8 outputs
+                    sg += __shfl_xor(sg, 1);
+                    sg += __shfl_xor(sg, 2);
+                    sg += __shfl_xor(sg, 4);
+                    if (r == 0 && i < n) sigma[(size_t)i * H + k] = sg;
+                }
+            }
+    }
+}
+
 // ------------------------------------------------------------------ dX ----
 // v_mfma_f32_16x16x4_f32, no LDS.  One wave = 16 rows x (16*CT) input columns.
 // Per head k the K = D product  t = dZ[i0.., kD..kD+D) W[kD.., c..]  runs on MFMA
@@ -1274,6 +1430,27 @@ int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float 
     const int bpr = (H + 1) / 2;
     hipLaunchKernelGGL((k_hproj_fwd_v8<2, 2>), dim3((unsigned)((nrt + 7) / 8 * 8 * bpr)), dim3(256), 0, st, n, in, H,
                        X, ldx, Wt, bits, s, Z, ldz, a1, sigma);
+    return status();
+}
+
+// D = 8 on bf16 limb MFMAs (k_hproj_fwd_mf): W as hsg_wsplit planes [3][Np][Kp] of
+// W [H*8][in] (rows = outputs)
+int hsg_hproj_fwd_mf_supported(int in, int H, int D) {
+    return D == 8 && H >= 1 && H <= 8 && in >= 4 && in % 4 == 0 ? 1 : 0;
+}
+int hsg_hproj_fwd_mf(int n, int in, int H, const float *X, int ldx, const void *planes, int Np, int Kp,
+                     const uint32_t *bits, float p, float *Z, int ldz, const float *a1, float *sigma, void *stream) {
+    if (n < 0 || !hsg_hproj_fwd_mf_supported(in, H, 8) || ldx < in || ldx % 4 != 0 || ldz < H * 8 || !X ||
+        !planes || !bits || !Z || !aligned16(X) || !aligned16(planes) || Np < H * 8 || Kp < in || Kp % 32 != 0 ||
+        !fits_buffers(n, in, H, 8, ldx) || (long)3 * Np * Kp * 2 >= (long)kOOB)
+        return HSG_EINVAL;
+    if ((a1 == nullptr) != (sigma == nullptr)) return HSG_EINVAL;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const float s = drop_scale(p);
+    const dim3 grid((unsigned)((n + 31) / 32));
+    hipLaunchKernelGGL(k_hproj_fwd_mf, grid, dim3(256), 0, st, n, in, H, X, ldx,
+                       reinterpret_cast<const __bf16 *>(planes), Np, Kp, bits, s, Z, ldz, a1, sigma);
     return status();
 }
 

@@ -17,6 +17,43 @@ __device__ __forceinline__ void hsg_split3(float x, __bf16 &x0, __bf16 &x1, __bf
     x2 = (__bf16)(r - (float)x1);         // exact difference, then RNE
 }
 
+// RNE split of 8 fp32 values into three bf16 limb vectors (two values per 32-bit word),
+// x = l0 + l1 + l2 exactly: l0 = RNE(x) and l1 = RNE(x - l0) by v_cvt_pk_bf16_f32 (two
+// values per instruction), l2 = x - l0 - l1 (at most 8 significant bits: exact in bf16,
+// packed by v_perm_b32).  11 VALU per pair, limb magnitudes |l1| <= 2^-9 |x|,
+// |l2| <= 2^-18 |x|: the dropped products a1 b2 + a2 b1 stay <= 2^-26 |ab|.  The
+// subtractions are pinned to scalar v_sub_f32 (inline asm): SLP-packed v_pk_add_f32 beside
+// MFMAs is an anti-lever on gfx950 (MI355X_MICROARCH.md, price of one filler).  The low
+// element is unpacked by a byte permute, (a & 0xffff) << 16: written as a shift, the
+// compiler saw through it and re-converted that element alone (v_cvt_pk_bf16_f32 x, 0).
+typedef unsigned int hsg_u32x4_t __attribute__((ext_vector_type(4)));
+typedef float hsg_f32x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 hsg_bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void hsg_split_rne_pair(float va, float vb, unsigned &w0, unsigned &w1, unsigned &w2) {
+    const unsigned a = __builtin_bit_cast(unsigned, hsg_bf16x2_t{(__bf16)va, (__bf16)vb});
+    w0 = a;
+    float ra, rb, sa, sb;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(ra) : "v"(va), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, a, 0x01000c0cu))));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(rb) : "v"(vb), "v"(__uint_as_float(a & 0xFFFF0000u)));
+    const unsigned b = __builtin_bit_cast(unsigned, hsg_bf16x2_t{(__bf16)ra, (__bf16)rb});
+    w1 = b;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(sa) : "v"(ra), "v"(__uint_as_float(__builtin_amdgcn_perm(0u, b, 0x01000c0cu))));
+    asm("v_sub_f32 %0, %1, %2" : "=v"(sb) : "v"(rb), "v"(__uint_as_float(b & 0xFFFF0000u)));
+    w2 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+}
+__device__ __forceinline__ void hsg_split_rne8(const hsg_f32x4_t x, const hsg_f32x4_t y, hsg_u32x4_t &w0,
+                                               hsg_u32x4_t &w1, hsg_u32x4_t &w2) {
+    const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned a, b, c;
+        hsg_split_rne_pair(v[2 * p], v[2 * p + 1], a, b, c);
+        w0[p] = a;
+        w1[p] = b;
+        w2[p] = c;
+    }
+}
+
 struct HsgWSplitJobs {
     const float *W[4];
     __bf16 *out[4];

@@ -508,6 +508,12 @@ int hsg_hproj_wt(int H, int D, int in, const float *W, float *Wt, void *stream);
 int hsg_hproj_fwd_t8_supported(int in, int H, int D);
 int hsg_hproj_fwd_t8(int n, int in, int H, const float *X, int ldx, const float *Wt, const uint32_t *bits,
                      float p, float *Z, int ldz, const float *a1, float *sigma, void *stream);
+/* The D = 8 forward on bf16 limb MFMAs (round 5): the same Z / sigma as
+ * hsg_hproj_fwd_t8 to fp32 rounding, W given as its hsg_wsplit limb planes
+ * [3][Np][Kp] (hsg_wsplit_dims(H*8, in)).  H <= 8, in % 4 == 0, X 16-byte aligned. */
+int hsg_hproj_fwd_mf_supported(int in, int H, int D);
+int hsg_hproj_fwd_mf(int n, int in, int H, const float *X, int ldx, const void *planes, int Np, int Kp,
+                     const uint32_t *bits, float p, float *Z, int ldz, const float *a1, float *sigma, void *stream);
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
                  const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);

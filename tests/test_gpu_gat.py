@@ -136,13 +136,19 @@ def random_docs(kind, seed):
     if kind == "hsg_hub":
         # 70 sentences all containing the same few words (>64-edge S2W segments)
         return [synth.make_hsg_doc(rng, N=70, W=6, k=4, tf_range=(0.0, 1.0))]
+    if kind == "hsg_skew":
+        # short S2W segments on average (~2.2 edges: the destination-batch forward) with
+        # four hub words in 100 sentences each (>64-edge segments inside that kernel)
+        return [synth.make_hsg_doc(rng, N=100, W=4, k=3, tf_range=(0.0, 1.0))] + \
+            [synth.make_hsg_doc(rng, N=35, W=600, k=36, tf_range=(0.0, 1.0)) for _ in range(3)]
     if kind == "hdsg":
         return [synth.make_hdsg_example(rng, tuple(int(x) for x in rng.integers(1, 6, size=3)), W=60, k=8,
                                         doc_words=25, tf_range=(0.0, 1.0)) for _ in range(3)]
     raise KeyError(kind)
 
 
-@pytest.mark.parametrize("kind,seed", [("hsg_edge", 0), ("hsg_edge", 1), ("hsg_hub", 0), ("hdsg", 0)])
+@pytest.mark.parametrize("kind,seed", [("hsg_edge", 0), ("hsg_edge", 1), ("hsg_hub", 0), ("hsg_skew", 0),
+                                       ("hdsg", 0)])
 def test_gat_vs_oracle_random_graphs(kind, seed):
     z = synth_fixture(random_docs(kind, seed))
     r = run_gat(z, 7 + seed)

@@ -139,3 +139,46 @@ def test_dw_4x4x1_equals_16x16x4_kernel(monkeypatch, n, d_in, H, D):
     err = ((outs[0].double() - outs[1].double()).abs() / mag.clamp_min(1e-30)).max().item()
     print(f"4x4x1 vs 16x16x4 dW: max |diff| / sum|terms| = {err:.2e}")
     assert err < 1e-6
+
+
+@pytest.mark.parametrize("n,d_in,H", [(19200, 300, 8), (70, 300, 8), (100, 20, 2), (50, 304, 4), (33, 8, 5),
+                                      (1000, 64, 8)])
+def test_fwd_mfma_limbs_match_fp64_and_valu_kernel(n, d_in, H):
+    """hsg_hproj_fwd_mf (D = 8 on bf16 limb MFMAs, W as hsg_wsplit planes) against the
+    fp64 masked reference and the VALU kernel hsg_hproj_fwd_t8 on the same keep bits:
+    Z and the fused source logits to fp32 rounding."""
+    from hetersumgraph_amd._lib import load, ptr, stream_of
+    from hetersumgraph_amd.dense import split_dims, split_weights
+    from hetersumgraph_amd.hproj import dropmask_bits, transposed_weight
+    lib = load()
+    D, p = 8, 0.1
+    torch.manual_seed(n + H)
+    X = torch.randn(n, d_in, device="cuda")
+    W = torch.randn(H * D, d_in, device="cuda") / d_in ** 0.5
+    a1 = torch.randn(H, D, device="cuda")
+    bits = dropmask_bits(X, H, p)
+    (sw,) = split_weights((W, False))
+    Np, Kp = split_dims(H * D, d_in)
+    outs = []
+    for kind in ("mf", "t8"):
+        Z = torch.full((n, H * D), float("nan"), device="cuda")
+        sg = torch.full((n, H), float("nan"), device="cuda")
+        if kind == "mf":
+            rc = lib.hsg_hproj_fwd_mf(n, d_in, H, ptr(X), d_in, ptr(sw.planes), Np, Kp, ptr(bits), p, ptr(Z), H * D,
+                                      ptr(a1), ptr(sg), stream_of(X))
+        else:
+            wt = transposed_weight(W, H, D)
+            rc = lib.hsg_hproj_fwd_t8(n, d_in, H, ptr(X), d_in, ptr(wt), ptr(bits), p, ptr(Z), H * D, ptr(a1),
+                                      ptr(sg), stream_of(X))
+        assert rc == 0
+        outs.append((Z, sg))
+    torch.cuda.synchronize()
+    keep = unpack(bits, n).double()
+    scale = 1.0 / (1.0 - float(int(p * 65536)) / 65536)
+    Zr = torch.einsum("kic,kdc->ikd", keep * X.double().unsqueeze(0) * scale, W.double().view(H, D, d_in))
+    sr = (Zr * a1.double().unsqueeze(0)).sum(-1)
+    Zr = Zr.reshape(n, H * D)
+    tol = 2e-6 * max(1.0, Zr.abs().max().item())
+    for Z, sg in outs:
+        assert (Z.double() - Zr).abs().max().item() < tol
+        assert (sg.double() - sr).abs().max().item() < 4 * tol * max(1.0, a1.abs().max().item())
