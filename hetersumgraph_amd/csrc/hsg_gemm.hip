@@ -2590,6 +2590,10 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     if (plan == 40 && epi_rows_ok(p)) return launch7<64, 2, 0, 2, true>(p, pl, Np, Kp, st);   // hoisted DMA offsets
     if (plan == 41 && epi_rows_ok(p))                       // + 80-wide tiles for N <= 320
         return N <= 320 ? launch7<80, 2, 0, 2, true>(p, pl, Np, Kp, st) : launch7<64, 2, 0, 2, true>(p, pl, Np, Kp, st);
+    if (plan == 43 && epi_rows_ok(p))                       // + hoisted DMA offsets
+        return N <= 320 && (N + 111) / 112 * 112 <= Np ? launch7<112, 2, 0, 2, true>(p, pl, Np, Kp, st)
+                                                       : launch7<64, 2, 0, 2, true>(p, pl, Np, Kp, st);
+    if (plan == 44 && epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);     // round-4 default: 64-wide
     if (plan != 27) return launch5<64, 2>(p, pl, Np, Kp, st);
     if (gemm11_on()) {
         // one round of big tiles (k_gemm11, dev opt-in: measured slower)
@@ -2600,7 +2604,14 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
             return rc;
     }
 #endif
-    if (epi_rows_ok(p)) return launch7<64, 2>(p, pl, Np, Kp, st);
+    // N <= 320 (ffn2 y = H W2^T at N = 300): 112-wide tiles, 3 per row band instead of 5
+    // of 64 -- 450 tiles at cfg2, ONE round of the 512 resident blocks instead of 1.46 --
+    // and each wave's A split feeds 7 instead of 4 column subtiles: 44.1 -> 39.1 us back
+    // to back (tools/gemm5_sweep.py, plan 42 against 27; same products, bitwise)
+    // (where the planes' padded rows cover the 112-wide tiles; else 64)
+    if (epi_rows_ok(p))
+        return N <= 320 && (N + 111) / 112 * 112 <= Np ? launch7<112, 2>(p, pl, Np, Kp, st)
+                                                       : launch7<64, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2, 0>(p, pl, Np, Kp, st);             // unaligned / ragged quads
 }
 
