@@ -34,7 +34,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_gat_bwd_dst_g", "hsg_gemm_f32_psw_elug", "hsg_gemm_bf16_psw",
            "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
            "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate",
-           "hsg_gat_bwd_src_g_blocks", "hsg_gemm_bf16_psw_io", "hsg_gemm_bf16_psw_elug_rho_a16", "hsg_ln_bwd_dy16",
+           "hsg_gat_bwd_src_g_blocks", "hsg_gemm_bf16_psw_io", "hsg_gemm_bf16_psw_elug_rho_a16", "hsg_gemm_psw_elug_rho_gw", "hsg_ln_bwd_dy16",
            "hsg_gemm_dw_slabs_io", "hsg_ln_fwd_y16", "hsg_gat_bwd_src_g_io")
 
 HSG_EPI_STORE = 0
@@ -141,6 +141,7 @@ _SIGS = {
     "hsg_gemm_psw_elug_rho": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P],
     "hsg_gemm_bf16_psw_io": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _I, _P, _I, _P],
     "hsg_gemm_bf16_psw_elug_rho_a16": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _P, _P, _I, _P, _I, _I, _P],
+    "hsg_gemm_psw_elug_rho_gw": [_I, _I, _I, _I, _I],
     "hsg_ln_bwd_dy16": [_I, _I, _P, _P, _I, _P, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _I, _P, _P, _P],
     "hsg_ln_fwd_y16": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_gat_bwd_src_g_io": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P],

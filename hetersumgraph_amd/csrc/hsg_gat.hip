@@ -1423,7 +1423,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
                                                       const float *__restrict__ mv,
                                                       const float *__restrict__ lv,
                                                       const float *__restrict__ G,
-                                                      const float *__restrict__ rhop, int rgroups,
+                                                      const float *__restrict__ rhop, int rgroups, int rgw,
                                                       const float *__restrict__ a1,
                                                       const float *__restrict__ Z,
                                                       float *__restrict__ dZ, float *__restrict__ dsigma,
@@ -1441,10 +1441,10 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
     float *sd = s_dtau[wid];
     for (int i = lane; i < HSG_NT * HSG_HMAX; i += 64) sd[i] = 0.f;
     wave_lds_sync();
-    // rho partial addresses of head kc: 64-column groups r0 (and r1 when the head
-    // straddles two; D <= 64), slot = head - first head of the group
-    const int r0 = c0 / 64, r1 = (c0 + D - 1) / 64;
-    const int o0 = r0 * 3 + (kc - (64 * r0) / D), o1 = r1 * 3 + (kc - (64 * r1) / D);
+    // rho partial addresses of head kc: rgw-column groups r0 (and r1 when the head
+    // straddles two; D <= rgw), slot = head - first head of the group
+    const int r0 = c0 / rgw, r1 = (c0 + D - 1) / rgw;
+    const int o0 = r0 * 3 + (kc - (rgw * r0) / D), o1 = r1 * 3 + (kc - (rgw * r1) / D);
     float da1[NE];                                // wave 0: sum_u dsigma[u,k] Z[u,k,:], (k, l) features
     int fo[NE];                                   // the lane's features c0 + d, clamped to the head
 #pragma unroll
@@ -2430,15 +2430,18 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
                     next_pow2(H), slope, sigma, tau, m, l, G, nullptr, a1, Z, dZ, dsigma, da1_part, rho, dtau_part);
         return launch_status();
     }
-    if (!srcg_wide(rel, H, D) || rho_groups != (H * D + 63) / 64) return HSG_EINVAL;
+    // the group width of the rho partials (hsg_gemm_psw_elug_rho_gw): 64, or 112 (the dx
+    // GEMM's 112-wide tiles); the two layouts coincide where their group counts do
+    const int rgw = rho_groups == (H * D + 63) / 64 ? 64 : rho_groups == (H * D + 111) / 112 ? 112 : 0;
+    if (!srcg_wide(rel, H, D) || rgw == 0 || D > rgw) return HSG_EINVAL;
     const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;
 #define HSG_SG(NE_, OCC_, EQ_)                                                                               \
     if (g_bf16)                                                                                              \
         HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_, true>), grid, dim3(256), st, R, H, D, lph,   \
-                    slope, sigma, tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part);    \
+                    slope, sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part);\
     else                                                                                                     \
         HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope,  \
-                    sigma, tau, m, l, G, rho, rho_groups, a1, Z, dZ, dsigma, da1_part, dtau_part)
+                    sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part)
     // EQ: destination rows in flight per wave, as many as fit 5 blocks per CU unspilled
 #ifdef HSG_DEV
     const char *eq = HSG_DEV_ENV("HSG_SRCG_EQ");                               // dev A/B

@@ -939,9 +939,18 @@ typedef __bf16 bf16x4v7 __attribute__((ext_vector_type(4)));
 // operand (the relu' mask H) read as bf16 quads (8 B) at the same element offsets
 // GBF: the ELU-gate epilogue's G rows stored as bf16 (the bf16 mode; rho is summed from
 // the fp32 G before the rounding)
+// Lane map: a row's QPR quads on QS = 16 / 32 / 64 lanes (the power of two >= QPR), RPS
+// rows per step.  rho groups (HSG_EPI_ADD_ELUG): 64 columns for tiles of a multiple of 64
+// (16 lanes), the whole tile row for other widths (GW = BN: 112-wide tiles, 32 lanes).
+template <int BN>
+struct EpiMap {
+    static constexpr int QPR = BN / 4, QS = QPR <= 16 ? 16 : QPR <= 32 ? 32 : 64, RPS = 64 / QS;
+    static constexpr int GW = BN % 64 == 0 ? 64 : BN;
+};
 template <int BN, bool CBF = false, bool AUXBF = false, bool GBF = false>
 struct EpiRows {
-    static constexpr int LDW = BN + 4, QPR = BN / 4, RPS = 64 / QPR;
+    static constexpr int LDW = BN + 4, QPR = EpiMap<BN>::QPR, QS = EpiMap<BN>::QS, RPS = EpiMap<BN>::RPS;
+    static constexpr int GW = EpiMap<BN>::GW;
     static constexpr int STEPS = (32 + RPS - 1) / RPS;
     f32x4 bn, aux[STEPS], ex[STEPS];
     bf16x4v7 auxb[AUXBF ? STEPS : 1];
@@ -950,7 +959,7 @@ struct EpiRows {
     // requested together; k_gemm7 issues this before its last K tile's MFMAs so the
     // round trip overlaps them
     __device__ __forceinline__ void load(const GemmArgs &p, int row0, int col0, int lane) {
-        const int q = lane % QPR, rs = lane / QPR;
+        const int q = min(lane % QS, QPR - 1), rs = lane / QS;
         const int n = col0 + 4 * q;
         const int nc = min(n, p.N - 4);                    // N % 4 == 0 (host-checked): whole quads
         bn = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -982,16 +991,15 @@ struct EpiRows {
                                            f32x4 &csum) {
         __builtin_amdgcn_s_waitcnt(0xc07f);                 // lgkmcnt(0): the wave's own LDS writes
         __builtin_amdgcn_wave_barrier();
-        const int q = lane % QPR, rs = lane / QPR;
+        const int q = lane % QS, rs = lane / QS;
         const int n = col0 + 4 * q;
-        const bool qok = rs < RPS && n < p.N;
-        // rho partials (BN % 64 == 0: the 16 lanes of a 64-column group are lanes
-        // 16c .. 16c + 15 of one row step): head slot of each of the lane's 4 columns
-        constexpr bool RHO_OK = BN % 64 == 0;
-        const bool rho = RHO_OK && p.epi == HSG_EPI_ADD_ELUG && p.rho;
+        const bool qok = q < QPR && rs < RPS && n < p.N;
+        // rho partials per GW-column group (the GW / 4 lanes of a group are consecutive
+        // lanes of one row step): head slot of each of the lane's 4 columns
+        const bool rho = p.epi == HSG_EPI_ADD_ELUG && p.rho;
         int slot[4] = {3, 3, 3, 3};
         if (rho) {
-            const int hb = (n & ~63) / p.rho_d;
+            const int hb = (n / GW * GW) / p.rho_d;
 #pragma unroll
             for (int e = 0; e < 4; ++e) slot[e] = n + e < p.N ? (n + e) / p.rho_d - hb : 3;
         }
@@ -1054,9 +1062,9 @@ struct EpiRows {
             }
             if (rho) {                                      // wave-uniform: sums over the group
 #pragma unroll
-                for (int s = 0; s < 3; ++s) c[s] = row16_sum(c[s]);
-                if ((q & 15) == 0 && qok && rok) {
-                    float *dst = p.rho + ((size_t)m * ((p.N + 63) / 64) + n / 64) * 3;
+                for (int s = 0; s < 3; ++s) c[s] = hsg_group_sum<GW == 64 ? 16 : QS>(c[s]);
+                if (q % (GW / 4) == 0 && qok && rok) {
+                    float *dst = p.rho + ((size_t)m * ((p.N + GW - 1) / GW) + n / GW) * 3;
                     dst[0] = c[0];
                     dst[1] = c[1];
                     dst[2] = c[2];
@@ -1079,10 +1087,10 @@ __device__ __forceinline__ void epi_rows(const float *wl, int row0, int col0, in
 template <int BN>
 __device__ __forceinline__ void epi_rows_colpart(float *red, const f32x4 &cs, int wid, int lane, int ty, int n0,
                                                  const GemmArgs &p) {
-    constexpr int QPR = BN / 4, RPS = 64 / QPR;
-    const int q = lane % QPR, rs = lane / QPR;
+    constexpr int QPR = EpiMap<BN>::QPR, QS = EpiMap<BN>::QS, RPS = EpiMap<BN>::RPS;
+    const int q = lane % QS, rs = lane / QS;
     __syncthreads();
-    if (rs < RPS) *reinterpret_cast<f32x4 *>(&red[(wid * RPS + rs) * BN + 4 * q]) = cs;
+    if (q < QPR && rs < RPS) *reinterpret_cast<f32x4 *>(&red[(wid * RPS + rs) * BN + 4 * q]) = cs;
     __syncthreads();
     const int rows64 = (p.M + 63) / 64;
     for (int cc = threadIdx.x; cc < 2 * BN; cc += 256) {
@@ -2745,6 +2753,25 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
     return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, io, (hipStream_t)stream);
 }
 
+// the dx GEMM with the ELU gate (fp32 mode): 112-wide tiles for N <= 320, as the plain
+// GEMM, where the weight planes cover them and every 112-column rho group meets at most
+// three heads (the edge backward reads three slots per group); else 64
+static int elug_gw(int M, int N, int K, int head_dim) {
+    (void)M;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    if (N > 320 || (N + 111) / 112 * 112 > Np) return 64;
+#ifdef HSG_DEV
+    if (const char *e = HSG_DEV_ENV("HSG_ELUG_GW")) if (atoi(e) == 64) return 64;     // dev A/B
+#endif
+    if (head_dim > 0) {
+        if (head_dim > 112) return 64;
+        for (int g0 = 0; g0 < N; g0 += 112)
+            if ((min(g0 + 112, N) - 1) / head_dim - g0 / head_dim > 2) return 64;
+    }
+    return 112;
+}
+
 int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     (void)K; (void)bf16;
     if (M < 0 || N < 1) return 0;
@@ -2771,10 +2798,16 @@ int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const vo
     p.rho = rho;
     p.rho_d = head_dim;
     if (!epi_rows_ok(p)) return HSG_EINVAL;
-    // every k_gemm7 plan's column tile is a multiple of 64 (EpiRows' rho groups); the
-    // dev library's k_gemm11 declines a rho GEMM (try11), so it falls through to k_gemm7
+    // rho groups: 64 columns, or the 112-wide tile (elug_gw); the dev library's k_gemm11
+    // declines a rho GEMM (try11), so it falls through to k_gemm7
     if (bf16) return launch7b(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+    if (elug_gw(M, N, K, head_dim) == 112)
+        return launch7<112, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
     return launch7<64, 2>(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, (hipStream_t)stream);
+}
+
+int hsg_gemm_psw_elug_rho_gw(int M, int N, int K, int head_dim, int bf16) {
+    return bf16 ? 64 : elug_gw(M, N, K, head_dim);
 }
 
 // hsg_gemm_psw_elug_rho in the bf16 mode on a bf16 A (the FFN's bf16 dH rows; lda %

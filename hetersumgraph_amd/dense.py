@@ -220,12 +220,21 @@ def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out
     return True
 
 
+def elug_rho_groups(Bs, M, head_dim):
+    """Groups per row of the rho partials gemm_psw_elug writes for this weight split:
+    ceil(N / W), W = hsg_gemm_psw_elug_rho_gw (64, or 112 on the fp32 mode's 112-wide
+    tiles)."""
+    gw = load().hsg_gemm_psw_elug_rho_gw(M, Bs.N, Bs.K, int(head_dim), int(Bs.mode == "bf16"))
+    return (Bs.N + gw - 1) // gw
+
+
 def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
     """out = out + A @ B^T (the FFN backward's dx += dH W1) and, in the same epilogue,
     G = out * elu'(h) with elu(h) = x - origin (hsg_gemm_f32_psw_elug: the edge
     layer's ELU gate, GAT.py:56-57, moved out of its dst pass).  ``rho`` ([M,
-    ceil(N/64), 3]): also the per-64-column partials of G . h per head of ``head_dim``
-    columns (hsg_gemm_psw_elug_rho) for the one-pass edge backward.  Returns False
+    elug_rho_groups(Bs, M, head_dim), 3]): also the per-column-group partials of G . h
+    per head of ``head_dim`` columns (hsg_gemm_psw_elug_rho) for the one-pass edge
+    backward.  Returns False
     (nothing launched) when the shape / alignment does not allow the fused epilogue."""
     lib = load()
     M, K = A.shape
@@ -233,7 +242,7 @@ def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
     ts = (out, x, origin, G)
     if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in ts):
         return False
-    if rho is not None and (rho.shape != (M, (N + 63) // 64, 3) or not rho.is_contiguous()):
+    if rho is not None and (rho.shape != (M, elug_rho_groups(Bs, M, head_dim), 3) or not rho.is_contiguous()):
         return False
     if rho is not None and rho.dtype != torch.float32:
         raise RuntimeError("gemm_psw_elug: rho partials are fp32")

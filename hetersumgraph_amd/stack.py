@@ -37,7 +37,7 @@ import torch
 from . import _lib
 from . import rng as hsg_rng
 from ._lib import load, stream_of
-from .dense import gemm, gemm_dw_slabs, gemm_slabs
+from .dense import elug_rho_groups, gemm, gemm_dw_slabs, gemm_slabs
 from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
@@ -203,7 +203,8 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     if elug is not None and merged:
         # ... and the rho partials, so the edge backward is one source-centric pass
         n_dst, HD = elug[1].shape
-        elug += (elug[1].new_empty(n_dst, (HD + 63) // 64, 3, dtype=torch.float32), gsaved[13])
+        groups = elug_rho_groups(fsaved[11][3], n_dst, gsaved[13])     # the dx GEMM's (W1^T split)
+        elug += (elug[1].new_empty(n_dst, groups, 3, dtype=torch.float32), gsaved[13])
     # narrow heads (W2S) with h stored: the narrow FFN's backward epilogue makes G and the
     # per-head rho, and the edge backward is one head-lane pass over the words
     gate = None

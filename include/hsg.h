@@ -115,7 +115,7 @@ int hsg_gat_bwd_src_blocks(const hsg_rel *rel);
 /* The whole backward of one table-mode application in ONE source-centric pass (the
  * S2W shape: D in [32, 64], long CSC segments -- hsg_gat_bwd_src_g_supported), given
  * G = dOut * elu'(h) and rho[v][g][s] = the per-64-column-group partials of
- * G_v . h_v that hsg_gemm_psw_elug_rho writes (rho_groups = ceil(H*D / 64)):
+ * G_v . h_v that hsg_gemm_psw_elug_rho writes (rho_groups = ceil(H*D / W), W its group width):
  *   dpre[e,k]   = alpha_ek (G[v,k,:] . Z[u,k,:] - rho_vk) * leaky'(pre_ek)
  *   dZ, dsigma, da1_part as hsg_gat_bwd_src, dtau_part[b][box][k] per-block partials
  * with b < hsg_gat_bwd_src_g_blocks(rel, H, D) for both slabs.  Replaces hsg_gat_bwd_dst_g +
@@ -271,12 +271,16 @@ int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const vo
                           const float *aux, const float *x, const float *origin, float *G, int ld, int bf16,
                           void *stream);
 /* hsg_gemm_f32_psw_elug that also writes rho (optional: NULL = the call above) for
- * hsg_gat_bwd_src_g: rho[m][g][s], g < ceil(N / 64), s < 3, = sum of G[m,c] * h[m,c]
- * over the columns c of group g (64g <= c < 64g + 64) in head c / head_dim =
- * 64g / head_dim + s, h = e for e > 0 else log1p(e); head_dim >= 32 divides N. */
+ * hsg_gat_bwd_src_g: rho[m][g][s], g < ceil(N / W), s < 3, = sum of G[m,c] * h[m,c]
+ * over the columns c of group g (Wg <= c < Wg + W) in head c / head_dim =
+ * Wg / head_dim + s, h = e for e > 0 else log1p(e); head_dim >= 32 divides N.  The
+ * group width W = hsg_gemm_psw_elug_rho_gw(M, N, K, head_dim, bf16): 64, or 112 in the
+ * fp32 mode for N <= 320 (the GEMM's 112-wide tiles; round 5) when every group meets at
+ * most three heads. */
 int hsg_gemm_psw_elug_rho(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,
                           const float *aux, const float *x, const float *origin, float *G, int ld, float *rho,
                           int head_dim, int bf16, void *stream);
+int hsg_gemm_psw_elug_rho_gw(int M, int N, int K, int head_dim, int bf16);
 /* hsg_gemm_bf16 (A and the weight rounded to bf16 RNE, fp32 accumulation: config 5's
  * mode) on the pre-split weight: only its limb plane 0 = RNE(W) is read, one bf16
  * MFMA product per element pair.  Same arguments as hsg_gemm_f32_psw; N % 4 == 0 and

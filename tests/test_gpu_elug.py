@@ -133,17 +133,18 @@ def test_dst_pass_with_given_G_equals_noh_pass():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
 
 
-def _rho_ref(G, h, D):
-    """fp64 rho partials: [M, ceil(N/64), 3], slot s of 64-column group g = the sum of
-    G * h over the group's columns in head 64g // D + s (hsg_gemm_psw_elug_rho)."""
+def _rho_ref(G, h, D, gw=64):
+    """fp64 rho partials: [M, ceil(N/gw), 3], slot s of gw-column group g = the sum of
+    G * h over the group's columns in head gw g // D + s (hsg_gemm_psw_elug_rho; gw = 64,
+    or 112 on the fp32 mode's 112-wide dx tiles)."""
     M, N = G.shape
-    ng = (N + 63) // 64
+    ng = (N + gw - 1) // gw
     prod = G.double() * h.double()
     out = torch.zeros(M, ng, 3, dtype=torch.float64, device=G.device)
     for g in range(ng):
-        hb = 64 * g // D
+        hb = gw * g // D
         for s in range(3):
-            cols = [c for c in range(64 * g, min(64 * g + 64, N)) if c // D == hb + s]
+            cols = [c for c in range(gw * g, min(gw * g + gw, N)) if c // D == hb + s]
             if cols:
                 out[:, g, s] = prod[:, cols].sum(1)
     return out
@@ -161,7 +162,7 @@ def test_psw_elug_rho_partials(M, mode):
     second term: the log and the summation roundings; the kernel takes u log u with
     u = 1 + e rounded, whose rounding moves G h by <= |v| ulp(1)).  Rows with h = -20
     take the e <= -1 branch (G h = 0) where e + 1 rounds to zero or below."""
-    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    from hetersumgraph_amd.dense import elug_rho_groups, gemm_dtype, gemm_psw_elug, split_weights
     N, K, D = 300, 512, 50
     torch.manual_seed(M + 1)
     dH = torch.randn(M, K, device="cuda")
@@ -178,16 +179,20 @@ def test_psw_elug_rho_partials(M, mode):
     for with_rho in (False, True):
         out = ds.clone()
         G = torch.empty_like(ds)
-        rho = torch.full((M, (N + 63) // 64, 3), float("nan"), device="cuda") if with_rho else None
+        ng = elug_rho_groups(S, M, D)                          # f32: 112-wide groups (3), bf16: 64 (5)
+        rho = torch.full((M, ng, 3), float("nan"), device="cuda") if with_rho else None
         assert gemm_psw_elug(dH, S, out, x, origin, G, rho, D if with_rho else 0)
         outs.append((out, G, rho))
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     G, rho = outs[1][1], outs[1][2]
-    ref = _rho_ref(G, h, D)
+    gw = 112 if rho.shape[1] == (N + 111) // 112 and rho.shape[1] != (N + 63) // 64 else 64
+    assert gw == (112 if mode == "f32" else 64)
+    ref = _rho_ref(G, h, D, gw)
     out = outs[1][0]
     delta = 4 * 2.0 ** -23 * (x.abs() + origin.abs()) + 2.0 ** -23
-    bound = _rho_ref(out.abs(), delta * (h.abs() + 1), D) + 1e-5 * _rho_ref(G.abs(), h.abs() + 1, D) + 1e-12
+    bound = (_rho_ref(out.abs(), delta * (h.abs() + 1), D, gw) + 1e-5 * _rho_ref(G.abs(), h.abs() + 1, D, gw)
+             + 1e-12)
     err = (rho.double() - ref).abs()
     print(f"{mode} M={M}: worst rho error / bound {(err / bound).max().item():.3f}")
     assert torch.isfinite(rho).all()
@@ -202,7 +207,7 @@ def test_psw_elug_rho_under_big_tile_switch(mode, monkeypatch):
     run without the switch, C and G too.  Dev library only."""
     from helpers import skip_unless_dev
     skip_unless_dev(False)
-    from hetersumgraph_amd.dense import gemm_dtype, gemm_psw_elug, split_weights
+    from hetersumgraph_amd.dense import elug_rho_groups, gemm_dtype, gemm_psw_elug, split_weights
     M, N, K, D = 19200, 300, 512, 50
     torch.manual_seed(5)
     dH = torch.randn(M, K, device="cuda")
@@ -216,7 +221,7 @@ def test_psw_elug_rho_under_big_tile_switch(mode, monkeypatch):
     for switch in ("0", "1"):
         monkeypatch.setenv("HSG_GEMM11", switch)
         out, G = ds.clone(), torch.empty_like(ds)
-        rho = torch.full((M, (N + 63) // 64, 3), float("nan"), device="cuda")
+        rho = torch.full((M, elug_rho_groups(S, M, D), 3), float("nan"), device="cuda")
         assert gemm_psw_elug(dH, S, out, x, origin, G, rho, D)
         outs.append((out, G, rho))
     torch.cuda.synchronize()
@@ -226,18 +231,19 @@ def test_psw_elug_rho_under_big_tile_switch(mode, monkeypatch):
 
 
 def test_psw_elug_rho_declines_bad_head_dim():
-    from hetersumgraph_amd.dense import gemm_psw_elug, split_weights
+    from hetersumgraph_amd.dense import elug_rho_groups, gemm_psw_elug, split_weights
     W1 = torch.randn(64, 300, device="cuda")
     (S,) = split_weights((W1, True))
     t = torch.randn(50, 300, device="cuda")
-    rho = torch.empty(50, 5, 3, device="cuda")
     for hd in (16, 70):                                         # < 32 / does not divide N
+        rho = torch.empty(50, elug_rho_groups(S, 50, hd), 3, device="cuda")
         assert not gemm_psw_elug(torch.randn(50, 64, device="cuda"), S, t.clone(), t, t, torch.empty_like(t),
                                  rho, hd)
 
 
+@pytest.mark.parametrize("gw", [64, 112])
 @pytest.mark.parametrize("n_docs,N,W,k", [(4, 35, 600, 36), (3, 20, 200, 24)])
-def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k):
+def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k, gw):
     """hsg_gat_bwd_src_g (one source-centric pass on G and the rho partials) against
     hsg_gat_bwd_dst_g + hsg_gat_bwd_src on the same S2W application, forward stats
     from a real forward: dZ and every attention-parameter gradient within 1e-5 of the
@@ -268,7 +274,7 @@ def test_one_pass_edge_bwd_equals_two_pass(n_docs, N, W, k):
     e = (out - org).double()
     G = torch.where(e > 0, dout.double(), dout.double() * (e + 1)).float()
     h = torch.where(e > 0, e, torch.log1p(e.clamp_min(-1 + 1e-12)))
-    rho = _rho_ref(G, h, D).float().contiguous()
+    rho = _rho_ref(G, h, D, gw).float().contiguous()          # the 64- or 112-column group layout
     res = []
     for merged in (False, True):
         dst = (torch.zeros_like(attn), torch.zeros_like(wf), torch.zeros_like(bf), torch.zeros_like(T), False, False)

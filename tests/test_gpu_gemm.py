@@ -579,7 +579,7 @@ def test_bf16_io_elug_rho_bitwise(M):
     outs = []
     for A, gdt in ((dHb.float().contiguous(), torch.float32), (dHb, torch.float32), (dHb, torch.bfloat16)):
         out, G = ds.clone(), torch.empty_like(ds, dtype=gdt)
-        rho = torch.empty(M, (N + 63) // 64, 3, device="cuda")
+        rho = torch.empty(M, (N + 63) // 64, 3, device="cuda")          # the bf16 mode: 64-column groups
         assert gemm_psw_elug(A, S, out, x, origin, G, rho, D)
         outs.append((out, G, rho))
     torch.cuda.synchronize()
