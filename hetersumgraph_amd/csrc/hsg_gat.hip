@@ -421,13 +421,21 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
 // over the lanes of each head, merged across the block's 4 waves through LDS and a
 // barrier, then the alphas staged in LDS and the Z rows gathered -- i.e. four dependent
 // memory round trips and two block barriers per destination.  Here one wave owns a
-// destination and lane f its feature f (head f / D) end to end: lane j < EB loads edge
-// j's (source, box) once, the wave broadcasts them by readlane, and every lane requests
-// its own head's (sigma, tau) and its Z feature for all EB edges at once; the softmax
-// is online per lane over the batch (one rescale per batch), so h = sum_e p_e Z_u / l
-// needs no alpha staging and no cross-lane reduction.  Chain: indptr -> (src, box) ->
-// (sigma, tau, Z) -> stores.  Same numbers as k_gat_fwd up to fp32 summation order
-// (the per-edge exp and the accumulation order differ); m, l as it writes them.
+// destination and lane f its feature f (head f / D) end to end: lane j loads edge j's
+// (source, box) for up to 64 edges at once; then per sub-batch of EB edges every lane
+// requests, for each edge (source and box broadcast by readlane into SGPRs), its head's
+// sigma and its Z feature by buffer loads (scalar row offset, per-lane feature offset:
+// no address VALU) and reads tau from the block's LDS copy of the table.  The loads
+// are unconditional (edges past the segment repeat the last one, weight 0) so a
+// sub-batch's 2 EB loads issue back to back, and the next sub-batch's loads are issued
+// before this one's arithmetic.  The softmax is online per lane over the sub-batch (one
+// rescale per sub-batch), h = sum_e p_e Z_u / l: no alpha staging, no cross-lane
+// reduction.  Same numbers as k_gat_fwd up to fp32 summation order; m, l as it writes.
+// Measured (dev, HSG_GAT_FWD_SP=16 | 8): 25.5 / 30.4 us per cfg2 W2S launch against 7.9
+// us for k_gat_fwd's four waves per destination -- 1,120 destinations are ~one wave per
+// SIMD here, so each wave's whole issue stream (readlanes, 2 loads and ~10 VALU per edge)
+// and its round trips are exposed; the first round-5 form (a per-edge branch that made
+// every edge wait for its own loads) ran 16-17 us.  Dev only.
 template <int TAU_MODE, int EB>
 __global__ __launch_bounds__(256) void k_gat_fwd_sp(RelPtrs R, int H, int D, float slope,
                                                     const float *__restrict__ Z,
@@ -436,51 +444,69 @@ __global__ __launch_bounds__(256) void k_gat_fwd_sp(RelPtrs R, int H, int D, flo
                                                     const float *__restrict__ origin,
                                                     float *__restrict__ hout, float *__restrict__ out,
                                                     float *__restrict__ mout, float *__restrict__ lout) {
+    static_assert(TAU_MODE == HSG_TAU_TABLE, "the tau table staged in LDS");
+    __shared__ float s_tau[HSG_NT * HSG_HMAX];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const bool fok = lane < HD;
     const int f = fok ? lane : HD - 1;
     const int kf = div_small(f, 1.f / (float)D);
+    for (int i = threadIdx.x; i < HSG_NT * H; i += blockDim.x) s_tau[i] = tau[i];
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t zr = buf_rsrc(Z, (long)R.n_src * HD * 4);
+    const __amdgpu_buffer_rsrc_t sr = buf_rsrc(sigma, (long)R.n_src * H * 4);
+    const unsigned fb = 4u * (unsigned)f, kb = 4u * (unsigned)kf;
     const WorkRange wr = work_range(R.n_dst, HSG_WAVES, wid, R.xcd);
     for (int v_ = wr.first; v_ < wr.end; v_ += wr.stride) {
         const int v = __builtin_amdgcn_readfirstlane(v_);
         const int beg = R.indptr[v], end = R.indptr[v + 1], c = R.phantom[v];
         const float org = origin ? origin[(size_t)v * HD + f] : 0.f;
         float m = -INFINITY, l = 0.f, acc = 0.f;
-        for (int e0 = beg; e0 < end; e0 += EB) {
-            const int nb = min(EB, end - e0);
-            int uj = 0, tj = 0;
-            if (lane < nb) {
-                uj = R.src[e0 + lane];
-                tj = tau_row<TAU_MODE>(R, e0 + lane);
-            }
-            float sc[EB], zz[EB];
+        for (int e0 = beg; e0 < end; e0 += 64) {
+            const int nb = min(64, end - e0);
+            const int ej = e0 + min(lane, nb - 1);              // lanes past the chunk repeat its last edge
+            const int uj = R.src[ej], tj = tau_row<TAU_MODE>(R, ej);
+            float sg[2][EB], zz[2][EB];
+            int tt[2][EB];
+            auto issue = [&](int b, float (&sgb)[EB], float (&zzb)[EB], int (&ttb)[EB]) {
 #pragma unroll
-            for (int j = 0; j < EB; ++j) {
-                if (j < nb) {                                    // wave-uniform
-                    const int u = __builtin_amdgcn_readlane(uj, j), t = __builtin_amdgcn_readlane(tj, j);
-                    sc[j] = sigma[u * H + kf] + tau[t * H + kf];
-                    zz[j] = Z[(size_t)u * HD + f];
+                for (int j = 0; j < EB; ++j) {
+                    const int jj = min(b * EB + j, 63);
+                    const int u = __builtin_amdgcn_readlane(uj, jj);
+                    ttb[j] = __builtin_amdgcn_readlane(tj, jj);
+                    sgb[j] = buf_ld(sr, kb, (unsigned)u * H * 4u);
+                    zzb[j] = buf_ld(zr, fb, (unsigned)u * HD * 4u);
                 }
-            }
-            float bm = m;
+            };
+            const int nsb = (nb + EB - 1) / EB;
+            issue(0, sg[0], zz[0], tt[0]);
+            for (int b = 0; b < nsb; ++b) {
+                const int cur = b & 1;
+                if (b + 1 < nsb) {
+                    if (cur == 0) issue(b + 1, sg[1], zz[1], tt[1]);
+                    else issue(b + 1, sg[0], zz[0], tt[0]);
+                }
+                float sc[EB];
+                float bm = m;
 #pragma unroll
-            for (int j = 0; j < EB; ++j)
-                if (j < nb) {
-                    sc[j] = leaky(sc[j], slope);
+                for (int j = 0; j < EB; ++j) {
+                    const bool ok = b * EB + j < nb;                 // wave-uniform
+                    const float x = leaky((cur ? sg[1][j] : sg[0][j]) + s_tau[(cur ? tt[1][j] : tt[0][j]) * H + kf],
+                                          slope);
+                    sc[j] = ok ? x : -INFINITY;
                     bm = fmaxf(bm, sc[j]);
                 }
-            const float r = __expf(m - bm);                     // m = -inf on the first batch: 0
-            acc *= r;
-            l *= r;
+                const float r = __expf(m - bm);                      // m = -inf on the first batch: 0
+                acc *= r;
+                l *= r;
 #pragma unroll
-            for (int j = 0; j < EB; ++j)
-                if (j < nb) {
-                    const float pj = __expf(sc[j] - bm);
+                for (int j = 0; j < EB; ++j) {
+                    const float pj = __expf(sc[j] - bm);             // 0 past the segment
                     l += pj;
-                    acc = fmaf(pj, zz[j], acc);
+                    acc = fmaf(pj, cur ? zz[1][j] : zz[0][j], acc);
                 }
-            m = bm;
+                m = bm;
+            }
         }
         if (c > 0) {                                             // phantom in-edges: e = 0, no message
             const float bm = fmaxf(m, 0.f), r = __expf(m - bm);
@@ -2036,13 +2062,13 @@ int bwd_src_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D,
 
 // dst-side launch shape (fwd and bwd_dst share it; the d tau slab has one row per block)
 int dst_wpn(const hsg_rel *r) { return wpn_for(r->n_dst, r->n_edges); }
-// single-pass narrow-row forward (k_gat_fwd_sp): its edge batch, 0 = off.  Measured
-// slower than the 4-wave k_gat_fwd on the cfg2 W2S destinations (17.4 / 16.2 us with
-// 64- / 32-edge batches against 7.8 us, profiles/r05/): dev opt-in (HSG_GAT_FWD_SP=32|64)
+// single-pass narrow-row forward (k_gat_fwd_sp): its sub-batch of edges, 0 = off.  Measured
+// slower than the 4-wave k_gat_fwd on the cfg2 W2S destinations (see the kernel): dev
+// opt-in (HSG_GAT_FWD_SP=16|8)
 int fwd_sp() {
     const char *e = HSG_DEV_ENV("HSG_GAT_FWD_SP");
     const int eb = e ? atoi(e) : 0;
-    return eb == 0 ? 0 : (eb == 32 ? 32 : 64);
+    return eb == 0 ? 0 : (eb == 8 ? 8 : 16);
 }
 int src_wpn(const hsg_rel *r) { return wpn_for(r->n_src, r->n_edges); }
 // destinations per wave batch of the short-segment forward (k_gat_fwd_b, dev only); 0 =
@@ -2100,18 +2126,14 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
 #endif
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
-    if (nf == 1 && fwd_sp()) {                      // narrow rows: one single-pass wave per destination
+    if (nf == 1 && fwd_sp() && tau_mode == HSG_TAU_TABLE &&
+        (long)rel->n_src * H * D * 4 < 0x7fffffffL) {  // narrow rows: one single-pass wave per destination
         const dim3 g(grid_nodes(rel->n_dst, 1, kFwdGridCap));
         const int eb = fwd_sp();
 #define HSG_SP(TAU, EB_) HSG_KLAUNCH(true, true, (k_gat_fwd_sp<TAU, EB_>), g, dim3(256), st, R, H, D, slope, Z, sigma, \
                                      tau, origin, h, out, m, l)
-        if (tau_mode == HSG_TAU_TABLE) {
-            if (eb == 64) HSG_SP(HSG_TAU_TABLE, 64);
-            else HSG_SP(HSG_TAU_TABLE, 32);
-        } else {
-            if (eb == 64) HSG_SP(HSG_TAU_PER_EDGE, 64);
-            else HSG_SP(HSG_TAU_PER_EDGE, 32);
-        }
+        if (eb == 8) HSG_SP(HSG_TAU_TABLE, 8);
+        else HSG_SP(HSG_TAU_TABLE, 16);
 #undef HSG_SP
         return launch_status();
     }
