@@ -1634,8 +1634,16 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int NQ = DV / 4;
     __shared__ float s_tau[HSG_NT * HSG_HMAX];
-    __shared__ __attribute__((aligned(16))) float s_da1[HSG_WAVES][64 * DV];
-    __shared__ float s_dt[RHO ? 256 * HSG_NT : 1];
+    // d a1 partial rows padded to DV + 4 floats: the lanes' 16-byte stores then fall on
+    // 16 distinct 4-bank slots per 16-lane group (at DV = 8, 32 B apart, they were 2-way)
+    constexpr int DA = DV + 4;
+    __shared__ __attribute__((aligned(16))) float s_da1[HSG_WAVES][64 * DA];
+    // d tau lane partials box-major, rows of 264: the reduction's reads of one (wave,
+    // slot) across lanes (t = i / 8, head i % 8) then sit on banks 8 t + head, distinct
+    // within a wave (thread-major with 11 per thread they collided 2-way: 1.6e5
+    // SQ_LDS_BANK_CONFLICT per launch)
+    constexpr int DTS = 264;
+    __shared__ float s_dt[RHO ? DTS * HSG_NT : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int sl = lane / hp, k = lane - sl * hp;
@@ -1744,20 +1752,20 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
     }
     if (da1_part) {
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) *reinterpret_cast<f4 *>(&s_da1[wid][lane * DV + 4 * q]) = da1[q];
+        for (int q = 0; q < NQ; ++q) *reinterpret_cast<f4 *>(&s_da1[wid][lane * DA + 4 * q]) = da1[q];
         __syncthreads();
         for (int f = threadIdx.x; f < HD; f += blockDim.x) {
             const int kk = f / D, d = f - kk * D;
             float a = 0.f;
 #pragma unroll
             for (int w = 0; w < HSG_WAVES; ++w)
-                for (int ss = 0; ss < wpw; ++ss) a += s_da1[w][(ss * hp + kk) * DV + d];
+                for (int ss = 0; ss < wpw; ++ss) a += s_da1[w][(ss * hp + kk) * DA + d];
             da1_part[(size_t)blockIdx.x * HD + f] = a;
         }
     }
     if constexpr (RHO) {                     // d tau block partials, lanes in (wave, slot) order
 #pragma unroll
-        for (int t = 0; t < HSG_NT; ++t) s_dt[threadIdx.x * HSG_NT + t] = dt[t];
+        for (int t = 0; t < HSG_NT; ++t) s_dt[t * DTS + threadIdx.x] = dt[t];
         __syncthreads();
         const int nt = HSG_NT * H;
         for (int i = threadIdx.x; i < nt; i += blockDim.x) {
@@ -1765,7 +1773,7 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_hl(RelPtrs R, int H, int D,
             float a = 0.f;
 #pragma unroll
             for (int w = 0; w < HSG_WAVES; ++w)
-                for (int ss = 0; ss < wpw; ++ss) a += s_dt[(w * 64 + ss * hp + kk) * HSG_NT + t];
+                for (int ss = 0; ss < wpw; ++ss) a += s_dt[t * DTS + w * 64 + ss * hp + kk];
             dtau_part[(size_t)blockIdx.x * nt + i] = a;
         }
     }
