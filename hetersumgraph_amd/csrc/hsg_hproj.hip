@@ -1090,6 +1090,139 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
     }
 }
 
+// ---------------------------------------------- dW on bf16 limb MFMAs (round 5) ----
+// D = 8, H <= 8 (the W2S projection).  k_hproj_dw pads each 8-wide head to a 16-wide
+// slot of v_mfma_f32_16x16x4_f32 (half its exact-f32 MFMA work is zeros) and was 53 %
+// issue-stalled.  Here  dW_k = dZ_k^T (M_k o X)  runs on v_mfma_f32_16x16x32_bf16 with
+// the K axis = 32 rows, fp32-accurate (three RNE bf16 limbs per operand, six products):
+// C[m][c] += A[m][i] B[i][c], A = dZ^T of head k (rows m = its 8 outputs, repeated in
+// m = 8..15 and discarded), B = the keep-masked X.  The keep bits of 32 rows at one
+// column are ONE mask word -- the MFMA's K axis is the word's axis -- so a lane's 8 rows
+// are one byte of it, and a 256-entry LDS table turns that byte into the four 16-bit
+// lane masks of its bf16 pairs (one ds_read_b128 instead of ~12 VALU).
+// Block = 64 columns (wave w: columns 16w .. 16w + 15) x all heads x one chunk of rows
+// (the 16x16x4 kernel's chunking, so the partial slabs part[chunk][H*8][in] are the
+// same); per 32-row step the block stages, double-buffered with the next step's
+// global loads in registers: X and dZ split ONCE into limb images stored column-major
+// (thread = (column, 8 rows): 8 coalesced dword loads, three ds_write_b128), and the
+// step's mask words.  A wave then reads its B fragments once, and per head its A
+// fragments, the table entry and the masked B (12 v_and), and runs 6 MFMAs.
+constexpr int kDwMfP = 40;                        // image row pitch (bf16): 8-row fragments 80 B apart
+__global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, int rows_per_chunk,
+                                                       const float *__restrict__ dZ, int ldz,
+                                                       const float *__restrict__ X, int ldx,
+                                                       const uint32_t *__restrict__ bits, float *__restrict__ part) {
+    constexpr int HM = 8;
+    __shared__ __attribute__((aligned(16))) __bf16 sX[2][3][64 * kDwMfP];    // X limbs [column][row]
+    __shared__ __attribute__((aligned(16))) __bf16 sZ[2][3][64 * kDwMfP];    // dZ limbs [output][row]
+    __shared__ uint32_t sM[2][HM][64];                                       // keep words [head][column]
+    __shared__ __attribute__((aligned(16))) hsg_u32x4_t s_lut[256];          // byte -> bf16-pair masks
+    const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c0 = blockIdx.x * 64;
+    const int rb = blockIdx.y * rows_per_chunk;
+    const int rend = min(rb + rows_per_chunk, n);
+    {
+        hsg_u32x4_t e;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            e[q] = ((tid >> (2 * q)) & 1 ? 0x0000FFFFu : 0u) | ((tid >> (2 * q + 1)) & 1 ? 0xFFFF0000u : 0u);
+        s_lut[tid] = e;
+    }
+    const auto rX = rsrc(X, (long)n * ldx * 4);
+    const auto rZ = rsrc(dZ, (long)n * ldz * 4);
+    const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
+    // staging: thread = (column sc, rows 8 sr .. 8 sr + 7) of X and of dZ; mask words
+    // (head tid / 64 and 4 + tid / 64, column tid % 64)
+    const int sc = tid & 63, sr = tid >> 6;
+    const int gx = c0 + sc;
+    const bool xok = gx < in, zok = sc < H * 8;
+    float vx[8], vz[8];
+    uint32_t vm[2];
+    auto gload = [&](int r0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int r = r0 + 8 * sr + j;
+            const bool rok = r < rend;
+            vx[j] = __uint_as_float(bldu(rX, rok && xok ? (uint32_t)(r * ldx + gx) * 4 : kOOB));
+            vz[j] = __uint_as_float(bldu(rZ, rok && zok ? (uint32_t)(r * ldz + sc) * 4 : kOOB));
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k = sr + 4 * u;
+            vm[u] = bldu(rM, k < H && gx < LDC ? (uint32_t)((k * NWI + r0 / 32) * LDC + gx) * 4 : kOOB);
+        }
+    };
+    auto lstore = [&](int b) {
+        hsg_u32x4_t x0, x1, x2, z0, z1, z2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            unsigned a, bb, c;
+            hsg_split_rne_pair(vx[2 * q], vx[2 * q + 1], a, bb, c);
+            x0[q] = a; x1[q] = bb; x2[q] = c;
+            hsg_split_rne_pair(vz[2 * q], vz[2 * q + 1], a, bb, c);
+            z0[q] = a; z1[q] = bb; z2[q] = c;
+        }
+        const int o = sc * kDwMfP + 8 * sr;
+        *reinterpret_cast<hsg_u32x4_t *>(&sX[b][0][o]) = x0;
+        *reinterpret_cast<hsg_u32x4_t *>(&sX[b][1][o]) = x1;
+        *reinterpret_cast<hsg_u32x4_t *>(&sX[b][2][o]) = x2;
+        *reinterpret_cast<hsg_u32x4_t *>(&sZ[b][0][o]) = z0;
+        *reinterpret_cast<hsg_u32x4_t *>(&sZ[b][1][o]) = z1;
+        *reinterpret_cast<hsg_u32x4_t *>(&sZ[b][2][o]) = z2;
+        sM[b][sr][sc] = vm[0];
+        sM[b][sr + 4][sc] = vm[1];
+    };
+    f32x4v acc[HM];
+#pragma unroll
+    for (int k = 0; k < HM; ++k) acc[k] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int cl = lane & 15, ig = lane >> 4;
+    const int xo = (16 * w + cl) * kDwMfP + 8 * ig;               // B fragment: column 16w + cl, rows 8 ig ..
+    const int zo = (cl & 7) * kDwMfP + 8 * ig;                    // A fragment: output k*8 + (cl & 7)
+    if (rb < rend) gload(rb);
+    int b = 0;
+    for (int r0 = rb; r0 < rend; r0 += 32, b ^= 1) {
+        lstore(b);
+        __syncthreads();
+        if (r0 + 32 < rend) gload(r0 + 32);
+        hsg_u32x4_t bx[3];
+#pragma unroll
+        for (int l = 0; l < 3; ++l) bx[l] = *reinterpret_cast<const hsg_u32x4_t *>(&sX[b][l][xo]);
+#pragma unroll
+        for (int k = 0; k < HM; ++k) {
+            if (k >= H) break;                                    // wave-uniform
+            const uint32_t byte = (sM[b][k][16 * w + cl] >> (8 * ig)) & 0xFFu;
+            const hsg_u32x4_t M = s_lut[byte];
+            hsg_bf16x8_t az[3];
+#pragma unroll
+            for (int l = 0; l < 3; ++l)
+                az[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sZ[b][l][k * 8 * kDwMfP + zo]);
+            const hsg_bf16x8_t b0 = __builtin_bit_cast(hsg_bf16x8_t, bx[0] & M);
+            const hsg_bf16x8_t b1 = __builtin_bit_cast(hsg_bf16x8_t, bx[1] & M);
+            const hsg_bf16x8_t b2 = __builtin_bit_cast(hsg_bf16x8_t, bx[2] & M);
+            f32x4v c = acc[k];                                    // smallest limb products first
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[2], b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[1], b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[0], b2, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[1], b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[0], b1, c, 0, 0, 0);
+            acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[0], b0, c, 0, 0, 0);
+        }
+    }
+    // C: lane holds column 16w + cl, outputs 4 ig + e (ig < 2: the head's 8 outputs)
+    const int gc = c0 + 16 * w + cl;
+    if (ig < 2 && gc < in) {
+        float *dst = part + (size_t)blockIdx.y * H * 8 * in + gc;
+#pragma unroll
+        for (int k = 0; k < HM; ++k) {
+            if (k >= H) break;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dst[(size_t)(k * 8 + 4 * ig + e) * in] = acc[k][e];
+        }
+    }
+}
+
 // ------------------------------------------------- dW, narrow heads, 4x4x1 ----
 // (round 5) Heads of D % 4 == 0 with H * D <= 64 (the W2S projection: 8 heads x 8) on
 // v_mfma_f32_4x4x1_16b_f32: 16 independent 4 x 4 outer products per instruction, K = 1
@@ -1119,6 +1252,13 @@ struct DwM4Geom {
 // step): with the keep bit on the A value, each 4x4x1 MFMA (11 cycles alone) costs 27
 // cycles per wave (tools/census/mfma_rate_probe.hip), i.e. the two mask VALU per 256
 // MACs outweigh the padding the 16x16x4 form wastes.  Dev opt-in (HSG_HPROJ_DWM4=1).
+// the bf16 limb MFMA dW (k_hproj_dw_mf): D = 8, H <= 8 (dev A/B: HSG_HPROJ_DWMF=0 restores
+// the 16x16x4 kernel)
+bool dw_mf_shape(int in, int H, int D) {
+    if (const char *e = HSG_DEV_ENV("HSG_HPROJ_DWMF")) if (atoi(e) == 0) return false;
+    return D == 8 && H >= 1 && H <= 8 && in >= 1;
+}
+
 bool dw_m4_shape(int in, int H, int D) {
     const char *e = HSG_DEV_ENV("HSG_HPROJ_DWM4");
     return e && atoi(e) == 1 && D % 4 == 0 && H * D <= 64 && in % 4 == 0;
@@ -1517,6 +1657,7 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
 
 int hsg_hproj_dw_chunks(int n, int in, int H, int D) {
     if (n < 0 || in < 1 || H < 1 || D < 1) return 0;
+    if (dw_mf_shape(in, H, D)) return dw_geom(n, in, H, D).chunks;
     return dw_m4_shape(in, H, D) ? dw_m4_geom(n, in).chunks : dw_geom(n, in, H, D).chunks;
 }
 
@@ -1528,6 +1669,18 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     hipStream_t st = (hipStream_t)stream;
     DwGeom g = dw_geom(n, in, H, D);
     const long total = (long)H * D * in;
+    if (dw_mf_shape(in, H, D) && n > 0) {
+        // D = 8 on bf16 limb MFMAs, on the 16x16x4 kernel's row chunks (same slabs)
+        hipLaunchKernelGGL(k_hproj_dw_mf, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ, ldz,
+                           X, ldx, bits, part);
+        if (int rc = status()) return rc;
+        if (!dW) return 0;
+        int blocks = (int)((total + 255) / 256);
+        if (blocks > 2048) blocks = 2048;
+        hipLaunchKernelGGL(k_sum_parts, dim3(blocks), dim3(256), 0, st, total, g.chunks, drop_scale(p), part, dW,
+                           accumulate);
+        return status();
+    }
     if (dw_m4_shape(in, H, D)) {
         // the chunking is the 4x4x1 kernel's (hsg_hproj_dw_chunks); operands it cannot
         // take as 16-byte rows go to the 16x16x4 kernel on the same row chunks

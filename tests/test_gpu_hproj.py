@@ -124,6 +124,7 @@ def test_dw_4x4x1_equals_16x16x4_kernel(monkeypatch, n, d_in, H, D):
     dZ = torch.randn(n, H * D, device="cuda")
     bits = dropmask_bits(X, H, 0.1)
     outs = []
+    monkeypatch.setenv("HSG_HPROJ_DWMF", "0")                 # off the round-5 bf16 limb kernel
     for flag in ("1", "0"):
         monkeypatch.setenv("HSG_HPROJ_DWM4", flag)
         chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
@@ -182,3 +183,36 @@ def test_fwd_mfma_limbs_match_fp64_and_valu_kernel(n, d_in, H):
     for Z, sg in outs:
         assert (Z.double() - Zr).abs().max().item() < tol
         assert (sg.double() - sr).abs().max().item() < 4 * tol * max(1.0, a1.abs().max().item())
+
+
+@pytest.mark.parametrize("n,d_in,H", [(19200, 300, 8), (70, 300, 8), (100, 20, 2), (50, 304, 4), (33, 8, 5),
+                                      (1000, 64, 8), (4800, 300, 8)])
+def test_dw_mfma_limbs_match_fp64(n, d_in, H):
+    """hsg_hproj_dw for D = 8 (round 5: k_hproj_dw_mf, bf16 limb MFMAs, the keep byte
+    through the LDS table) against the fp64 masked reference dW = s sum_i dZ_k^T (M_k o X),
+    both as the summed partial slabs and through k_sum_parts: fp32 rounding relative to
+    the summed magnitudes."""
+    from hetersumgraph_amd._lib import load, ptr
+    from hetersumgraph_amd.hproj import dropmask_bits
+    lib = load()
+    D, p = 8, 0.1
+    torch.manual_seed(n + 7 * H)
+    X = torch.randn(n, d_in, device="cuda")
+    dZ = torch.randn(n, H * D, device="cuda")
+    bits = dropmask_bits(X, H, p)
+    chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+    part = torch.full((chunks * H * D * d_in,), float("nan"), device="cuda")
+    dW = X.new_empty(H * D, d_in)
+    assert lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), p, ptr(part), ptr(dW), 0,
+                            None) == 0
+    torch.cuda.synchronize()
+    keep = unpack(bits, n).double()
+    scale = 1.0 / (1.0 - float(int(p * 65536)) / 65536)
+    ref = torch.einsum("kic,ikd->kdc", keep * X.double().unsqueeze(0), dZ.double().view(n, H, D)) * scale
+    mag = torch.einsum("kic,ikd->kdc", keep * X.double().abs().unsqueeze(0), dZ.double().abs().view(n, H, D)) * scale
+    ref, mag = ref.reshape(H * D, d_in), mag.reshape(H * D, d_in)
+    assert torch.isfinite(part).all()
+    sums = part.view(chunks, H * D, d_in).double().sum(0) * scale
+    for got in (dW.double(), sums):
+        err = ((got - ref).abs() / mag.clamp_min(1e-30)).max().item()
+        assert err < 2e-6, err
