@@ -1105,9 +1105,12 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
 // same); per 32-row step the block stages, double-buffered with the next step's
 // global loads in registers: X and dZ split ONCE into limb images stored column-major
 // (thread = (column, 8 rows): 8 coalesced dword loads, three ds_write_b128), and the
-// step's mask words.  A wave then reads its B fragments once, and per head its A
+// step's mask words; two steps of global loads in flight (22.1 -> 20.2 us with one).  A wave then reads its B fragments once, and per head its A
 // fragments, the table entry and the masked B (12 v_and), and runs 6 MFMAs.
-constexpr int kDwMfP = 40;                        // image row pitch (bf16): 8-row fragments 80 B apart
+// kDwMfP: image row pitch (bf16).  40 (80 B): fragment reads 2-way, staging writes
+// conflict-free; 48 (96 B): reads conflict-free, writes 2-way (tools/lds_banks.py-style
+// check over gfx950's ds_read_b128 lane groups)
+template <int kDwMfP>
 __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, int rows_per_chunk,
                                                        const float *__restrict__ dZ, int ldz,
                                                        const float *__restrict__ X, int ldx,
@@ -1116,20 +1119,19 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
     __shared__ __attribute__((aligned(16))) __bf16 sX[2][3][64 * kDwMfP];    // X limbs [column][row]
     __shared__ __attribute__((aligned(16))) __bf16 sZ[2][3][64 * kDwMfP];    // dZ limbs [output][row]
     __shared__ uint32_t sM[2][HM][64];                                       // keep words [head][column]
-    __shared__ __attribute__((aligned(16))) hsg_u32x4_t s_lut[256];          // byte -> bf16-pair masks
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int c0 = blockIdx.x * 64;
-    const int rb = blockIdx.y * rows_per_chunk;
+    // XCD-aware order: workgroup b runs on XCD b % 8, so logical block L = xcd_order(b)
+    // puts the column tiles of one row chunk on one XCD and their dZ rows (re-read by
+    // every column tile) come from its L2 instead of HBM
+    const int ctiles = (int)gridDim.x, total = ctiles * (int)gridDim.y;
+    const int bl = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int L = (bl & 7) * (total >> 3) + min(bl & 7, total & 7) + (bl >> 3);     // a bijection
+    const int chunk = L / ctiles;
+    const int c0 = (L % ctiles) * 64;
+    const int rb = chunk * rows_per_chunk;
     const int rend = min(rb + rows_per_chunk, n);
-    {
-        hsg_u32x4_t e;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-            e[q] = ((tid >> (2 * q)) & 1 ? 0x0000FFFFu : 0u) | ((tid >> (2 * q + 1)) & 1 ? 0xFFFF0000u : 0u);
-        s_lut[tid] = e;
-    }
     const auto rX = rsrc(X, (long)n * ldx * 4);
     const auto rZ = rsrc(dZ, (long)n * ldz * 4);
     const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
@@ -1138,9 +1140,10 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
     const int sc = tid & 63, sr = tid >> 6;
     const int gx = c0 + sc;
     const bool xok = gx < in, zok = sc < H * 8;
-    float vx[8], vz[8];
-    uint32_t vm[2];
-    auto gload = [&](int r0) {
+    // two steps of global loads in flight: register sets 0 / 1 for even / odd steps
+    float vxs[2][8], vzs[2][8];
+    uint32_t vms[2][2];
+    auto gload = [&](int r0, float (&vx)[8], float (&vz)[8], uint32_t (&vm)[2]) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int r = r0 + 8 * sr + j;
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             vm[u] = bldu(rM, k < H && gx < LDC ? (uint32_t)((k * NWI + r0 / 32) * LDC + gx) * 4 : kOOB);
         }
     };
-    auto lstore = [&](int b) {
+    auto lstore = [&](int b, const float (&vx)[8], const float (&vz)[8], const uint32_t (&vm)[2]) {
         hsg_u32x4_t x0, x1, x2, z0, z1, z2;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1180,20 +1183,26 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
     const int cl = lane & 15, ig = lane >> 4;
     const int xo = (16 * w + cl) * kDwMfP + 8 * ig;               // B fragment: column 16w + cl, rows 8 ig ..
     const int zo = (cl & 7) * kDwMfP + 8 * ig;                    // A fragment: output k*8 + (cl & 7)
-    if (rb < rend) gload(rb);
-    int b = 0;
-    for (int r0 = rb; r0 < rend; r0 += 32, b ^= 1) {
-        lstore(b);
+    if (rb < rend) gload(rb, vxs[0], vzs[0], vms[0]);
+    if (rb + 32 < rend) gload(rb + 32, vxs[1], vzs[1], vms[1]);
+    auto step = [&](int r0, int b) {                             // b = step parity (compile-time below)
+        lstore(b, vxs[b], vzs[b], vms[b]);
         __syncthreads();
-        if (r0 + 32 < rend) gload(r0 + 32);
+        if (r0 + 64 < rend) gload(r0 + 64, vxs[b], vzs[b], vms[b]);
         hsg_u32x4_t bx[3];
 #pragma unroll
         for (int l = 0; l < 3; ++l) bx[l] = *reinterpret_cast<const hsg_u32x4_t *>(&sX[b][l][xo]);
 #pragma unroll
         for (int k = 0; k < HM; ++k) {
             if (k >= H) break;                                    // wave-uniform
-            const uint32_t byte = (sM[b][k][16 * w + cl] >> (8 * ig)) & 0xFFu;
-            const hsg_u32x4_t M = s_lut[byte];
+            // the lane's 8 rows are bits 8 ig .. 8 ig + 7 of the word: pair q's mask from
+            // bits 2q / 2q + 1 shifted to 15 / 31 and v_perm_b32's sign-byte selectors (a
+            // 256-entry LDS table here cost 2.3e6 bank-conflict cycles per launch: random rows)
+            const uint32_t x = sM[b][k][16 * w + cl] >> (8 * ig);
+            hsg_u32x4_t M;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                M[q] = __builtin_amdgcn_perm(x << (30 - 2 * q), x << (15 - 2 * q), 0x0B0B0808u);
             hsg_bf16x8_t az[3];
 #pragma unroll
             for (int l = 0; l < 3; ++l)
@@ -1209,11 +1218,15 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[0], b1, c, 0, 0, 0);
             acc[k] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(az[0], b0, c, 0, 0, 0);
         }
+    };
+    for (int r0 = rb; r0 < rend; r0 += 64) {
+        step(r0, 0);
+        if (r0 + 32 < rend) step(r0 + 32, 1);
     }
     // C: lane holds column 16w + cl, outputs 4 ig + e (ig < 2: the head's 8 outputs)
     const int gc = c0 + 16 * w + cl;
     if (ig < 2 && gc < in) {
-        float *dst = part + (size_t)blockIdx.y * H * 8 * in + gc;
+        float *dst = part + (size_t)chunk * H * 8 * in + gc;
 #pragma unroll
         for (int k = 0; k < HM; ++k) {
             if (k >= H) break;
@@ -1671,8 +1684,17 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
     const long total = (long)H * D * in;
     if (dw_mf_shape(in, H, D) && n > 0) {
         // D = 8 on bf16 limb MFMAs, on the 16x16x4 kernel's row chunks (same slabs)
-        hipLaunchKernelGGL(k_hproj_dw_mf, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ, ldz,
-                           X, ldx, bits, part);
+#ifdef HSG_DEV
+        // dev A/B: pitch 48 (conflict-free fragment reads): 22.05 / 22.21 vs 22.53 / 22.17 us
+        // with pitch 40 back to back -- the 2-way reads do not bound it
+        const char *pe = HSG_DEV_ENV("HSG_HPROJ_DWMF_P");
+        if (pe && atoi(pe) == 48)
+            hipLaunchKernelGGL(k_hproj_dw_mf<48>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
+                               ldz, X, ldx, bits, part);
+        else
+#endif
+            hipLaunchKernelGGL(k_hproj_dw_mf<40>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
+                               ldz, X, ldx, bits, part);
         if (int rc = status()) return rc;
         if (!dW) return 0;
         int blocks = (int)((total + 255) / 256);
