@@ -1098,15 +1098,18 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
 // C[m][c] += A[m][i] B[i][c], A = dZ^T of head k (rows m = its 8 outputs, repeated in
 // m = 8..15 and discarded), B = the keep-masked X.  The keep bits of 32 rows at one
 // column are ONE mask word -- the MFMA's K axis is the word's axis -- so a lane's 8 rows
-// are one byte of it, and a 256-entry LDS table turns that byte into the four 16-bit
-// lane masks of its bf16 pairs (one ds_read_b128 instead of ~12 VALU).
+// are one byte of it, turned into the four 16-bit lane masks of its bf16 pairs by two
+// shifts and a v_perm_b32 with sign-byte selectors per pair (a 256-entry LDS table
+// instead: 2.3e6 bank-conflict cycles per launch, its rows are random).
 // Block = 64 columns (wave w: columns 16w .. 16w + 15) x all heads x one chunk of rows
 // (the 16x16x4 kernel's chunking, so the partial slabs part[chunk][H*8][in] are the
-// same); per 32-row step the block stages, double-buffered with the next step's
-// global loads in registers: X and dZ split ONCE into limb images stored column-major
-// (thread = (column, 8 rows): 8 coalesced dword loads, three ds_write_b128), and the
-// step's mask words; two steps of global loads in flight (22.1 -> 20.2 us with one).  A wave then reads its B fragments once, and per head its A
-// fragments, the table entry and the masked B (12 v_and), and runs 6 MFMAs.
+// same), the chunks XCD-local (their dZ rows, re-read by every column tile, stay in
+// one L2); per 32-row step the block stages, double-buffered in LDS with two steps of
+// global loads in flight in registers (22.1 -> 20.2 us against one): X and dZ split ONCE
+// into limb images stored column-major (thread = (column, 8 rows): 8 coalesced dword
+// loads, three ds_write_b128), and the step's mask words.  A wave then reads its B
+// fragments once, and per head its A fragments and mask word, masks B (12 + 12 VALU)
+// and runs 6 MFMAs.
 // kDwMfP: image row pitch (bf16).  40 (80 B): fragment reads 2-way, staging writes
 // conflict-free; 48 (96 B): reads conflict-free, writes 2-way (tools/lds_banks.py-style
 // check over gfx950's ds_read_b128 lane groups)
