@@ -758,7 +758,20 @@ __global__ __launch_bounds__(256) void k_hproj_dx(int n, int in, int H, int D, c
 // the reduction index of head k's two 16x16x4 steps is hd = kD + 2 lk + s, so the
 // lane's dZ pair is one 8-byte load: 8 + 16 + 8 vector loads per wave instead of the
 // chained kernel's 112 dword loads.  Heads are added in head order.
-template <int HH, int HG>
+// byte B of y as a float (v_cvt_f32_ubyteB); spelled out because the compiler, knowing
+// each byte of the spread keep bits is 0 or 1, would rewrite (y >> 8B) & 0xff into a
+// v_bfe_u32 + v_cvt_f32_ubyte0 pair
+template <int B>
+__device__ __forceinline__ float cvt_ubyte(uint32_t y) {
+    float f;
+    if constexpr (B == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(f) : "v"(y));
+    else if constexpr (B == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(f) : "v"(y));
+    else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(f) : "v"(y));
+    return f;
+}
+
+template <int HH, int HG, bool SPREAD = true>
 __global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const float *__restrict__ dZ, int ldz,
                                                      const float *__restrict__ W,
                                                      const uint32_t *__restrict__ bits, float scale,
@@ -812,11 +825,25 @@ __global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[f][1], bv[f][1][t], acc[t], 0, 0, 0);
-            if (k0 + f < H) {
+            if (!SPREAD && k0 + f < H) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) tot[t][r] += ((mw[f][t] >> (sh + r)) & 1u) ? acc[t][r] : 0.f;
+            }
+            if (SPREAD && k0 + f < H) {
+                // the tile's 4 keep bits (rows 4 lk .. +3) spread to bytes 0..3
+                // (bit i -> bit 8i: x * 0x204081), each byte -> 0.0 / 1.0 by
+                // v_cvt_f32_ubyteN, then one fma per value: 2.75 VALU per value
+                // instead of select + add on a compare (+ the AGPR read)
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t y = (__builtin_amdgcn_ubfe(mw[f][t], sh, 4) * 0x204081u) & 0x01010101u;
+                    tot[t][0] = __builtin_fmaf(cvt_ubyte<0>(y), acc[t][0], tot[t][0]);
+                    tot[t][1] = __builtin_fmaf(cvt_ubyte<1>(y), acc[t][1], tot[t][1]);
+                    tot[t][2] = __builtin_fmaf(cvt_ubyte<2>(y), acc[t][2], tot[t][2]);
+                    tot[t][3] = __builtin_fmaf(cvt_ubyte<3>(y), acc[t][3], tot[t][3]);
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1644,8 +1671,14 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         aligned16(dX) && ((uintptr_t)dZ & 7) == 0 && aligned16(W)) {
         // narrow heads: 16-byte operand pieces, all requested up front (W2S)
         // two heads' operands at a time (22.4 us cold; 4 / 8 at a time: 23.2 / 23.1 us)
-        hipLaunchKernelGGL((k_hproj_dx_n8<8, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, dZ, ldz,
-                           W, bits, s, dX, ldx, accumulate);
+        // dev A/B: HSG_HPROJ_DX_SEL=1 restores the compare + select masking
+        const char *se = HSG_DEV_ENV("HSG_HPROJ_DX_SEL");
+        if (se && atoi(se) == 1)
+            hipLaunchKernelGGL((k_hproj_dx_n8<8, 2, false>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in,
+                               H, dZ, ldz, W, bits, s, dX, ldx, accumulate);
+        else
+            hipLaunchKernelGGL((k_hproj_dx_n8<8, 2>), dim3((unsigned)((wide + 3) / 4)), dim3(256), 0, st, n, in, H, dZ,
+                               ldz, W, bits, s, dX, ldx, accumulate);
         return status();
     }
     if (mode != 0 && (wide < 2048 || mode == 2) && H <= 16 && D <= 64) {
