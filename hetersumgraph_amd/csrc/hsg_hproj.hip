@@ -145,6 +145,7 @@ struct DropJobs {
     uint32_t *bits[8];
     int start[9];
     int njobs;
+    int upt;                                         // units per thread (blocks of 256 * upt units)
     // optional: the narrow-head projection's weight transpose (hsg_hproj_wt) in the
     // blocks after the masks' (W == nullptr: none)
     const float *W;
@@ -185,10 +186,17 @@ __global__ __launch_bounds__(256) void k_dropmask_multi(DropJobs j, const int64_
     }
     int q = 0;
     while (q + 1 < j.njobs && (int)blockIdx.x >= j.start[q + 1]) ++q;
-    const long t = (long)((int)blockIdx.x - j.start[q]) * 256 + threadIdx.x;
+    // upt units per thread (256 apart: each pass stays coalesced), so the per-wave
+    // prologue -- the job search, the seed load, the key -- is paid once per upt units
+    const long t0 = (long)((int)blockIdx.x - j.start[q]) * 256 * j.upt + threadIdx.x;
     const long total = (long)((j.H[q] + 1) / 2) * ((j.n[q] + 31) / 32) * mask_ldc(j.in[q]);
-    if (t >= total) return;
-    dropmask_unit(j.n[q], j.in[q], j.H[q], thr16(j.p[q]), drop_key(seedp, j.offset[q]), t, j.bits[q]);
+    if (t0 >= total) return;
+    const uint32_t thr = thr16(j.p[q]), key = drop_key(seedp, j.offset[q]);
+    for (int u = 0; u < j.upt; ++u) {
+        const long t = t0 + 256L * u;
+        if (t >= total) break;
+        dropmask_unit(j.n[q], j.in[q], j.H[q], thr, key, t, j.bits[q]);
+    }
 }
 
 // ---------------------------------------------------------------- forward ----
@@ -1502,12 +1510,16 @@ int hsg_step_prologue(int njobs, const int *n, const int *in, const int *H, cons
     j.wIn = wIn;
     j.njobs = njobs;
     j.start[0] = 0;
+    // 2 units per thread: 26.1 -> 24.4 us per cfg2 prologue (4: 24.6, 8: 27.1;
+    // profiles/r05/ab_dropmask_upt/)
+    j.upt = 2;
+    if (const char *e = HSG_DEV_ENV("HSG_DROPMASK_UPT")) j.upt = max(1, min(16, atoi(e)));    // dev A/B
     for (int q = 0; q < njobs; ++q) {
         if (n[q] < 0 || in[q] < 1 || H[q] < 1 || p[q] < 0.f || p[q] >= 1.f || !bits[q]) return HSG_EINVAL;
         if ((long)n[q] * in[q] * ((H[q] + 1) / 2) >= (1L << 32)) return HSG_EINVAL;
         j.n[q] = n[q]; j.in[q] = in[q]; j.H[q] = H[q]; j.p[q] = p[q]; j.offset[q] = offset[q]; j.bits[q] = bits[q];
         const long total = (long)((H[q] + 1) / 2) * ((n[q] + 31) / 32) * mask_ldc(in[q]);
-        j.start[q + 1] = j.start[q] + (int)((total + 255) / 256);
+        j.start[q + 1] = j.start[q] + (int)((total + 256L * j.upt - 1) / (256L * j.upt));
     }
     const int wblocks = W ? (wIn + 63) / 64 * wH : 0;
     j.ws_first = j.start[njobs] + wblocks;
