@@ -235,6 +235,18 @@ def main():
                  "vocab_size": np.array(2000), "n_iter": np.array(1)}
         np.savez_compressed(os.path.join(HERE, "model_hsg_cfg1_n1.npz"), **graph_arrays(cdocs), **compact(res),
                             **extra, **meta)
+    if args.only == "model_hsg_cfg2":
+        # BASELINE config 2 at full size (32 CNN/DM-shaped documents, N=35, W=600, k=36:
+        # 159,040 graph edges -- the bench's batch shape) through the whole HSumGraph;
+        # generated on request only (--only model_hsg_cfg2: the reference CPU path takes
+        # minutes at this size)
+        cdocs = sort_by_sentences(synth.make_batch_docs("cfg2", seed=21, vocab_size=5000))
+        res = model_case(HiGraph, cdocs, 8, "HSumGraph", vocab_size=5000)
+        extra = {"sent_words": np.concatenate([d.words for d in cdocs]).astype(np.int32),
+                 "sent_label": np.concatenate([d.label for d in cdocs]).astype(np.int8),
+                 "vocab_size": np.array(5000)}
+        np.savez_compressed(os.path.join(HERE, "model_hsg_cfg2.npz"), **graph_arrays(cdocs), **compact(res),
+                            **extra, **meta)
     if args.only is not None:
         return
 

@@ -39,7 +39,10 @@ MODEL_CASES = [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5),
                # 4 config-1-shaped documents (N=30, W=400, k=20; 12,000 graph edges)
                ("model_hsg_cfg1", "HSumGraph", 6),
                # the same documents at train.py's default n_iter = 1 (train.py:282)
-               ("model_hsg_cfg1_n1", "HSumGraph", 7)]
+               ("model_hsg_cfg1_n1", "HSumGraph", 7),
+               # BASELINE config 2 at full size: 32 CNN/DM-shaped documents (N=35, W=600,
+               # k=36; 159,040 graph edges, the bench's batch shape)
+               ("model_hsg_cfg2", "HSumGraph", 8)]
 
 
 @pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
