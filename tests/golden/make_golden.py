@@ -247,6 +247,16 @@ def main():
                  "vocab_size": np.array(5000)}
         np.savez_compressed(os.path.join(HERE, "model_hsg_cfg2.npz"), **graph_arrays(cdocs), **compact(res),
                             **extra, **meta)
+    if args.only == "model_hdsg_cfg4":
+        # BASELINE config 4 at full size (32 multi-document HDSG examples with doc nodes,
+        # 3 x 15 sentences, W=700, k=20: 107,040 graph edges) through HSumDocGraph
+        cdocs = sort_by_sentences(synth.make_batch_docs("cfg4", seed=22, vocab_size=5000))
+        res = model_case(HiGraph, cdocs, 9, "HSumDocGraph", vocab_size=5000)
+        extra = {"sent_words": np.concatenate([d.words for d in cdocs]).astype(np.int32),
+                 "sent_label": np.concatenate([d.label for d in cdocs]).astype(np.int8),
+                 "vocab_size": np.array(5000)}
+        np.savez_compressed(os.path.join(HERE, "model_hdsg_cfg4.npz"), **graph_arrays(cdocs), **compact(res),
+                            **extra, **meta)
     if args.only is not None:
         return
 

@@ -42,7 +42,10 @@ MODEL_CASES = [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5),
                ("model_hsg_cfg1_n1", "HSumGraph", 7),
                # BASELINE config 2 at full size: 32 CNN/DM-shaped documents (N=35, W=600,
                # k=36; 159,040 graph edges, the bench's batch shape)
-               ("model_hsg_cfg2", "HSumGraph", 8)]
+               ("model_hsg_cfg2", "HSumGraph", 8),
+               # BASELINE config 4 at full size: 32 HDSG examples with doc nodes (3 x 15
+               # sentences, W=700, k=20; 107,040 graph edges)
+               ("model_hdsg_cfg4", "HSumDocGraph", 9)]
 
 
 @pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
