@@ -257,6 +257,16 @@ def main():
                  "vocab_size": np.array(5000)}
         np.savez_compressed(os.path.join(HERE, "model_hdsg_cfg4.npz"), **graph_arrays(cdocs), **compact(res),
                             **extra, **meta)
+    if args.only == "model_hsg_cfg5":
+        # BASELINE config 5 at full size (NYT50-shaped: 32 documents, 481,280 graph edges
+        # with the phantom sentence in-edges of doc_max_timesteps = 80) through HSumGraph
+        cdocs = sort_by_sentences(synth.make_batch_docs("cfg5", seed=23, vocab_size=5000))
+        res = model_case(HiGraph, cdocs, 10, "HSumGraph", vocab_size=5000, doc_max_timesteps=80)
+        extra = {"sent_words": np.concatenate([d.words for d in cdocs]).astype(np.int32),
+                 "sent_label": np.concatenate([d.label for d in cdocs]).astype(np.int8),
+                 "vocab_size": np.array(5000), "doc_max_timesteps": np.array(80)}
+        np.savez_compressed(os.path.join(HERE, "model_hsg_cfg5.npz"), **graph_arrays(cdocs), **compact(res),
+                            **extra, **meta)
     if args.only is not None:
         return
 

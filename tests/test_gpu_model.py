@@ -25,9 +25,9 @@ class HPS:
         self.__dict__.update(d)
 
 
-def build_model(cls_name, seed, vocab_size=500, n_iter=2):
+def build_model(cls_name, seed, vocab_size=500, n_iter=2, doc_max_timesteps=50):
     from hetersumgraph_amd import HiGraph
-    hps = HPS(vocab_size=int(vocab_size), n_iter=int(n_iter))
+    hps = HPS(vocab_size=int(vocab_size), n_iter=int(n_iter), doc_max_timesteps=int(doc_max_timesteps))
     torch.manual_seed(seed)
     embed = torch.nn.Embedding(hps.vocab_size, 300, padding_idx=0)
     model = getattr(HiGraph, cls_name)(hps, embed)
@@ -45,7 +45,10 @@ MODEL_CASES = [("model_hsg", "HSumGraph", 4), ("model_hdsg", "HSumDocGraph", 5),
                ("model_hsg_cfg2", "HSumGraph", 8),
                # BASELINE config 4 at full size: 32 HDSG examples with doc nodes (3 x 15
                # sentences, W=700, k=20; 107,040 graph edges)
-               ("model_hdsg_cfg4", "HSumDocGraph", 9)]
+               ("model_hdsg_cfg4", "HSumDocGraph", 9),
+               # BASELINE config 5 (north star) at full size: 32 NYT50-shaped documents
+               # (N=80, W=900, k=14, doc_max_timesteps=80; 481,280 graph edges)
+               ("model_hsg_cfg5", "HSumGraph", 10)]
 
 
 @pytest.mark.parametrize("name,cls,seed", MODEL_CASES)
@@ -54,7 +57,7 @@ def test_model_logits_match_reference(name, cls, seed):
     z = load_fixture(name)
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))                      # in-place, train.py:112
-    model = build_model(cls, seed, z.get("vocab_size", 500), z.get("n_iter", 2))
+    model = build_model(cls, seed, z.get("vocab_size", 500), z.get("n_iter", 2), z.get("doc_max_timesteps", 50))
     # MIOpen (like cuDNN) has no RNN backward in eval mode; train-mode LSTM with
     # its inter-layer dropout set to 0 is numerically the eval LSTM
     model.lstm.train()
@@ -141,7 +144,7 @@ def test_model_logits_bf16_gemm_error_budget(name, cls, seed):
     z = load_fixture(name)
     G = build_graph(z, z["sent_words"], z["sent_label"])
     G.to(torch.device("cuda"))
-    model = build_model(cls, seed, z.get("vocab_size", 500), z.get("n_iter", 2))
+    model = build_model(cls, seed, z.get("vocab_size", 500), z.get("n_iter", 2), z.get("doc_max_timesteps", 50))
     model.lstm.train()
     model.lstm.dropout = 0.0
     with gemm_dtype("bf16"):
