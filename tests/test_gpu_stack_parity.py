@@ -160,7 +160,10 @@ CASES = [("cfg2", "f32", 31, 2), ("cfg4", "f32", 32, 2), ("cfg5", "f32", 33, 2),
 
 def compare(config, dtype, r, o, n_docs, n_edges):
     from hetersumgraph_amd.module.GATStackLayer import reference_named_grads
-    out_tol, fro_tol, worst_tol = (2e-5, 2e-4, 1e-2) if dtype == "f32" else (2e-2, 5e-2, 1e-1)
+    # bf16 mode, measured at cfg5 (round 5, profiles/r05/stack_parity_bf16_errors.log):
+    # output 2.3e-3 / 3.1e-3 (eval / train), gradients fro <= 2.3e-2 and worst <= 5.7e-2,
+    # attention parameters <= 6.2e-2 -- the bounds below keep ~2-3x of that
+    out_tol, fro_tol, worst_tol = (2e-5, 2e-4, 1e-2) if dtype == "f32" else (1e-2, 5e-2, 1e-1)
     err = (_f64(r["s"]) - o["s"]).abs().max().item()
     print(f"{config} {dtype}: {n_docs} docs, {n_edges} edges, output max|diff| {err:.3e}")
     assert err <= out_tol
