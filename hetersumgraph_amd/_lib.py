@@ -20,7 +20,7 @@ HSG_TAU_PER_EDGE = 1
 
 # every symbol include/hsg.h declares (checked by tests/test_abi.py)
 EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_src",
-           "hsg_gat_bwd_src_blocks", "hsg_attn_src_logits", "hsg_attn_params_fwd", "hsg_attn_params_fwd_pair", "hsg_attn_params_finish_pair", "hsg_attn_params_bwd",
+           "hsg_gat_bwd_src_blocks", "hsg_attn_src_logits", "hsg_attn_params_fwd", "hsg_attn_params_fwd_pair", "hsg_attn_params_fwd_pair_seed", "hsg_attn_params_finish_pair", "hsg_attn_params_bwd",
            "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_f32_mfma", "hsg_gemm_bf16", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_ffn_colsums",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
@@ -70,6 +70,7 @@ _SIGS = {
     "hsg_gat_bwd_src_blocks": [_RELP],
     "hsg_attn_params_fwd": [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_attn_params_fwd_pair": [_I, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P],
+    "hsg_attn_params_fwd_pair_seed": [_I, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P],
     "hsg_attn_params_finish_pair": [_I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I,
                                     _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P],
     "hsg_attn_params_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],

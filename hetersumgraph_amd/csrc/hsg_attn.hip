@@ -99,13 +99,21 @@ __global__ __launch_bounds__(256) void k_attn_params_fwd(int H, int D, int F, co
 
 // the tables of two layers (the stack's W2S and S2W, sharing T) in one launch:
 // blocks [0, H0) are layer 0's heads, [H0, H0 + H1) layer 1's
+// optional seed / snap: the step's dropout-seed advance (what k_seed_advance does:
+// seed += 1, snap = the new value) rides in this launch, the first of the step's forward
 struct AttnFwdPair {
     int H[2], D[2];
     const float *attn[2], *wf[2], *bf[2];
     float *a1[2], *tau[2];
+    int64_t *seed, *snap;
 };
 
 __global__ __launch_bounds__(256) void k_attn_params_fwd_pair(AttnFwdPair j, int F, const float *__restrict__ T) {
+    if (j.seed != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t s = j.seed[0] + 1;
+        j.seed[0] = s;
+        j.snap[0] = s;
+    }
     const int q = (int)blockIdx.x >= j.H[0] ? 1 : 0;
     const int k = (int)blockIdx.x - (q ? j.H[0] : 0);
     attn_fwd_head(k, j.H[q], j.D[q], F, j.attn[q], j.wf[q], j.bf[q], T, j.a1[q], j.tau[q]);
@@ -373,7 +381,18 @@ int hsg_attn_params_fwd_pair(int H0, int D0, const float *attn0, const float *wf
     if (!dims_ok(H0, D0, F) || !dims_ok(H1, D1, F) || !attn0 || !wf0 || !a1_0 || !tau0 || !attn1 || !wf1 || !a1_1 ||
         !tau1 || !T)
         return HSG_EINVAL;
-    AttnFwdPair j{{H0, H1}, {D0, D1}, {attn0, attn1}, {wf0, wf1}, {bf0, bf1}, {a1_0, a1_1}, {tau0, tau1}};
+    return hsg_attn_params_fwd_pair_seed(H0, D0, attn0, wf0, bf0, a1_0, tau0, H1, D1, attn1, wf1, bf1, a1_1, tau1, F,
+                                         T, nullptr, nullptr, stream);
+}
+
+int hsg_attn_params_fwd_pair_seed(int H0, int D0, const float *attn0, const float *wf0, const float *bf0,
+                                  float *a1_0, float *tau0, int H1, int D1, const float *attn1, const float *wf1,
+                                  const float *bf1, float *a1_1, float *tau1, int F, const float *T, int64_t *seed,
+                                  int64_t *snap, void *stream) {
+    if (!dims_ok(H0, D0, F) || !dims_ok(H1, D1, F) || !attn0 || !wf0 || !a1_0 || !tau0 || !attn1 || !wf1 || !a1_1 ||
+        !tau1 || !T || (seed == nullptr) != (snap == nullptr))
+        return HSG_EINVAL;
+    AttnFwdPair j{{H0, H1}, {D0, D1}, {attn0, attn1}, {wf0, wf1}, {bf0, bf1}, {a1_0, a1_1}, {tau0, tau1}, seed, snap};
     hipLaunchKernelGGL(k_attn_params_fwd_pair, dim3(H0 + H1), dim3(256), 0, (hipStream_t)stream, j, F, T);
     return status();
 }

@@ -123,18 +123,22 @@ def attn_tables(attn, T, wf, bf, H, D):
     return a1, tau
 
 
-def attn_tables_pair(lay0, lay1, T):
+def attn_tables_pair(lay0, lay1, T, seed_advance=None):
     """:func:`attn_tables` of two layers sharing T in ONE launch
     (hsg_attn_params_fwd_pair): [(a1, tau) of lay0, (a1, tau) of lay1]; a layer is any
-    object with attn / wf / bf / H / D."""
+    object with attn / wf / bf / H / D.  ``seed_advance``: a pending dropout-seed
+    advance claimed from rng (its (seed, snap) tensors), performed by the same launch
+    (hsg_attn_params_fwd_pair_seed)."""
     lib = load()
     outs = []
     for lay in (lay0, lay1):
         outs.append((lay.attn.new_empty(lay.H, lay.D), lay.attn.new_empty(N_BOX + 1, lay.H)))
     (a0, t0), (a1, t1) = outs
-    check(lib.hsg_attn_params_fwd_pair(lay0.H, lay0.D, ptr(lay0.attn), ptr(lay0.wf), ptr(lay0.bf), ptr(a0), ptr(t0),
-                                       lay1.H, lay1.D, ptr(lay1.attn), ptr(lay1.wf), ptr(lay1.bf), ptr(a1), ptr(t1),
-                                       T.shape[1], ptr(T), stream_of(T)), "hsg_attn_params_fwd_pair")
+    seed, snap = seed_advance if seed_advance is not None else (None, None)
+    check(lib.hsg_attn_params_fwd_pair_seed(lay0.H, lay0.D, ptr(lay0.attn), ptr(lay0.wf), ptr(lay0.bf), ptr(a0),
+                                            ptr(t0), lay1.H, lay1.D, ptr(lay1.attn), ptr(lay1.wf), ptr(lay1.bf),
+                                            ptr(a1), ptr(t1), T.shape[1], ptr(T), ptr(seed), ptr(snap),
+                                            stream_of(T)), "hsg_attn_params_fwd_pair_seed")
     return outs
 
 

@@ -23,27 +23,45 @@ class DropoutRNG:
         self.seed = torch.tensor([seed], dtype=torch.int64, device=device)
         self.offset = 0
         self._snap = None
+        self._pending = False
 
     def take(self):
         """(seed snapshot tensor, offset) for one dropout call."""
+        self._flush()
         if self._snap is None:
             self._snap = self.seed.clone()        # device copy: graph-capturable
         self.offset = (self.offset + 1) & 0xFFFFFFFF
         return self._snap, self.offset
 
     def advance(self):
-        """New masks for the next step (device-side: graph-capturable).  On a GPU one
-        launch (hsg_seed_advance) increments the seed and writes the new value into a
-        fresh snapshot, which the following take() calls hand out."""
+        """New masks for the next step (device-side: graph-capturable).  On a GPU the
+        seed is incremented and the new value written into a fresh snapshot, which the
+        following take() calls hand out -- by the first launch that needs it: either
+        take() (one hsg_seed_advance launch) or a kernel of the step that performs the
+        advance itself after :meth:`claim` (the fused stack's first launch)."""
         if self.seed.is_cuda:
-            from ._lib import check, load
-            snap = torch.empty_like(self.seed)
-            st = torch.cuda.current_stream(self.seed.device).cuda_stream
-            check(load().hsg_seed_advance(self.seed.data_ptr(), snap.data_ptr(), st), "hsg_seed_advance")
-            self._snap = snap
+            self._flush()                           # an unclaimed earlier advance still counts
+            self._snap = torch.empty_like(self.seed)
+            self._pending = True
         else:
             self.seed.add_(1)
             self._snap = None
+
+    def _flush(self):
+        if self._pending:
+            from ._lib import check, load
+            st = torch.cuda.current_stream(self.seed.device).cuda_stream
+            check(load().hsg_seed_advance(self.seed.data_ptr(), self._snap.data_ptr(), st), "hsg_seed_advance")
+            self._pending = False
+
+    def claim(self):
+        """(seed, snap) of a pending advance, handed to a kernel that performs it in its
+        own launch -- which must come before anything reads the seed (stream order) --
+        or None when no advance is pending."""
+        if not self._pending:
+            return None
+        self._pending = False
+        return self.seed, self._snap
 
 
 def get(device) -> DropoutRNG:
@@ -60,6 +78,7 @@ def manual_seed(seed, device=None):
     r = get(device)
     r.seed.fill_(int(seed))
     r._snap = None
+    r._pending = False
     r.offset = 0
 
 

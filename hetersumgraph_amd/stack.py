@@ -262,6 +262,13 @@ class _GatStack(torch.autograd.Function):
         # same masks; the head-projection keep-masks are then made in ONE launch
         seq = [(w2s, rw)] + [(s2w, rs), (w2s, rw)] * n_iter
         gen = hsg_rng.get(w0.device)
+        # the attention tables depend on the parameters only: once per layer, in the
+        # forward's first launch, which also performs the step's pending dropout-seed
+        # advance (before any draw below reads the seed)
+        if _lib.path_option("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
+            tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T, seed_advance=gen.claim())))
+        else:
+            tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
         draws = []
         for lay, _ in seq:
             hm = gen.take() if lay.p_attn > 0 else None
@@ -323,12 +330,7 @@ class _GatStack(torch.autograd.Function):
             states[outk] = out
             apps.append((lay, saved, nb, org, a))
 
-        # the attention tables depend on the parameters only: once per layer
-        if _lib.path_option("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
-            tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T)))
-        else:
-            tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
-        # likewise the transposed head weights of a narrow-head (VALU) projection
+        # the transposed head weights of a narrow-head (VALU) projection
         wts = {id(lay): ((wt_fold if lay is fold else transposed_weight(lay.W, lay.H, lay.D))
                          if any(lay is q for q in narrow) else None)
                for lay in (w2s, s2w)}

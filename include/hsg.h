@@ -179,6 +179,15 @@ int hsg_attn_params_fwd(int H, int D, int F, const float *attn, const float *wf,
 int hsg_attn_params_fwd_pair(int H0, int D0, const float *attn0, const float *wf0, const float *bf0, float *a1_0,
                              float *tau0, int H1, int D1, const float *attn1, const float *wf1, const float *bf1,
                              float *a1_1, float *tau1, int F, const float *T, void *stream);
+/* hsg_attn_params_fwd_pair that also performs the step's dropout-seed advance in the
+ * same launch (seed[0] += 1; snap[0] = the new value: hsg_seed_advance), so the fused
+ * stack's forward starts with one launch instead of two.  seed and snap both given or
+ * both NULL (then exactly hsg_attn_params_fwd_pair).  Nothing else may read seed or
+ * snap before this launch completes (stream order). */
+int hsg_attn_params_fwd_pair_seed(int H0, int D0, const float *attn0, const float *wf0, const float *bf0,
+                                  float *a1_0, float *tau0, int H1, int D1, const float *attn1, const float *wf1,
+                                  const float *bf1, float *a1_1, float *tau1, int F, const float *T, int64_t *seed,
+                                  int64_t *snap, void *stream);
 int hsg_attn_params_bwd(int H, int D, int F, int n_dtau_part, const float *dtau_part, int n_da1_part,
                         const float *da1_part, const float *attn, const float *wf, const float *bf,
                         const float *T, float *dattn, float *dwf, float *dbf, float *dT, float *workspace,
