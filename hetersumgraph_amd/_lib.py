@@ -24,7 +24,7 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_attn_params_bwd_workspace_floats", "hsg_version", "hsg_gemm_f32", "hsg_gemm_f32_mfma", "hsg_gemm_bf16", "hsg_gemm_workspace_floats", "hsg_gemm_auto_splits", "hsg_gemm_row_tiles", "hsg_ffn_colsums",
            "hsg_ln_bwd_blocks", "hsg_ln_fwd", "hsg_ln_bwd",
            "hsg_dropmask_words", "hsg_dropmask_scale", "hsg_dropmask", "hsg_hproj_fwd", "hsg_hproj_dx",
-           "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
+           "hsg_hproj_dw_chunks", "hsg_hproj_dw", "hsg_hproj_bwd", "hsg_rel_build_workspace_bytes", "hsg_rel_build",
            "hsg_cnn_taps", "hsg_cnn_gather", "hsg_cnn_pool", "hsg_cnn_pool_bwd",
            "hsg_ffn_small_supported", "hsg_ffn_small_fwd", "hsg_ffn_small_bwd_blocks", "hsg_ffn_small_bwd",
            "hsg_attn_params_stage", "hsg_attn_params_finish", "hsg_hproj_fwd_logits_supported",
@@ -105,6 +105,7 @@ _SIGS = {
     "hsg_hproj_fwd_mf": [_I, _I, _I, _P, _I, _P, _I, _I, _P, _F, _P, _I, _P, _P, _P],
     "hsg_hproj_dx": [_I, _I, _I, _I, _P, _I, _P, _P, _F, _P, _I, _I, _P],
     "hsg_hproj_dw_chunks": [_I, _I, _I, _I],
+    "hsg_hproj_bwd": [_I, _I, _I, _I, _P, _I, _P, _P, _I, _P, _F, _P, _I, _I, _P, _P],
     "hsg_hproj_dw": [_I, _I, _I, _I, _P, _I, _P, _I, _P, _F, _P, _P, _I, _P],
     "hsg_rel_build_workspace_bytes": [_I, _I],
     "hsg_rel_build": [_F, _F, _I, _I] + [_P] * 17 + [ctypes.c_size_t, _P],

@@ -874,41 +874,45 @@ __global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const
 // DS W values and keep word up front, runs the DS-step MFMA chain, and leaves the
 // masked product in LDS; the block then adds the heads in head order (the order of
 // k_hproj_dx: bitwise equal results).  DSM = largest DS the instance holds.
+// (the body as a device function of the block index: also the dX half of
+// k_hproj_bwd_hw, whose 256-thread blocks run heads k, k + 4, ... per wave)
 template <int DSM>
-__global__ __launch_bounds__(1024) void k_hproj_dx_hw(int n, int in, int H, int D, const float *__restrict__ dZ,
-                                                      int ldz, const float *__restrict__ W,
-                                                      const uint32_t *__restrict__ bits, float scale,
-                                                      float *__restrict__ dX, int ldx, int accumulate) {
+__device__ __forceinline__ void hproj_dx_hw_tile(int bid, int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                 int ldz, const float *__restrict__ W,
+                                                 const uint32_t *__restrict__ bits, float scale,
+                                                 float *__restrict__ dX, int ldx, int accumulate) {
     __shared__ float sP[16][4][64];                   // [head][r][lane]
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int nct = (in + 15) / 16;
-    const int rt = blockIdx.x / nct, ctile = blockIdx.x - rt * nct;
+    const int rt = bid / nct, ctile = bid - rt * nct;
     const int i0 = rt * 16;
     const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
-    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nw = (int)(blockDim.x >> 6);
     const int DS = (D + 3) / 4;
     const auto rZ = rsrc(dZ, (long)n * ldz * 4);
     const auto rW = rsrc(W, (long)H * D * in * 4);
     const auto rM = rsrc(bits, (long)H * NWI * LDC * 4);
     const int zi = i0 + li, c = ctile * 16 + li;
     const uint32_t zbase = zi < n ? (uint32_t)zi * ldz * 4 : kOOB;
-    float av[DSM], bv[DSM];
-#pragma unroll
-    for (int s = 0; s < DSM; ++s) {
-        const int d = 4 * s + lk;
-        const bool ok = s < DS && d < D;
-        const int hd = k * D + d;
-        av[s] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
-        bv[s] = bld(rW, (ok && c < in) ? (uint32_t)(hd * in + c) * 4 : kOOB);
-    }
-    const uint32_t mw = bldu(rM, c < in ? (uint32_t)(((k * NWI + i0 / 32) * LDC) + c) * 4 : kOOB);
-    f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < DSM; ++s)
-        if (s < DS) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
     const int sh = (i0 & 31) + 4 * lk;
+    for (int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); k < H; k += nw) {
+        float av[DSM], bv[DSM];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) sP[k][r][lane] = ((mw >> (sh + r)) & 1u) ? acc[r] : 0.f;
+        for (int s = 0; s < DSM; ++s) {
+            const int d = 4 * s + lk;
+            const bool ok = s < DS && d < D;
+            const int hd = k * D + d;
+            av[s] = bld(rZ, (ok && zbase != kOOB) ? zbase + hd * 4 : kOOB);
+            bv[s] = bld(rW, (ok && c < in) ? (uint32_t)(hd * in + c) * 4 : kOOB);
+        }
+        const uint32_t mw = bldu(rM, c < in ? (uint32_t)(((k * NWI + i0 / 32) * LDC) + c) * 4 : kOOB);
+        f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DSM; ++s)
+            if (s < DS) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sP[k][r][lane] = ((mw >> (sh + r)) & 1u) ? acc[r] : 0.f;
+    }
     __syncthreads();
     for (int o = threadIdx.x; o < 256; o += blockDim.x) {         // 16 x 16 outputs
         const int r = o >> 6, ln = o & 63;
@@ -920,6 +924,14 @@ __global__ __launch_bounds__(1024) void k_hproj_dx_hw(int n, int in, int H, int 
             dX[ofs] = accumulate ? dX[ofs] + tot * scale : tot * scale;
         }
     }
+}
+
+template <int DSM>
+__global__ __launch_bounds__(1024) void k_hproj_dx_hw(int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                      int ldz, const float *__restrict__ W,
+                                                      const uint32_t *__restrict__ bits, float scale,
+                                                      float *__restrict__ dX, int ldx, int accumulate) {
+    hproj_dx_hw_tile<DSM>((int)blockIdx.x, n, in, H, D, dZ, ldz, W, bits, scale, dX, ldx, accumulate);
 }
 
 // ------------------------------------------------------------------ dW ----
@@ -968,10 +980,10 @@ DwGeom dw_geom(int n, int in, int H, int D) {
 // per 32-row step instead of 17 dword loads; the padding columns of the dZ stage are
 // zeroed once.  Same LDS image, same products (bitwise equal).
 template <int SL, bool VEC = false>
-__global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, int rows_per_chunk,
-                                                  const float *__restrict__ dZ, int ldz,
-                                                  const float *__restrict__ X, int ldx,
-                                                  const uint32_t *__restrict__ bits, float *__restrict__ part) {
+__device__ __forceinline__ void hproj_dw_block(int bx, int by, int bz, int n, int in, int H, int D,
+                                               int rows_per_chunk, const float *__restrict__ dZ, int ldz,
+                                               const float *__restrict__ X, int ldx,
+                                               const uint32_t *__restrict__ bits, float *__restrict__ part) {
     __shared__ __attribute__((aligned(16))) float Xs[32][kDwXs];
     constexpr int ZC = SL * 16, NZ = 32 * ZC / 256, NM = SL * 64 / 256;   // slot columns, per-thread loads
     // dZ stage: slot q at column ZS q.  VEC: slots 24 apart, so the eight 16-byte
@@ -985,9 +997,9 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
     const int SPH = (D + 15) / 16, NS = H * SPH;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, lk = lane >> 4;
-    const int c0 = blockIdx.x * 64;
-    const int s0 = blockIdx.y * SL;
-    const int rb = blockIdx.z * rows_per_chunk;
+    const int c0 = bx * 64;
+    const int s0 = by * SL;
+    const int rb = bz * rows_per_chunk;
     const int rend = min(rb + rows_per_chunk, n);
     // per-thread staging: X 2 x 4 columns, dZ 16 values, 2 mask words.  The
     // column parts of every offset are fixed per thread; buffer loads with kOOB
@@ -1110,7 +1122,7 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
         }
     }
     // D: col = lane & 15 -> slot output j, row = (lane >> 4) * 4 + r -> input column
-    const long base = (long)blockIdx.z * H * D * in;
+    const long base = (long)bz * H * D * in;
 #pragma unroll
     for (int q = 0; q < SL; ++q) {
         const int v = s0 + q;
@@ -1123,6 +1135,37 @@ __global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, i
             if (gc < in) part[base + (long)(k * D + j) * in + gc] = acc[q][r];
         }
     }
+}
+
+template <int SL, bool VEC = false>
+__global__ __launch_bounds__(256) void k_hproj_dw(int n, int in, int H, int D, int rows_per_chunk,
+                                                  const float *__restrict__ dZ, int ldz,
+                                                  const float *__restrict__ X, int ldx,
+                                                  const uint32_t *__restrict__ bits, float *__restrict__ part) {
+    hproj_dw_block<SL, VEC>((int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, n, in, H, D, rows_per_chunk, dZ, ldz,
+                            X, ldx, bits, part);
+}
+
+// The wide-head (S2W) backward of one projection in ONE launch: blocks [0, dx_blocks)
+// are k_hproj_dx_hw tiles (4 waves per block, heads k, k + 4, ... per wave: the same
+// products and the same head-order sums, so dX is bitwise the two-launch one), the rest
+// k_hproj_dw<4> blocks (the same row chunks and partial slabs).  The two halves only
+// share dZ; each was a latency-bound launch of a few hundred blocks (7.3 + 6.6 us).
+template <int DSM>
+__global__ __launch_bounds__(256) void k_hproj_bwd_hw(int n, int in, int H, int D, const float *__restrict__ dZ,
+                                                      int ldz, const float *__restrict__ W,
+                                                      const uint32_t *__restrict__ bits, float scale,
+                                                      float *__restrict__ dX, int ldxo, int accumulate,
+                                                      const float *__restrict__ X, int ldx, int rows_per_chunk,
+                                                      float *__restrict__ part, int dx_blocks, int cx, int cy) {
+    const int b = (int)blockIdx.x;
+    if (b < dx_blocks) {
+        hproj_dx_hw_tile<DSM>(b, n, in, H, D, dZ, ldz, W, bits, scale, dX, ldxo, accumulate);
+        return;
+    }
+    const int e = b - dx_blocks;
+    hproj_dw_block<4, false>(e % cx, (e / cx) % cy, e / (cx * cy), n, in, H, D, rows_per_chunk, dZ, ldz, X, ldx, bits,
+                             part);
 }
 
 // ---------------------------------------------- dW on bf16 limb MFMAs (round 5) ----
@@ -1713,6 +1756,40 @@ int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         hipLaunchKernelGGL((k_hproj_dx<1, 4>), dim3((unsigned)((narrow + 3) / 4)), dim3(256), 0, st, n, in, H, D,
                            dZ, ldz, W, bits, s, dX, ldx, accumulate);
     }
+    return status();
+}
+
+int hsg_hproj_bwd(int n, int in, int H, int D, const float *dZ, int ldz, const float *W, const float *X, int ldx,
+                  const uint32_t *bits, float p, float *dX, int ldxo, int accumulate, float *part, void *stream) {
+    if (n < 0 || in < 1 || H < 1 || D < 1 || !dZ || !W || !X || !bits || !dX || !part || ldx < in || ldxo < in ||
+        ldz < H * D || !fits_buffers(n, in, H, D, ldx > ldz ? ldx : ldz) || !fits_buffers(n, in, H, D, ldxo))
+        return HSG_EINVAL;
+    if (n == 0) return 0;
+    // the merged launch where the two-launch path would run k_hproj_dx_hw and the
+    // dword-staged k_hproj_dw<4> (the S2W shape); dev A/B: HSG_HPROJ_BWD_MERGE=0
+    const long rtiles = (n + 15) / 16, wide = rtiles * ((in + 63) / 64);
+    const char *me = HSG_DEV_ENV("HSG_HPROJ_BWD_MERGE");
+    const char *pe = HSG_DEV_ENV("HSG_HPROJ_DXPRE");
+    const bool vec = dw_slots() == 4 && D == 8 && in % 4 == 0 && ldx % 4 == 0 && ldz % 4 == 0 && aligned16(X) &&
+                     aligned16(dZ);
+    const bool merge = (!me || atoi(me) != 0) && (!pe || atoi(pe) == 1) && wide < 2048 && H <= 16 && D <= 64 &&
+                       !dw_mf_shape(in, H, D) && !dw_m4_shape(in, H, D) && dw_slots() == 4 && !vec;
+    if (!merge) {
+        int rc = hsg_hproj_dx(n, in, H, D, dZ, ldz, W, bits, p, dX, ldxo, accumulate, stream);
+        if (rc) return rc;
+        return hsg_hproj_dw(n, in, H, D, dZ, ldz, X, ldx, bits, p, part, nullptr, 0, stream);
+    }
+    const DwGeom g = dw_geom(n, in, H, D);
+    const int dx_blocks = (int)(rtiles * ((in + 15) / 16));
+    const unsigned total = (unsigned)(dx_blocks + g.ctiles * g.sgroups * g.chunks);
+    if (D <= 32)
+        hipLaunchKernelGGL(k_hproj_bwd_hw<8>, dim3(total), dim3(256), 0, (hipStream_t)stream, n, in, H, D, dZ, ldz, W,
+                           bits, drop_scale(p), dX, ldxo, accumulate, X, ldx, g.rows, part, dx_blocks, g.ctiles,
+                           g.sgroups);
+    else
+        hipLaunchKernelGGL(k_hproj_bwd_hw<16>, dim3(total), dim3(256), 0, (hipStream_t)stream, n, in, H, D, dZ, ldz, W,
+                           bits, drop_scale(p), dX, ldxo, accumulate, X, ldx, g.rows, part, dx_blocks, g.ctiles,
+                           g.sgroups);
     return status();
 }
 

@@ -127,6 +127,15 @@ def hproj_bwd(saved, dZ, dX=None, dX_acc=False, dW=None, dW_acc=False, batch=Non
     dZ = dZ.contiguous()
     n, d_in = X.shape
     st = stream_of(X)
+    if dX is not None and dW is not None and batch is not None and n > 0:
+        # both in one call (hsg_hproj_bwd: one launch for the small wide-head shape)
+        chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+        part = X.new_empty(chunks * H * D * d_in)
+        check(lib.hsg_hproj_bwd(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(X), d_in, ptr(bits), p, ptr(dX), d_in,
+                                int(dX_acc), ptr(part), st), "hsg_hproj_bwd")
+        batch.add((key, "W"), dW.view(-1), H * D * d_in, H * D * d_in, 0, lib.hsg_dropmask_scale(p), dW_acc,
+                  part, chunks)
+        return dX
     if dX is not None:
         check(lib.hsg_hproj_dx(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(bits), p, ptr(dX), d_in, int(dX_acc), st),
               "hsg_hproj_dx")

@@ -529,6 +529,12 @@ int hsg_hproj_fwd_mf(int n, int in, int H, const float *X, int ldx, const void *
                      const uint32_t *bits, float p, float *Z, int ldz, const float *a1, float *sigma, void *stream);
 int hsg_hproj_dx(int n, int in, int H, int D, const float *dZ, int ldz, const float *W,
                  const uint32_t *bits, float p, float *dX, int ldx, int accumulate, void *stream);
+/* dX and the dW partial slabs of one projection (hsg_hproj_dx + hsg_hproj_dw with
+ * dW = NULL: part holds hsg_hproj_dw_chunks(n, in, H, D) slabs [H*D][in], unscaled)
+ * in ONE launch where both would be small wide-head launches (the S2W shape: heads
+ * of D <= 64, few rows), else the two launches.  X row pitch ldx, dX row pitch ldxo. */
+int hsg_hproj_bwd(int n, int in, int H, int D, const float *dZ, int ldz, const float *W, const float *X, int ldx,
+                  const uint32_t *bits, float p, float *dX, int ldxo, int accumulate, float *part, void *stream);
 int hsg_hproj_dw_chunks(int n, int in, int H, int D);
 /* dW == NULL: only the partial slabs part[chunk][H*D][in] (unscaled), to be summed
  * with scale hsg_dropmask_scale(p) by hsg_slab_reduce. */

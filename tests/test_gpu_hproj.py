@@ -109,6 +109,37 @@ def test_batched_dropmask_equals_single_launches():
         assert torch.equal(g, ref), (n, d_in, H, p, off)
 
 
+@pytest.mark.parametrize("n,d_in,H,D", [(1120, 64, 6, 50), (333, 72, 3, 16), (65, 33, 1, 64), (130, 50, 2, 75),
+                                         (200, 40, 3, 5), (19200 // 4, 300, 8, 8)])
+def test_hproj_bwd_one_launch_equals_two(monkeypatch, n, d_in, H, D):
+    """hsg_hproj_bwd (round 5: dX and the dW slabs of the S2W shape in ONE launch,
+    k_hproj_bwd_hw) against hsg_hproj_dx + hsg_hproj_dw (HSG_HPROJ_BWD_MERGE=0, dev
+    library): bitwise equal dX and partial slabs (shapes it does not merge take the
+    two launches either way)."""
+    from helpers import skip_unless_dev
+    skip_unless_dev(False)
+    from hetersumgraph_amd._lib import load, ptr
+    from hetersumgraph_amd.hproj import dropmask_bits
+    lib = load()
+    torch.manual_seed(n + D)
+    X = torch.randn(n, d_in, device="cuda")
+    W = torch.randn(H * D, d_in, device="cuda") / d_in ** 0.5
+    dZ = torch.randn(n, H * D, device="cuda")
+    bits = dropmask_bits(X, H, 0.1)
+    chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HSG_HPROJ_BWD_MERGE", flag)
+        dX = torch.full_like(X, 0.5)                              # accumulate onto it
+        part = X.new_empty(chunks * H * D * d_in)
+        assert lib.hsg_hproj_bwd(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(X), d_in, ptr(bits), 0.1, ptr(dX), d_in,
+                                 1, ptr(part), None) == 0
+        outs.append((dX, part))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 @pytest.mark.parametrize("n,d_in,H,D", [(19200, 300, 8, 8), (1000, 64, 16, 4), (257, 128, 3, 16), (70, 300, 8, 8)])
 def test_dw_4x4x1_equals_16x16x4_kernel(monkeypatch, n, d_in, H, D):
     """The unpadded 4x4x1 dW kernel (k_hproj_dw_m4, round 5) against the 16x16x4 slot
