@@ -1871,6 +1871,18 @@ int device_cus() {
     return c;
 }
 
+// 112- against 64-wide k_gemm7 tiles for N <= 320 (two blocks per CU resident, 128-row
+// tiles): a tile's time grows with its width, so the cost is rounds x width -- cfg2
+// (150 row tiles): 450 tiles in ONE round x 112 against 750 in two x 64, so 112 (40.0
+// vs 45.6 us); cfg4 / cfg5 (175 / 225 row tiles): 525 / 675 tiles take two rounds x 112
+// against two / three x 64 (84.5 / 91.8 us on 112-wide tiles against ~57 / ~70)
+bool wide112_pays(int M, int N) {
+    const int cus = device_cus() > 0 ? device_cus() : 256;
+    const long slots = 2L * cus, mt = (M + 127) / 128;
+    const long r112 = (mt * ((N + 111) / 112) + slots - 1) / slots, r64 = (mt * ((N + 63) / 64) + slots - 1) / slots;
+    return r112 * 112 < r64 * 64;
+}
+
 template <int BM, int BN, int WGM, int WGN, int PM, int S = 2, int OCC = 1>
 int launch11(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     p.splits = 1;
@@ -2618,8 +2630,8 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
     // to back (tools/gemm5_sweep.py, plan 42 against 27; same products, bitwise)
     // (where the planes' padded rows cover the 112-wide tiles; else 64)
     if (epi_rows_ok(p))
-        return N <= 320 && (N + 111) / 112 * 112 <= Np ? launch7<112, 2>(p, pl, Np, Kp, st)
-                                                       : launch7<64, 2>(p, pl, Np, Kp, st);
+        return N <= 320 && (N + 111) / 112 * 112 <= Np && wide112_pays(M, N) ? launch7<112, 2>(p, pl, Np, Kp, st)
+                                                                             : launch7<64, 2>(p, pl, Np, Kp, st);
     return launch5<64, 2, 0>(p, pl, Np, Kp, st);             // unaligned / ragged quads
 }
 
@@ -2757,10 +2769,9 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
 // GEMM, where the weight planes cover them and every 112-column rho group meets at most
 // three heads (the edge backward reads three slots per group); else 64
 static int elug_gw(int M, int N, int K, int head_dim) {
-    (void)M;
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
-    if (N > 320 || (N + 111) / 112 * 112 > Np) return 64;
+    if (N > 320 || (N + 111) / 112 * 112 > Np || !wide112_pays(M, N)) return 64;
 #ifdef HSG_DEV
     if (const char *e = HSG_DEV_ENV("HSG_ELUG_GW")) if (atoi(e) == 64) return 64;     // dev A/B
 #endif

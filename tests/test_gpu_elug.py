@@ -187,7 +187,9 @@ def test_psw_elug_rho_partials(M, mode):
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     G, rho = outs[1][1], outs[1][2]
     gw = 112 if rho.shape[1] == (N + 111) // 112 and rho.shape[1] != (N + 63) // 64 else 64
-    assert gw == (112 if mode == "f32" else 64)
+    # 112-wide tiles (and rho groups) where they take fewer rounds x width than 64-wide
+    # ones (hsg_gemm.hip wide112_pays): the cfg2 rows, not a 777-row GEMM
+    assert gw == (112 if mode == "f32" and M == 19200 else 64)
     ref = _rho_ref(G, h, D, gw)
     out = outs[1][0]
     delta = 4 * 2.0 ** -23 * (x.abs() + origin.abs()) + 2.0 ** -23
