@@ -244,15 +244,30 @@ def step_work(rel_w, rel_s, n_iter, gemm_dtype, word_grad=False, issued=False):
     return items
 
 
+DW_TILES = ((160, 128), (128, 160), (128, 128))
+
+
+def dw_tiles(M, N):
+    """Output tiles of one hsg_gemm_dw_slabs job (csrc/hsg_dw.hip pick_cfg: the tile
+    with the least padded area, ties to the first), mirrored on the host so the byte
+    count needs no HIP library (tests/test_abi.py pins it to hsg_gemm_dw_tiles)."""
+    best = None
+    for bm, bn in DW_TILES:
+        t = (-(-M // bm), -(-N // bn))
+        area = t[0] * bm * t[1] * bn
+        if best is None or area < best[0]:
+            best = (area, t[0] * t[1])
+    return best[1]
+
+
 def dw_slab_splits(K, d, dh):
     """K slices of a layer's FFN weight-gradient pair over K rows, mirrored on the host
     for the byte count: the product backward runs both gradients in one
     hsg_gemm_dw_slabs launch with dense.gemm_dw_slabs' rule -- two blocks per CU over
     the pair's tiles, at least 4 K tiles per slice, every slice non-empty -- and
     falls back to dense.gemm_slabs' 64 slices only when that declines (1: not split)."""
-    from hetersumgraph_amd._lib import load
     kt = (K + 31) // 32
-    tiles = load().hsg_gemm_dw_tiles(d, dh) + load().hsg_gemm_dw_tiles(dh, d)
+    tiles = dw_tiles(d, dh) + dw_tiles(dh, d)
     splits = max(1, min(max(1, (2 * 256) // max(tiles, 1)), kt // 4))
     per = (kt + splits - 1) // splits
     splits = (kt + per - 1) // per

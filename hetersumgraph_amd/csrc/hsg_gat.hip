@@ -2461,7 +2461,9 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
         return launch_status();
     }
     // the group width of the rho partials (hsg_gemm_psw_elug_rho_gw): 64, or 112 (the dx
-    // GEMM's 112-wide tiles); the two layouts coincide where their group counts do
+    // GEMM's 112-wide tiles), told apart by the count: the GEMM picks 112 only where the
+    // counts differ (elug_gw), and where they are equal (H*D <= 64: one group, the same
+    // layout; 113..128: 64 by that rule) 64 is the layout written
     const int rgw = rho_groups == (H * D + 63) / 64 ? 64 : rho_groups == (H * D + 111) / 112 ? 112 : 0;
     if (!srcg_wide(rel, H, D) || rgw == 0 || D > rgw) return HSG_EINVAL;
     const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;

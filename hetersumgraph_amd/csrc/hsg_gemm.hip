@@ -2767,11 +2767,14 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
 
 // the dx GEMM with the ELU gate (fp32 mode): 112-wide tiles for N <= 320, as the plain
 // GEMM, where the weight planes cover them and every 112-column rho group meets at most
-// three heads (the edge backward reads three slots per group); else 64
+// three heads (the edge backward reads three slots per group); else 64.  112 only where
+// its group count differs from 64's: hsg_gat_bwd_src_g_io tells the two layouts apart by
+// the count alone, and for N in 113..128 both would give 2 groups
 static int elug_gw(int M, int N, int K, int head_dim) {
     int Np, Kp;
     hsg_wsplit_dims(N, K, &Np, &Kp);
     if (N > 320 || (N + 111) / 112 * 112 > Np || !wide112_pays(M, N)) return 64;
+    if ((N + 111) / 112 == (N + 63) / 64) return 64;
 #ifdef HSG_DEV
     if (const char *e = HSG_DEV_ENV("HSG_ELUG_GW")) if (atoi(e) == 64) return 64;     // dev A/B
 #endif

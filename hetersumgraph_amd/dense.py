@@ -211,6 +211,8 @@ def gemm_psw_ln(A, Bs, bias, x, gamma, beta, eps, p_drop, seed_t, offset, y, out
     N = Bs.N
     if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in (x, y, out)):
         return False
+    if any(t.dtype != torch.float32 for t in (A, x, y, out)):      # the kernel reads / writes fp32 rows only
+        return False
     rc = lib.hsg_gemm_psw_ln(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(bias), ptr(y), ptr(x), ptr(gamma),
                              ptr(beta), float(eps), float(p_drop), ptr(seed_t), offset, ptr(out), ptr(mean),
                              ptr(rstd), int(Bs.mode == "bf16"), stream_of(A))
@@ -294,6 +296,17 @@ def gemm_slabs(A, B, a_t=False, b_t=False):
     return ws, splits
 
 
+def dw_slab_workspaces(pairs, splits):
+    """The partial slabs hsg_gemm_dw_slabs(_io) writes, one fp32 [splits * M * N] buffer
+    per (A [K, M], B [K, N]) pair WHATEVER the operands' dtype: k_dw stores fp32 partial
+    products (csrc/hsg_dw.hip, dw_tile's epilogue).  Round 5's first bf16-operand run
+    allocated them with ``A.new_empty(n)``, which inherits a bf16 A's dtype -- half the
+    bytes -- and the kernel's stores ran past the buffer: the hipErrorIllegalAddress of
+    test_dw_pair_bf16_operands_bitwise.  Pinned on the CPU by
+    tests/test_fault_regressions.py."""
+    return [A.new_empty(splits * A.shape[1] * B.shape[1], dtype=torch.float32) for A, B in pairs]
+
+
 def gemm_dw_slabs(pairs, splits=None):
     """Split-K partial products of A_q^T B_q for up to two (A [K, M], B [K, N]) pairs
     sharing K -- a layer's two FFN weight gradients dW2 = dY^T H and dW1 = dH^T X --
@@ -326,10 +339,7 @@ def gemm_dw_slabs(pairs, splits=None):
         return None
     n = len(pairs)
     arr = lambda t, xs: (t * n)(*xs)
-    # fp32 slabs whatever the operands' dtype (a bf16 operand's new_empty would be bf16:
-    # half the bytes the kernel writes)
-    ws = [pairs[q][0].new_empty(splits * pairs[q][0].shape[1] * pairs[q][1].shape[1], dtype=torch.float32)
-          for q in range(n)]
+    ws = dw_slab_workspaces(pairs, splits)
     c_i, c_p = ctypes.c_int, ctypes.c_void_p
     io = [int(A.dtype == torch.bfloat16) | (2 * int(B.dtype == torch.bfloat16)) for A, B in pairs]
     dims = (arr(c_i, [A.shape[1] for A, _ in pairs]), arr(c_i, [B.shape[1] for _, B in pairs]), K,

@@ -44,6 +44,18 @@ def _fused_ok(lib, x, w1, w2):
             and w2.is_contiguous())
 
 
+def bf16_rows_ok(d, d_hid):
+    """The bf16 GEMM mode may keep this wide FFN's activation rows (H, y, dY, dH and the
+    edge gate G) in bf16: the kernels that read or write them take the shape.  Mirrors
+    their host checks -- hsg_ln_fwd_y16 / hsg_ln_bwd_dy16 (csrc/hsg_rows.hip: the
+    persistent vector kernels, d % 4 == 0 and 257 <= d <= 512) and hsg_gemm_bf16_psw_io
+    / hsg_gemm_bf16_psw_elug_rho_a16 (csrc/hsg_gemm.hip: a bf16 A operand needs
+    lda % 8 == 0, and H / dH have d_hid columns).  Any other shape keeps fp32 rows
+    (a 256- or 768-wide embedding, or ffn_inner_hidden_size % 8 != 0,
+    would otherwise reach a kernel that refuses it)."""
+    return d % 4 == 0 and 257 <= d <= 512 and d_hid % 8 == 0
+
+
 def _draw(x, p_drop, rng):
     if p_drop <= 0:
         return None, 0
@@ -102,7 +114,8 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
         if b2 is not None and gemm_psw_ln(H, wsplit[1], b2, x, gamma, beta, eps, p_drop, seed_t, off, y, out,
                                           mean, rstd):
             return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
-        if H.dtype == torch.bfloat16 and _lib.path_option("HSG_FFN_BF16_ROWS", "1") != "0":
+        if (H.dtype == torch.bfloat16 and bf16_rows_ok(d, H.shape[1])
+                and _lib.path_option("HSG_FFN_BF16_ROWS", "1") != "0"):
             # the bf16 GEMM mode's bf16 activations: the FFN output y (the LayerNorm
             # input) as bf16 too -- rounded once, <= 2^-9 |y| per element
             y = x.new_empty(n, d, dtype=torch.bfloat16)

@@ -57,11 +57,17 @@ class DropoutRNG:
     def claim(self):
         """(seed, snap) of a pending advance, handed to a kernel that performs it in its
         own launch -- which must come before anything reads the seed (stream order) --
-        or None when no advance is pending."""
+        or None when no advance is pending.  The advance stays pending until the caller
+        reports the launch with :meth:`claimed`: a launch that was refused (HSG_EINVAL,
+        an exception before it) leaves it to the next take(), so a step never reuses the
+        previous step's masks."""
         if not self._pending:
             return None
-        self._pending = False
         return self.seed, self._snap
+
+    def claimed(self):
+        """The kernel handed the pending advance by :meth:`claim` was launched."""
+        self._pending = False
 
 
 def get(device) -> DropoutRNG:

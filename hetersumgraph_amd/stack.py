@@ -38,7 +38,7 @@ from . import _lib
 from . import rng as hsg_rng
 from ._lib import load, stream_of
 from .dense import elug_rho_groups, gemm, gemm_dw_slabs, gemm_slabs
-from .ffn import ffn_bwd, ffn_fwd, ffn_wsplit
+from .ffn import bf16_rows_ok, ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
 from .ops import (LEAKY_SLOPE, attn_params_finish, attn_params_finish_pair, attn_params_workspace, attn_tables,
@@ -169,6 +169,16 @@ def _attn_dst(grads, lay, T):
     return dattn, dwf, dbf, dT, a_h, a_T
 
 
+def rho_partials(G, groups):
+    """The rho partials [n_dst, groups, 3] the dx GEMM's ELU-gate epilogue writes beside
+    the G rows: fp32 whatever G's dtype (hsg_gemm_bf16_psw_elug_rho_a16 stores fp32
+    sums; the one-pass edge backward reads fp32).  Round 5's first bf16-G run made them
+    with ``G.new_empty(...)``, i.e. bf16 -- half the bytes -- and the epilogue's stores
+    ran past the buffer into the allocator's neighbours: the abort in the cfg5-bf16
+    stack backward.  Pinned on the CPU by tests/test_fault_regressions.py."""
+    return G.new_empty(G.shape[0], groups, 3, dtype=torch.float32)
+
+
 def _merged_bwd(gsaved):
     """The one-pass edge backward (hsg_gat_bwd_src_g) covers this application's
     relation and head shape (HSG_GAT_MERGED=0: the dst + src pair, for A/B tests)."""
@@ -204,7 +214,7 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
         # ... and the rho partials, so the edge backward is one source-centric pass
         n_dst, HD = elug[1].shape
         groups = elug_rho_groups(fsaved[11][3], n_dst, gsaved[13])     # the dx GEMM's (W1^T split)
-        elug += (elug[1].new_empty(n_dst, groups, 3, dtype=torch.float32), gsaved[13])
+        elug += (rho_partials(elug[1], groups), gsaved[13])
     # narrow heads (W2S) with h stored: the narrow FFN's backward epilogue makes G and the
     # per-head rho, and the edge backward is one head-lane pass over the words
     gate = None
@@ -266,7 +276,10 @@ class _GatStack(torch.autograd.Function):
         # forward's first launch, which also performs the step's pending dropout-seed
         # advance (before any draw below reads the seed)
         if _lib.path_option("HSG_ATTN_PAIR", "1") != "0":      # both layers' tables in one launch
-            tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T, seed_advance=gen.claim())))
+            adv = gen.claim()
+            tables = dict(zip((id(w2s), id(s2w)), attn_tables_pair(w2s, s2w, T, seed_advance=adv)))
+            if adv is not None:                 # launched (check() raised otherwise): done
+                gen.claimed()
         else:
             tables = {id(lay): attn_tables(lay.attn, T, lay.wf, lay.bf, lay.H, lay.D) for lay in (w2s, s2w)}
         draws = []
@@ -317,7 +330,7 @@ class _GatStack(torch.autograd.Function):
                 # (with dY and dH in the backward): they are only GEMM operands there,
                 # rounded to bf16 by the GEMM anyway -- half their bytes, the same numbers
                 # (HSG_FFN_BF16_ACT=0: fp32 buffers, for the bitwise A/B test)
-                bf = (wsplits[key] is not None and wsplits[key][0].mode == "bf16"
+                bf = (wsplits[key] is not None and wsplits[key][0].mode == "bf16" and bf16_rows_ok(d, d_hid)
                       and _lib.path_option("HSG_FFN_BF16_ACT", "1") != "0")
                 bufs[key] = (X, X.new_empty(n_app[key], rel.n_dst, d_hid,
                                             dtype=torch.bfloat16 if bf else torch.float32))

@@ -57,3 +57,15 @@ def test_host_library_exports_graph_builder():
     for name in names:
         assert hasattr(lib, name), name
     assert ctypes.sizeof(datapipe.HsgDocs) == 8 + 12 * 8
+
+
+def test_host_mirror_of_dw_tiles():
+    """bench.dw_tiles (the byte count's host mirror, no HIP call) equals the library's
+    hsg_gemm_dw_tiles (a host-only query: no GPU needed) on the FFN shapes and a sweep."""
+    import bench
+    from hetersumgraph_amd import _lib
+    lib = _lib.load()
+    shapes = [(300, 512), (512, 300), (64, 512), (512, 64), (4, 4), (160, 128), (161, 129), (1024, 768)]
+    shapes += [(m, n) for m in range(4, 700, 36) for n in range(4, 700, 52)]
+    for m, n in shapes:
+        assert bench.dw_tiles(m, n) == lib.hsg_gemm_dw_tiles(m, n), (m, n)

@@ -1,5 +1,7 @@
 """bench.py's roofline arithmetic against SURVEY §8(d)'s published figures for
-config 2 (CPU only: relation sizes from the oracle's host-side restatement)."""
+config 2 (CPU only, no HIP library: relation sizes from the oracle's host-side
+restatement; the dW tile count from bench.dw_tiles, the host mirror pinned to the
+library in tests/test_abi.py)."""
 import numpy as np
 import pytest
 

@@ -273,3 +273,53 @@ def test_bf16_activations_bitwise_equal_fp32_buffers(train, monkeypatch):
             assert (p.grad is None) == (q.grad is None), n
             if p.grad is not None:
                 assert torch.equal(p.grad, q.grad), f"{m}.{n}"
+
+
+@pytest.mark.parametrize("d,d_hid,heads", [(256, 512, 8), (300, 500, 6)])
+def test_bf16_mode_off_shape_ffn_keeps_fp32_rows(d, d_hid, heads):
+    """in the bf16 GEMM mode the wide FFN's bf16 activation rows need
+    257 <= d <= 512, d % 4 == 0 and d_hid % 8 == 0 (ffn.bf16_rows_ok, the kernels' own
+    checks).  A 256-wide word embedding or an ffn_inner_hidden_size of 500 must keep
+    fp32 rows and run -- forward and backward -- within the bf16 budget of the f32 mode
+    instead of reaching a kernel that refuses the shape."""
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    from hetersumgraph_amd.dense import gemm_dtype
+    from hetersumgraph_amd.module.GAT import WSWGAT
+    from hetersumgraph_amd.stack import gat_stack
+    dev = torch.device("cuda")
+    docs = synth.make_batch_docs("cfg2", seed=0)[:6]
+    z = synth_fixture(docs)
+    n_w, n_s = int(z["n_w"]), int(z["n_s"])
+    torch.manual_seed(11)
+    w2s = WSWGAT(d, 64, 8, 0.1, d_hid, 0.1, 50, "W2S").to(dev).eval()
+    s2w = WSWGAT(64, d, heads, 0.1, d_hid, 0.1, 50, "S2W").to(dev).eval()
+    Xw0 = 0.4 * torch.randn(n_w, d, device=dev)
+    Xs0 = torch.randn(n_s, 64, device=dev)
+    T0 = 0.1 * torch.randn(10, 50, device=dev)
+    R = torch.randn(n_s, 64, device=dev)
+    runs = {}
+    for dt in ("f32", "bf16"):
+        G = build_graph(z).to(dev)
+        Xw, Xs, T = (t.clone().requires_grad_() for t in (Xw0, Xs0, T0))
+        register_tfidf_table(G, T)
+        for m in (w2s, s2w):
+            m.zero_grad(set_to_none=True)
+        with gemm_dtype(dt):
+            s = gat_stack(G, w2s, s2w, T, Xw, Xs, 2)
+            ctx = s.grad_fn
+            h_dtypes = {k: v[1].dtype for k, v in ctx.bufs.items()}
+            s.backward(R)
+        torch.cuda.synchronize()
+        runs[dt] = dict(s=s.detach(), Xw=Xw.grad, Xs=Xs.grad, T=T.grad, h=h_dtypes,
+                        p={n: p.grad.clone() for m in (w2s, s2w) for n, p in m.named_parameters()
+                           if p.grad is not None})
+    a, b = runs["f32"], runs["bf16"]
+    assert all(t == torch.float32 for t in b["h"].values())      # no bf16 rows for this shape
+    assert (a["s"] - b["s"]).abs().max().item() <= 1e-2
+    for k in ("Xw", "Xs", "T"):
+        assert ((a[k] - b[k]).norm() / a[k].norm()).item() <= 5e-2, k
+    assert a["p"].keys() == b["p"].keys()
+    for n in a["p"]:
+        tol = 1.5e-1 if ("feat_" in n or "attn_" in n) else 5e-2      # cancelling attention sums
+        assert ((a["p"][n] - b["p"][n]).norm() / a["p"][n].norm().clamp_min(1e-30)).item() <= tol, n
