@@ -35,7 +35,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_gemm_bf16_slabs", "hsg_gemm_dw_slabs", "hsg_gemm_dw_tiles", "hsg_gemm_psw_row_tiles", "hsg_gemm_psw_ln",
            "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate",
            "hsg_gat_bwd_src_g_blocks", "hsg_gemm_bf16_psw_io", "hsg_gemm_bf16_psw_elug_rho_a16", "hsg_gemm_psw_elug_rho_gw", "hsg_ln_bwd_dy16",
-           "hsg_gemm_dw_slabs_io", "hsg_ln_fwd_y16", "hsg_gat_bwd_src_g_io")
+           "hsg_gemm_dw_slabs_io", "hsg_ln_fwd_y16", "hsg_gat_bwd_src_g_io", "hsg_rel_work", "hsg_gat_fwd_ws_floats",
+           "hsg_gat_fwd_ws", "hsg_gat_bwd_src_g_ws_floats", "hsg_gat_bwd_src_g_ws")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -52,7 +53,9 @@ class HsgRel(ctypes.Structure):
     _fields_ = [("n_src", ctypes.c_int32), ("n_dst", ctypes.c_int32), ("n_edges", ctypes.c_int32),
                 ("indptr", ctypes.c_void_p), ("src", ctypes.c_void_p), ("tf", ctypes.c_void_p),
                 ("phantom", ctypes.c_void_p), ("cindptr", ctypes.c_void_p),
-                ("cdst", ctypes.c_void_p), ("cperm", ctypes.c_void_p)]
+                ("cdst", ctypes.c_void_p), ("cperm", ctypes.c_void_p),
+                ("n_dwork", ctypes.c_int32), ("n_swork", ctypes.c_int32),
+                ("dwork", ctypes.c_void_p), ("swork", ctypes.c_void_p)]
 
 
 _lib = None
@@ -148,11 +151,17 @@ _SIGS = {
     "hsg_ln_fwd_y16": [_I, _I, _P, _P, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
     "hsg_gat_bwd_src_g_io": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P],
     "hsg_gemm_dw_slabs_io": [_I, _P, _P, _I, _P, _P, _P, _P, _P, _I, _P, _P],
+    "hsg_rel_work": [_I, _P, _I, _I, _P, _I, _P, _P],
+    "hsg_gat_fwd_ws_floats": [_RELP, _I, _I],
+    "hsg_gat_fwd_ws": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_bwd_src_g_ws_floats": [_RELP, _I, _I],
+    "hsg_gat_bwd_src_g_ws": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
 }
 _RESTYPE = {"hsg_version": ctypes.c_char_p, "hsg_wsplit_dims": None, "hsg_gemm_workspace_floats": ctypes.c_size_t,
             "hsg_attn_params_bwd_workspace_floats": ctypes.c_size_t,
             "hsg_dropmask_scale": ctypes.c_float,
-            "hsg_rel_build_workspace_bytes": ctypes.c_size_t}
+            "hsg_rel_build_workspace_bytes": ctypes.c_size_t, "hsg_gat_fwd_ws_floats": ctypes.c_size_t,
+            "hsg_gat_bwd_src_g_ws_floats": ctypes.c_size_t}
 
 
 def load():

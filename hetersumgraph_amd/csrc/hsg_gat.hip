@@ -89,6 +89,9 @@ struct RelPtrs {
     const int32_t *__restrict__ cdst;
     const int32_t *__restrict__ cperm;
     int xcd;                 // 1: XCD-local node order (work_range)
+    int n_dwork, n_swork;    // work lists (hsg_rel.dwork / swork; round 6), 0 = none
+    const int32_t *__restrict__ dwork;
+    const int32_t *__restrict__ swork;
 };
 
 // XCD-local node order (round 4).  The batched graph is a disjoint union of documents
@@ -113,7 +116,8 @@ RelPtrs rel_ptrs(const hsg_rel *r) {
     int xcd = 1;
     if (const char *e = HSG_DEV_ENV("HSG_GAT_XCD")) xcd = atoi(e);      // dev A/B
     return RelPtrs{r->n_src, r->n_dst, r->n_edges, r->indptr, r->src, r->tf, r->phantom,
-                   r->cindptr, r->cdst, r->cperm, xcd};
+                   r->cindptr, r->cdst, r->cperm, xcd, r->dwork ? r->n_dwork : 0, r->swork ? r->n_swork : 0,
+                   r->dwork, r->swork};
 }
 
 template <int TAU_MODE>
@@ -180,7 +184,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                                                 const float *__restrict__ tau,
                                                 const float *__restrict__ origin,
                                                 float *__restrict__ hout, float *__restrict__ out,
-                                                float *__restrict__ mout, float *__restrict__ lout) {
+                                                float *__restrict__ mout, float *__restrict__ lout,
+                                                float *__restrict__ pws) {
     constexpr int NPB = HSG_WAVES / WPN;
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
     __shared__ int s_nb[HSG_WAVES][HSG_CHUNK];
@@ -206,7 +211,11 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     int *sn = s_nb[wid];
 
     static_assert(PF == 0 || WPN == 1, "prefetch: one destination per wave");
-    const WorkRange wr = work_range(R.n_dst, NPB, wid / WPN, R.xcd);
+    // round 6: with the relation's CSR work list (and the piece scratch pws) the loop
+    // walks its items -- whole destinations, and pieces of the long ones, whose (max,
+    // sum, partial h) go to pws for k_gat_fwd_merge (multi-wave form only)
+    const bool wl = WPN > 1 && pws != nullptr && R.n_dwork > 0;
+    const WorkRange wr = work_range(wl ? R.n_dwork : R.n_dst, NPB, wid / WPN, R.xcd);
     const int vstride = wr.stride;
     int pf_beg = 0, pf_end = 0, pf_c = 0;
     int pu = 0, pt = 0;                                   // PF = 2: next destination, edge l
@@ -243,7 +252,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         }
     }
     for (int v_ = wr.first; v_ < wr.end; v_ += vstride) {
-        const int v = __builtin_amdgcn_readfirstlane(v_);      // scalar loads of indptr / phantom
+        const int item = __builtin_amdgcn_readfirstlane(v_);   // scalar loads of indptr / phantom
+        int v = item;
+        bool piece = false;
         int beg, end, c;
         float org[NF];
         if constexpr (PF) {
@@ -260,6 +271,13 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             }
             const int vn = v_ + vstride;
             if (vn < wr.end) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
+        } else if (wl) {
+            const int code = R.dwork[3 * item];
+            beg = R.dwork[3 * item + 1];
+            end = R.dwork[3 * item + 2];
+            piece = code < 0;
+            v = piece ? -code - 1 : code;
+            c = piece ? 0 : R.phantom[v];                      // a piece's phantoms: in the merge
         } else {
             beg = R.indptr[v];
             end = R.indptr[v + 1];
@@ -317,7 +335,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         // the residual row: independent of the gathers below
         if constexpr (PF == 0) {
 #pragma unroll
-            for (int i = 0; i < NF; ++i) org[i] = (origin && writer) ? origin[(size_t)v * HD + fo[i]] : 0.f;
+            for (int i = 0; i < NF; ++i) org[i] = (origin && writer && !piece) ? origin[(size_t)v * HD + fo[i]] : 0.f;
         }
 
         // PF = 3: the next destination's (sigma, tau) and residual row, requested once
@@ -394,8 +412,20 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             }
         }
         if constexpr (PF == 2) pf_scores();              // ... and its (sigma, tau), before the stores
-        // epilogue: h, and elu(h) + origin (GAT.py:56-57)
-        if (writer) {
+        // epilogue: h, and elu(h) + origin (GAT.py:56-57); a piece: its partial h (normalised
+        // by its own sum), max and sum, [HD | H | H] per item
+        if (writer && piece) {
+            float *pw = pws + (size_t)item * (HD + 2 * H);
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                const int f = lane + 64 * i;
+                if (f < HD) pw[f] = acc[i];
+            }
+            if (kact && l == 0) {
+                pw[HD + k] = mx;
+                pw[HD + H + k] = sm;
+            }
+        } else if (writer) {
 #pragma unroll
             for (int i = 0; i < NF; ++i) {
                 const int f = lane + 64 * i;
@@ -412,6 +442,59 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             }
         }
         if constexpr (WPN > 1) __syncthreads();          // s_ml / s_acc are reused
+    }
+}
+
+// Merge of the pieces of long destinations (round 6; after k_gat_fwd with a CSR work
+// list).  One wave per work item; the wave of a destination's FIRST piece merges all
+// of its pieces in item order with its phantoms, exactly the online-softmax algebra of
+// a whole destination: M = max(max_p m_p, 0 if c > 0), L = sum_p l_p e^(m_p - M) +
+// c e^(-M), h = sum_p (l_p e^(m_p - M) / L) h_p, then elu(h) + origin and (m, l) = (M,
+// L).  Lane = feature (flat mapping, as k_gat_fwd); deterministic.
+template <int NF>
+__global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, const float *__restrict__ origin,
+                                                       const float *__restrict__ pws, float *__restrict__ hout,
+                                                       float *__restrict__ out, float *__restrict__ mout,
+                                                       float *__restrict__ lout) {
+    const int lane = threadIdx.x & 63;
+    const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * HSG_WAVES + (threadIdx.x >> 6)));
+    if (item >= R.n_dwork) return;
+    const int code = R.dwork[3 * item];
+    if (code >= 0 || (item > 0 && R.dwork[3 * (item - 1)] == code)) return;   // not a first piece
+    int last = item + 1;
+    while (last < R.n_dwork && R.dwork[3 * last] == code) ++last;
+    const int v = -code - 1, HD = H * D, W = HD + 2 * H;
+    const float c = (float)R.phantom[v];
+    const float *pw = pws + (size_t)item * W;
+    const int np = last - item;
+    // per head (lanes k < H, then the features' heads): M and L
+    auto head_ml = [&](int k, float &M, float &L) {
+        M = c > 0.f ? 0.f : -INFINITY;
+        for (int p = 0; p < np; ++p) M = fmaxf(M, pw[p * W + HD + k]);
+        L = c > 0.f ? c * __expf(-M) : 0.f;
+        for (int p = 0; p < np; ++p) L += pw[p * W + HD + H + k] * __expf(pw[p * W + HD + k] - M);
+    };
+    if (lane < H) {
+        float M, L;
+        head_ml(lane, M, L);
+        mout[v * H + lane] = M;
+        lout[v * H + lane] = L;
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        if (f < HD) {
+            const int k = f / D;
+            float M, L;
+            head_ml(k, M, L);
+            const float inv = 1.f / L;
+            float h = 0.f;
+            for (int p = 0; p < np; ++p)
+                h = fmaf(pw[p * W + HD + H + k] * __expf(pw[p * W + HD + k] - M) * inv, pw[p * W + f], h);
+            const size_t o = (size_t)v * HD + f;
+            if (hout) hout[o] = h;
+            if (origin) out[o] = elu1(h) + origin[o];
+        }
     }
 }
 
@@ -1442,7 +1525,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
 // hsg_gat_bwd_dst_g + hsg_gat_bwd_src pair (G read once, no dpre round trip).
 // GBF (round 5, the bf16 GEMM mode): G comes as bf16 rows (hsg_gemm_bf16_psw_elug_rho_a16
 // with g_bf16), held raw until the edge uses them.
-template <int NE, int OCC = 1, int EQ = 4, bool GBF = false>
+template <int NE, int OCC = 1, int EQ = 4, bool GBF = false, bool WL = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, int D, int lph, float slope,
                                                       const float *__restrict__ sigma,
                                                       const float *__restrict__ tau,
@@ -1454,7 +1537,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
                                                       const float *__restrict__ Z,
                                                       float *__restrict__ dZ, float *__restrict__ dsigma,
                                                       float *__restrict__ da1_part,
-                                                      float *__restrict__ dtau_part) {
+                                                      float *__restrict__ dtau_part,
+                                                      float *__restrict__ pws) {
     constexpr int WPN = HSG_WAVES;
     __shared__ float s_acc[HSG_WAVES][512];
     __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
@@ -1479,14 +1563,30 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
         fo[i] = c0 + min(l + lph * i, D - 1);
     }
 
-    const WorkRange wr = work_range(R.n_src, 1, 0, R.xcd);
+    // round 6: with the relation's CSC work list (and the piece scratch pws) the loop walks
+    // its items -- whole sources, and pieces of the long ones (the HDSG doc supernodes),
+    // whose dZ / dsigma partials go to pws for k_gat_bwd_src_g_merge
+    // (WL: a template flag, so the kernel without a list keeps its registers)
+    constexpr bool wl = WL;
+    const WorkRange wr = work_range(wl ? R.n_swork : R.n_src, 1, 0, R.xcd);
     for (int u_ = wr.first; u_ < wr.end; u_ += wr.stride) {
-        const int u = __builtin_amdgcn_readfirstlane(u_);
+        const int item = __builtin_amdgcn_readfirstlane(u_);
         // opaque per source: the compiler would otherwise hoist a 64-bit address per
         // feature and array (Z, a1, dZ, s_acc) out of the source loop and spill them
 #pragma unroll
         for (int i = 0; i < NE; ++i) asm volatile("" : "+v"(fo[i]));
-        const int beg = R.cindptr[u], end = R.cindptr[u + 1];
+        int u = item, beg, end;
+        bool piece = false;
+        if (wl) {
+            const int code = R.swork[3 * item];
+            beg = R.swork[3 * item + 1];
+            end = R.swork[3 * item + 2];
+            piece = code < 0;
+            u = piece ? -code - 1 : code;
+        } else {
+            beg = R.cindptr[u];
+            end = R.cindptr[u + 1];
+        }
         int eb, ee;
         subrange(beg, end, wid, WPN, eb, ee);
         const float sig = kact ? sigma[u * H + k] : 0.f;
@@ -1565,7 +1665,13 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
             float ds = 0.f;
 #pragma unroll
             for (int w = 0; w < WPN; ++w) ds += s_dsig[w][kc];
-            if (dsigma && kact && l == 0) dsigma[u * H + k] = ds;
+            // a piece: its dZ partial without the ds * a1 term and its ds to pws
+            // ([HD | H] per item), for the merge; its ds * Z_u into d a1 as any source's
+            float *pw = piece ? pws + (size_t)item * (HD + H) : nullptr;
+            if (kact && l == 0) {
+                if (piece) pw[HD + k] = ds;
+                else if (dsigma) dsigma[u * H + k] = ds;
+            }
 #pragma unroll
             for (int i = 0; i < NE; ++i) {
                 if (kact && l + lph * i < D) {
@@ -1573,8 +1679,12 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
                     float a = 0.f;
 #pragma unroll
                     for (int w = 0; w < WPN; ++w) a += s_acc[w][f];
-                    if (a1) a = fmaf(ds, a1[f], a);
-                    dZ[(size_t)u * HD + f] = a;
+                    if (piece) {
+                        pw[f] = a;
+                    } else {
+                        if (a1) a = fmaf(ds, a1[f], a);
+                        dZ[(size_t)u * HD + f] = a;
+                    }
                     da1[i] = fmaf(ds, zk[i], da1[i]);
                 }
             }
@@ -1595,6 +1705,40 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
 #pragma unroll
         for (int w = 0; w < HSG_WAVES; ++w) a += s_dtau[w][i];
         dtau_part[(size_t)blockIdx.x * nt + i] = a;
+    }
+}
+
+// Merge of the pieces of long sources (round 6; after k_gat_bwd_src_g with a CSC work
+// list).  One wave per work item; the wave of a source's FIRST piece sums its pieces'
+// partials in item order: dsigma_u,k = sum_p ds_p,k, dZ_u = sum_p dZ_p + dsigma_u * a1.
+template <int NF>
+__global__ __launch_bounds__(256) void k_gat_bwd_src_g_merge(RelPtrs R, int H, int D, const float *__restrict__ pws,
+                                                             const float *__restrict__ a1, float *__restrict__ dZ,
+                                                             float *__restrict__ dsigma) {
+    const int lane = threadIdx.x & 63;
+    const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * HSG_WAVES + (threadIdx.x >> 6)));
+    if (item >= R.n_swork) return;
+    const int code = R.swork[3 * item];
+    if (code >= 0 || (item > 0 && R.swork[3 * (item - 1)] == code)) return;   // not a first piece
+    int last = item + 1;
+    while (last < R.n_swork && R.swork[3 * last] == code) ++last;
+    const int u = -code - 1, HD = H * D, W = HD + H, np = last - item;
+    const float *pw = pws + (size_t)item * W;
+    auto head_ds = [&](int k) {
+        float ds = 0.f;
+        for (int p = 0; p < np; ++p) ds += pw[p * W + HD + k];
+        return ds;
+    };
+    if (dsigma && lane < H) dsigma[u * H + lane] = head_ds(lane);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        if (f < HD) {
+            float a = 0.f;
+            for (int p = 0; p < np; ++p) a += pw[p * W + f];
+            if (a1) a = fmaf(head_ds(f / D), a1[f], a);
+            dZ[(size_t)u * HD + f] = a;
+        }
     }
 }
 
@@ -1857,11 +2001,11 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
 template <int TAU, int WPN, int OCC = 1, int PF = 0>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
-                 float *out, float *m, float *l) {
+                 float *out, float *m, float *l, float *pws = nullptr, bool last = true) {
 #define HSG_FWD(NF_)                                                                                     \
     case NF_:                                                                                            \
-        HSG_KLAUNCH(true, true, (k_gat_fwd<NF_, TAU, WPN, OCC, PF>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
-                    sg, tau, org, h, out, m, l);                                                         \
+        HSG_KLAUNCH(true, last, (k_gat_fwd<NF_, TAU, WPN, OCC, PF>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
+                    sg, tau, org, h, out, m, l, pws);                                                    \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
@@ -2114,6 +2258,18 @@ extern "C" {
 int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
                 const float *sigma, const float *tau, const float *origin, float *h, float *out,
                 float *m, float *l, void *stream) {
+    return hsg_gat_fwd_ws(rel, H, D, tau_mode, slope, Z, sigma, tau, origin, h, out, m, l, nullptr, stream);
+}
+
+size_t hsg_gat_fwd_ws_floats(const hsg_rel *rel, int H, int D) {
+    if (!rel || !shape_ok(H, D) || !rel->dwork || rel->n_dwork <= 0 || rel->n_dst == 0 || dst_wpn(rel) != 4)
+        return 0;
+    return (size_t)rel->n_dwork * (size_t)(H * D + 2 * H);
+}
+
+int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                   const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                   float *l, float *ws, void *stream) {
     if (!rel || !shape_ok(H, D) || (origin && !out) || (!origin && !h)) return HSG_EINVAL;
     if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     if (rel->n_dst == 0) return 0;
@@ -2227,9 +2383,30 @@ int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope, con
 #ifdef HSG_DEV
     if (wpn == 1) return tau_mode == HSG_TAU_TABLE ? HSG_F(HSG_TAU_TABLE, 1) : HSG_F(HSG_TAU_PER_EDGE, 1);
 #endif
-    if (tau_mode == HSG_TAU_TABLE) return HSG_F(HSG_TAU_TABLE, 4);         // wpn == 1 took the w = 7 kernel above
-    return HSG_F(HSG_TAU_PER_EDGE, 4);
 #undef HSG_F
+    // wpn == 1 took the w = 7 kernel above.  Multi-wave destinations: with the CSR work
+    // list (and its scratch) the items of the list, then the merge of the long
+    // destinations' pieces (round 6)
+    const bool wl = ws && R.n_dwork > 0;
+    const dim3 g4(grid_nodes(wl ? R.n_dwork : rel->n_dst, 4, fcap));
+    float *pws = wl ? ws : nullptr;
+    const int rc = tau_mode == HSG_TAU_TABLE
+                       ? fwd_dispatch<HSG_TAU_TABLE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out,
+                                                        m, l, pws, !wl)
+                       : fwd_dispatch<HSG_TAU_PER_EDGE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin, h,
+                                                           out, m, l, pws, !wl);
+    if (rc != 0 || !wl) return rc;
+    const dim3 gm((unsigned)((R.n_dwork + HSG_WAVES - 1) / HSG_WAVES));
+#define HSG_FM(NF_)                                                                                          \
+    case NF_:                                                                                                \
+        HSG_KLAUNCH(false, true, (k_gat_fwd_merge<NF_>), gm, dim3(256), st, R, H, D, origin, pws, h, out, m, l); \
+        break;
+    switch (nf) {
+        HSG_FM(1) HSG_FM(2) HSG_FM(3) HSG_FM(4) HSG_FM(5) HSG_FM(6) HSG_FM(7) HSG_FM(8)
+        default: return HSG_EINVAL;
+    }
+#undef HSG_FM
+    return launch_status();
 }
 
 int hsg_gat_bwd_blocks(const hsg_rel *rel) {
@@ -2420,7 +2597,17 @@ int hsg_gat_bwd_src_g_blocks(const hsg_rel *rel, int H, int D) {
         const int b = (groups + HSG_WAVES - 1) / HSG_WAVES;
         return b < 1 ? 1 : (b < kBwdSrcGridCap ? b : kBwdSrcGridCap);
     }
-    return grid_nodes(rel->n_src, 4, kBwdSrcGridCap);        // one source per block per iteration
+    // one source (or CSC work item, round 6) per block per iteration; the work-list grid
+    // whether or not the caller passes the piece scratch (a larger grid only adds
+    // partial rows of zeros), so the slabs are sized alike for both entry points
+    const int items = rel->swork && rel->n_swork > 0 ? rel->n_swork : rel->n_src;
+    return grid_nodes(items, 4, kBwdSrcGridCap);
+}
+
+size_t hsg_gat_bwd_src_g_ws_floats(const hsg_rel *rel, int H, int D) {
+    if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !srcg_wide(rel, H, D) || !rel->swork || rel->n_swork <= 0)
+        return 0;
+    return (size_t)rel->n_swork * (size_t)(H * D + H);
 }
 
 // the wide one-pass kernel on bf16 G rows (the bf16 GEMM mode): g_bf16 != 0 needs the
@@ -2442,6 +2629,14 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
                          const float *m, const float *l, const void *Gv, int g_bf16, const float *rho, int rho_groups,
                          const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                          float *dtau_part, void *stream) {
+    return hsg_gat_bwd_src_g_ws(rel, H, D, slope, sigma, tau, m, l, Gv, g_bf16, rho, rho_groups, a1, Z, dZ, dsigma,
+                                da1_part, dtau_part, nullptr, stream);
+}
+
+int hsg_gat_bwd_src_g_ws(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                         const float *m, const float *l, const void *Gv, int g_bf16, const float *rho, int rho_groups,
+                         const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                         float *dtau_part, float *ws, void *stream) {
     const float *G = reinterpret_cast<const float *>(Gv);
     if (g_bf16 && rho_groups == 0) return HSG_EINVAL;
     if (!hsg_gat_bwd_src_g_supported(rel, H, D) || !G || !rho || !Z || !dZ || !dtau_part) return HSG_EINVAL;
@@ -2467,13 +2662,22 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
     const int rgw = rho_groups == (H * D + 63) / 64 ? 64 : rho_groups == (H * D + 111) / 112 ? 112 : 0;
     if (!srcg_wide(rel, H, D) || rgw == 0 || D > rgw) return HSG_EINVAL;
     const int lph = lanes_per_head(H), ne = (D + lph - 1) / lph;
+    // the CSC work list with its scratch: pieces of the long sources, merged below (round 6)
+    const bool wl = ws && R.n_swork > 0;
+    float *pws = wl ? ws : nullptr;
+#define HSG_SG1(NE_, OCC_, EQ_, GBF_, WL_)                                                                   \
+    HSG_KLAUNCH(true, !wl, (k_gat_bwd_src_g<NE_, OCC_, EQ_, GBF_, WL_>), grid, dim3(256), st, R, H, D, lph,    \
+                slope, sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part, pws)
 #define HSG_SG(NE_, OCC_, EQ_)                                                                               \
-    if (g_bf16)                                                                                              \
-        HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_, true>), grid, dim3(256), st, R, H, D, lph,   \
-                    slope, sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part);\
-    else                                                                                                     \
-        HSG_KLAUNCH(true, true, (k_gat_bwd_src_g<NE_, OCC_, EQ_>), grid, dim3(256), st, R, H, D, lph, slope,  \
-                    sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part)
+    do {                                                                                                     \
+        if (g_bf16) {                                                                                        \
+            if (wl) HSG_SG1(NE_, OCC_, EQ_, true, true);                                                     \
+            else HSG_SG1(NE_, OCC_, EQ_, true, false);                                                       \
+        } else {                                                                                             \
+            if (wl) HSG_SG1(NE_, OCC_, EQ_, false, true);                                                    \
+            else HSG_SG1(NE_, OCC_, EQ_, false, false);                                                      \
+        }                                                                                                    \
+    } while (0)
     // EQ: destination rows in flight per wave, as many as fit 5 blocks per CU unspilled
 #ifdef HSG_DEV
     const char *eq = HSG_DEV_ENV("HSG_SRCG_EQ");                               // dev A/B
@@ -2485,6 +2689,20 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
     else if (ne <= 7) HSG_SG(7, 5, 2);
     else HSG_SG(8, 5, 1);
 #undef HSG_SG
+#undef HSG_SG1
+    const int rc = launch_status();
+    if (rc != 0 || !wl) return rc;
+    const int nf = (H * D + 63) / 64;
+    const dim3 gm((unsigned)((R.n_swork + HSG_WAVES - 1) / HSG_WAVES));
+#define HSG_SM(NF_)                                                                                           \
+    case NF_:                                                                                                 \
+        HSG_KLAUNCH(false, true, (k_gat_bwd_src_g_merge<NF_>), gm, dim3(256), st, R, H, D, pws, a1, dZ, dsigma); \
+        break;
+    switch (nf) {
+        HSG_SM(1) HSG_SM(2) HSG_SM(3) HSG_SM(4) HSG_SM(5) HSG_SM(6) HSG_SM(7) HSG_SM(8)
+        default: return HSG_EINVAL;
+    }
+#undef HSG_SM
     return launch_status();
 }
 

@@ -189,7 +189,79 @@ __global__ void k_node_fill(int n, const int32_t *__restrict__ fs, const int32_t
     }
 }
 
+// Work list of one CSR / CSC (hsg_rel_work, round 6).  One block of kWorkThreads walks
+// the nodes in tiles: per node k(v) = deg > P ? ceil(deg / P) : 1 items, an exclusive
+// block scan of k over the tile (+ the running offset) places them, and the pieces of
+// a long node split its segment into k near-equal runs.  *count = items, or 0 when no
+// node is long (nothing to balance: the kernels then walk the nodes).
+constexpr int kWorkThreads = 1024;
+
+__global__ __launch_bounds__(kWorkThreads) void k_rel_work(int n, const int32_t *__restrict__ indptr, int min_len,
+                                                            int mult, int32_t *__restrict__ work, int max_items,
+                                                            int32_t *__restrict__ count) {
+    __shared__ int s_scan[kWorkThreads];
+    __shared__ int s_any;
+    const int t = threadIdx.x;
+    const int E = indptr[n];
+    const int mean = (E + n - 1) / n;                       // ceil(E / n), n >= 1
+    const int P = max(min_len, mult * mean);
+    if (t == 0) s_any = 0;
+    __syncthreads();
+    int base = 0;
+    for (int v0 = 0; v0 < n; v0 += kWorkThreads) {
+        const int v = v0 + t;
+        int beg = 0, deg = 0, k = 0;
+        if (v < n) {
+            beg = indptr[v];
+            deg = indptr[v + 1] - beg;
+            k = deg > P ? (deg + P - 1) / P : 1;
+        }
+        if (k > 1) s_any = 1;                              // benign race: every writer stores 1
+        // inclusive Hillis-Steele scan of k over the tile
+        s_scan[t] = k;
+        __syncthreads();
+        for (int o = 1; o < kWorkThreads; o <<= 1) {
+            const int x = t >= o ? s_scan[t - o] : 0;
+            __syncthreads();
+            s_scan[t] += x;
+            __syncthreads();
+        }
+        const int first = base + s_scan[t] - k;
+        if (v < n) {
+            if (k == 1) {
+                if (first < max_items) {
+                    work[3 * first] = v;
+                    work[3 * first + 1] = beg;
+                    work[3 * first + 2] = beg + deg;
+                }
+            } else {
+                for (int p = 0; p < k; ++p) {            // near-equal runs: the first deg % k one longer
+                    const int q = deg / k, r = deg % k;
+                    const int b = beg + p * q + min(p, r), e = b + q + (p < r ? 1 : 0);
+                    if (first + p < max_items) {
+                        work[3 * (first + p)] = -(v + 1);
+                        work[3 * (first + p) + 1] = b;
+                        work[3 * (first + p) + 2] = e;
+                    }
+                }
+            }
+        }
+        base += s_scan[kWorkThreads - 1];
+        __syncthreads();                                 // s_scan reused by the next tile
+    }
+    if (t == 0) *count = (s_any && base <= max_items) ? base : 0;
+}
+
 }  // namespace
+
+extern "C" int hsg_rel_work(int n, const int32_t *indptr, int min_len, int mult, int32_t *work, int max_items,
+                            int32_t *count, void *stream) {
+    if (n < 0 || !count || mult < 0 || (n > 0 && (!indptr || !work || max_items < n))) return HSG_EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0 || min_len <= 0) return (int)hipMemsetAsync(count, 0, sizeof(int32_t), s);
+    k_rel_work<<<1, kWorkThreads, 0, s>>>(n, indptr, min_len, mult, work, max_items, count);
+    return (int)hipGetLastError();
+}
 
 extern "C" size_t hsg_rel_build_workspace_bytes(int n_nodes, int n_edges) {
     if (n_nodes < 0 || n_edges < 0) return 0;

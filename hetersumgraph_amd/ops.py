@@ -77,8 +77,9 @@ class _GatAggregate(torch.autograd.Function):
         out = Z.new_empty(n_dst, HD) if origin is not None else None
         m = Z.new_empty(n_dst, H)
         l = Z.new_empty(n_dst, H)
-        check(lib.hsg_gat_fwd(relp, H, D, tau_mode, slope, ptr(Z), ptr(sigma), ptr(tau),
-                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+        ws = fwd_workspace(lib, relp, H, D, Z)
+        check(lib.hsg_gat_fwd_ws(relp, H, D, tau_mode, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                 ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), ptr(ws), st), "hsg_gat_fwd_ws")
         ctx.save_for_backward(Z, a1, sigma, tau, h, m, l)
         ctx.rel, ctx.H, ctx.D, ctx.slope, ctx.tau_mode = rel, H, D, slope, tau_mode
         ctx.has_origin = origin is not None
@@ -109,6 +110,13 @@ class _GatAggregate(torch.autograd.Function):
             da1 = torch.einsum("uk,ukd->kd", dsig, Z.view(-1, H, D))
         dtau = dtp.sum(0) if mode == HSG_TAU_TABLE else dpre
         return dZ, da1, dtau, (dout if ctx.has_origin else None), None, None, None, None, None
+
+
+def fwd_workspace(lib, relp, H, D, like):
+    """Scratch of hsg_gat_fwd_ws for the relation's CSR work list (the pieces of its long
+    destinations), or None when it has none."""
+    n = lib.hsg_gat_fwd_ws_floats(relp, H, D)
+    return like.new_empty(n) if n else None
 
 
 def attn_tables(attn, T, wf, bf, H, D):
@@ -180,8 +188,9 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     l = Z.new_empty(n_dst, H)
     tok = _clock_start(("gat_fwd", rel.kind), Z)
     try:
-        check(lib.hsg_gat_fwd(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                              ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), st), "hsg_gat_fwd")
+        ws = fwd_workspace(lib, relp, H, D, Z)
+        check(lib.hsg_gat_fwd_ws(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                 ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), ptr(ws), st), "hsg_gat_fwd_ws")
     except BaseException:
         _clock_abort(tok)
         raise
@@ -232,14 +241,13 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
         if merged:                          # one source-centric pass (G and rho from the FFN epilogue)
             # rho [n_dst, groups, 3]: 64-column-group partials (wide heads); [n_dst, H]: per head
             groups = rho.shape[1] if rho.dim() == 3 else 0
-            if G.dtype == torch.bfloat16:   # the bf16 GEMM mode's bf16 G rows
-                check(lib.hsg_gat_bwd_src_g_io(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G), 1,
-                                               ptr(rho), groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p),
-                                               ptr(dtp), st), "hsg_gat_bwd_src_g_io")
-            else:
-                check(lib.hsg_gat_bwd_src_g(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G),
-                                            ptr(rho), groups, ptr(a1), ptr(Z), ptr(dZt), None, ptr(da1p), ptr(dtp),
-                                            st), "hsg_gat_bwd_src_g")
+            # (G bf16: the bf16 GEMM mode's bf16 G rows; ws: the pieces of the relation's
+            # long sources, when it has a CSC work list)
+            n_ws = lib.hsg_gat_bwd_src_g_ws_floats(relp, H, D)
+            ws = Z.new_empty(n_ws) if n_ws else None
+            check(lib.hsg_gat_bwd_src_g_ws(relp, H, D, slope, ptr(sigma), ptr(tau), ptr(m), ptr(l), ptr(G),
+                                           int(G.dtype == torch.bfloat16), ptr(rho), groups, ptr(a1), ptr(Z),
+                                           ptr(dZt), None, ptr(da1p), ptr(dtp), ptr(ws), st), "hsg_gat_bwd_src_g_ws")
         else:
             dpre = Z.new_empty(rel.n_typed, H)
             if g_given:                     # G from the FFN epilogue (forward without h)

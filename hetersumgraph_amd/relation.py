@@ -71,6 +71,8 @@ class Relation:
         r.__dict__.update(self.__dict__)
         r.device = device
         r.dev = {k: torch.from_numpy(np.ascontiguousarray(v)).to(device) for k, v in self.host.items()}
+        if device.type == "cuda":
+            attach_work_lists(r.dev, self.n_src, self.n_dst, self.n_typed)
         r._cstruct = None
         return r
 
@@ -86,12 +88,40 @@ class Relation:
         if self._cstruct is None:
             from ._lib import HsgRel
             d = self.dev
+            dw, sw = d.get("dwork"), d.get("swork")
             self._cstruct = HsgRel(
                 self.n_src, self.n_dst, self.n_typed,
                 d["indptr"].data_ptr(), d["src"].data_ptr(), d["tf"].data_ptr(),
                 d["phantom"].data_ptr(), d["cindptr"].data_ptr(), d["cdst"].data_ptr(),
-                d["cperm"].data_ptr())
+                d["cperm"].data_ptr(),
+                dw.shape[0] if dw is not None else 0, sw.shape[0] if sw is not None else 0,
+                dw.data_ptr() if dw is not None else None, sw.data_ptr() if sw is not None else None)
         return self._cstruct
+
+
+# Work lists of degree-skewed relations (round 6, hsg_rel_work): a node whose segment is
+# longer than P = max(PIECE_MIN, PIECE_MULT * ceil(mean segment)) is walked as near-equal
+# pieces, so the HDSG doc supernodes (~250 word edges each, dataloader.py:387-400, next
+# to ~20 per sentence) no longer set the edge kernels' critical path.  cfg2 / cfg5 have
+# no such node (no list: the kernels walk the nodes as before).
+PIECE_MIN = 32
+PIECE_MULT = 2
+
+
+def _work_list(lib, n, indptr, n_edges, stream):
+    """(work [items, 3] int32 tensor, or None) of one CSR / CSC: launched here, its item
+    count read back by the caller (``count``)."""
+    from . import _lib
+    pmin = int(_lib.path_option("HSG_PIECE_MIN", str(PIECE_MIN)))      # dev A/B (0: no lists)
+    mult = int(_lib.path_option("HSG_PIECE_MULT", str(PIECE_MULT)))
+    if n <= 0 or pmin <= 0:
+        return None, None
+    cap = n + 2 * n_edges // pmin + 1
+    work = torch.empty(cap, 3, dtype=torch.int32, device=indptr.device)
+    count = torch.zeros(1, dtype=torch.int32, device=indptr.device)
+    _lib.check(lib.hsg_rel_work(n, _lib.ptr(indptr), pmin, mult, _lib.ptr(work), cap, _lib.ptr(count), stream),
+               "hsg_rel_work")
+    return work, count
 
 
 def build_relation(kind, src, dst, unit, tffrac=None, edtype=None):
@@ -145,7 +175,27 @@ def build_relation(kind, src, dst, unit, tffrac=None, edtype=None):
     d = dict(src_nodes=src_nodes[:n_src], dst_nodes=dst_nodes[:n_dst], indptr=indptr[:n_dst + 1],
              src=esrc[:n_typed], tf=tf[:n_typed], eid=eid[:n_typed], phantom=phantom[:n_dst],
              cindptr=cindptr[:n_src + 1], cdst=cdst[:n_typed], cperm=cperm[:n_typed])
+    attach_work_lists(d, n_src, n_dst, n_typed)
     return Relation.on_device(kind, n_src, n_dst, d, E)
+
+
+def attach_work_lists(d, n_src, n_dst, n_typed):
+    """Add the CSR / CSC work lists (``dwork`` / ``swork``) of a relation's device arrays
+    ``d`` when some segment is long enough to be split (hsg_rel_work)."""
+    from . import _lib
+    lib = _lib.load()
+    dev = d["indptr"].device
+    with torch.cuda.device(dev):
+        st = _lib.stream_of(d["indptr"])
+        dw, dc = _work_list(lib, n_dst, d["indptr"], n_typed, st)
+        sw, sc = _work_list(lib, n_src, d["cindptr"], n_typed, st)
+        cs = [c for c in (dc, sc) if c is not None]
+        got = iter(torch.cat(cs).tolist() if cs else [])                 # one readback per batch
+        cnt = [next(got) if c is not None else 0 for c in (dc, sc)]
+    if cnt[0] > 0:
+        d["dwork"] = dw[:cnt[0]]
+    if cnt[1] > 0:
+        d["swork"] = sw[:cnt[1]]
 
 
 def _structure(g):

@@ -44,6 +44,16 @@ typedef struct hsg_rel {
     const int32_t *cindptr;   /* [n_src+1] CSC by source rank                       */
     const int32_t *cdst;      /* [E_T]     destination rank per CSC edge            */
     const int32_t *cperm;     /* [E_T]     CSR position of each CSC edge            */
+    /* Work lists for degree-skewed relations (round 6; hsg_rel_work): 0 / NULL = none.
+     * Items in node order, [n][3] = (node, beg, end): node >= 0 is a whole node, node =
+     * -(v + 1) one piece [beg, end) of a long segment of node v (the HDSG doc supernodes'
+     * ~250 word edges, dataloader.py:387-400, next to ~20 per sentence).  dwork splits
+     * the CSR (destinations: hsg_gat_fwd_ws), swork the CSC (sources:
+     * hsg_gat_bwd_src_g_ws); the pieces' partial results are merged in a fixed order. */
+    int32_t n_dwork;          /* items of dwork (0: no CSR work list)               */
+    int32_t n_swork;          /* items of swork (0: no CSC work list)               */
+    const int32_t *dwork;     /* [n_dwork][3]                                        */
+    const int32_t *swork;     /* [n_swork][3]                                        */
 } hsg_rel;
 
 /* tau addressing: HSG_TAU_TABLE -> tau is [11, H] indexed by rel->tf (tf-idf box
@@ -66,6 +76,17 @@ typedef struct hsg_rel {
 int hsg_gat_fwd(const hsg_rel *rel, int H, int D, int tau_mode, float slope,
                 const float *Z, const float *sigma, const float *tau, const float *origin,
                 float *h, float *out, float *m, float *l, void *stream);
+/* hsg_gat_fwd with the relation's CSR work list (round 6): a destination whose typed
+ * in-edges exceed the list's piece length is aggregated as pieces -- (max, sum, partial
+ * h) per piece written to ws, then merged with its phantoms in piece order by a second
+ * launch (the same online-softmax algebra; deterministic).  ws holds
+ * hsg_gat_fwd_ws_floats(rel, H, D) floats (0: no work list, ws may be NULL and the call
+ * equals hsg_gat_fwd).  Multi-wave (long-segment) forward only; other shapes ignore the
+ * list. */
+size_t hsg_gat_fwd_ws_floats(const hsg_rel *rel, int H, int D);
+int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                   const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                   float *l, float *ws, void *stream);
 
 /* Backward, destination-centric half: given dOut, computes
  *   G = origin_mode ? dOut * elu'(h) : dOut                      [n_dst, H*D]
@@ -137,6 +158,17 @@ int hsg_gat_bwd_src_g_io(const hsg_rel *rel, int H, int D, float slope, const fl
                          const float *m, const float *l, const void *G, int g_bf16, const float *rho, int rho_groups,
                          const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
                          float *dtau_part, void *stream);
+/* hsg_gat_bwd_src_g_io with the relation's CSC work list (round 6): a source whose
+ * out-edges exceed the piece length is walked as pieces (one block each), their dZ
+ * and dsigma partials written to ws and summed in piece order by a second launch, which
+ * adds dsigma * a1 (da1 / dtau partials stay per block).  ws holds
+ * hsg_gat_bwd_src_g_ws_floats(rel, H, D) floats (0: no work list; the call equals
+ * hsg_gat_bwd_src_g_io).  Wide heads only; the narrow head-lane kernel ignores the list. */
+size_t hsg_gat_bwd_src_g_ws_floats(const hsg_rel *rel, int H, int D);
+int hsg_gat_bwd_src_g_ws(const hsg_rel *rel, int H, int D, float slope, const float *sigma, const float *tau,
+                         const float *m, const float *l, const void *G, int g_bf16, const float *rho, int rho_groups,
+                         const float *a1, const float *Z, float *dZ, float *dsigma, float *da1_part,
+                         float *dtau_part, float *ws, void *stream);
 
 /* Measurement hook (bench.py's in-step kernel clock; not part of the reference
  * surface): the next hsg_gat_fwd launched FROM THE CALLING THREAD ON `stream` records
@@ -556,6 +588,15 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
  *   cindptr [n+1] (first n_src+1), cdst/cperm [E], src_nodes/dst_nodes [n] int64.
  * CSR edges of one destination keep edge-id order (the DGL mailbox order); CSC edges of
  * one source keep CSR order.  workspace >= hsg_rel_build_workspace_bytes(n, E). */
+/* Work list of one CSR / CSC (round 6, hsg_rel.dwork / swork): with mean segment m =
+ * indptr[n] / n, the piece length is P = max(min_len, mult * ceil(m)); a node with more
+ * than P edges becomes ceil(deg / P) near-equal pieces, every other node one item, in
+ * node order.  work holds max_items >= n + 2 * indptr[n] / min_len + 1 items of 3
+ * int32; *count receives the item count, or 0 when no node is longer than P (then the
+ * kernels walk the nodes as before).  min_len <= 0: *count = 0.  One block; once per
+ * batch (the relation build). */
+int hsg_rel_work(int n, const int32_t *indptr, int min_len, int mult, int32_t *work, int max_items,
+                 int32_t *count, void *stream);
 size_t hsg_rel_build_workspace_bytes(int n_nodes, int n_edges);
 int hsg_rel_build(float src_unit, float dst_unit, int n_nodes, int n_edges, const int64_t *src,
                   const int64_t *dst, const float *unit, const int64_t *tffrac, const float *edtype,

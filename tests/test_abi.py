@@ -35,9 +35,11 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_layout():
     from hetersumgraph_amd._lib import HsgRel
-    # 3 x int32 + pad to 8 + 7 pointers (x86-64 SysV)
-    assert ctypes.sizeof(HsgRel) == 16 + 7 * 8
+    # 3 x int32 + pad to 8 + 7 pointers, then the work lists (round 6): 2 x int32 + 2
+    # pointers (x86-64 SysV)
+    assert ctypes.sizeof(HsgRel) == 16 + 7 * 8 + 8 + 2 * 8
     assert HsgRel.indptr.offset == 16
+    assert HsgRel.n_dwork.offset == 72 and HsgRel.dwork.offset == 80 and HsgRel.swork.offset == 88
 
 
 def test_code_object_is_gfx950():
