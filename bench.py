@@ -129,6 +129,13 @@ def cpu_model():
     return platform.processor()
 
 
+def model_name(config):
+    """The reference model the config's batch feeds: HSumDocGraph for the HDSG
+    (doc-node) batch of config 4 (HiGraph.py:166-244), HSumGraph otherwise."""
+    from hetersumgraph_amd import synth
+    return "HDSG" if synth.CONFIGS[config][0] == "hdsg" else "HSG"
+
+
 def workload_shape(config):
     from hetersumgraph_amd import synth
     kind, per_gpu, p = synth.CONFIGS[config]
@@ -736,8 +743,8 @@ def main(backend_cls=HipBench):
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": be.data,
-        "config": {"workload": f"{args.config}: HSG WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) fwd+bwd, "
-                               f"train mode, {workload_shape(args.config)}",
+        "config": {"workload": f"{args.config}: {model_name(args.config)} WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) "
+                               f"fwd+bwd, train mode, {workload_shape(args.config)}",
                    "gemm_operands": args.dtype,
                    "bf16_rows": ("wide (S2W) FFN hidden H, its output y (LayerNorm input), dY, dH and the "
                                  "edge gate G rows; one RNE rounding each, GEMM operands rounded anyway"

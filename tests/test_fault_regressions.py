@@ -3,10 +3,10 @@ and the host-side guards that came with them.  CPU only: each checks the host co
 that sized or chose a device buffer, so the pre-fix code fails here without touching
 a GPU.
 
-* gpurun_out/r05f: hipErrorIllegalAddress in test_dw_pair_bf16_operands_bitwise --
+* profiles/r05_faults/r05f_pytest.log (gpurun_out/r05f): hipErrorIllegalAddress in test_dw_pair_bf16_operands_bitwise --
   the k_dw partial slabs (fp32 stores) were allocated with a bf16 operand's
   ``new_empty``: half the bytes;
-* gpurun_out/r05j: abort in the cfg5-bf16 stack backward -- the rho partials of the dx
+* profiles/r05_faults/r05j_pytest.log (gpurun_out/r05j): abort in the cfg5-bf16 stack backward -- the rho partials of the dx
   GEMM's ELU-gate epilogue (fp32 stores) were allocated with the bf16 G rows'
   ``new_empty``: half the bytes.
 """
