@@ -1190,7 +1190,17 @@ __global__ __launch_bounds__(256) void k_hproj_bwd_hw(int n, int in, int H, int 
 // and runs 6 MFMAs.
 // kDwMfP: image row pitch (bf16).  40 (80 B): fragment reads 2-way, staging writes
 // conflict-free; 48 (96 B): reads conflict-free, writes 2-way (tools/lds_banks.py-style
-// check over gfx950's ds_read_b128 lane groups)
+// check over gfx950's ds_read_b128 lane groups).  32 (round 6, the default): unpadded
+// 64-B rows of four 16-B slots (8 rows of K each), slot s of row r stored at s ^ ((r >> 1)
+// & 3): the staging ds_write_b128 (8 contiguous lanes = 8 rows, one slot: banks mod 32)
+// and both fragment reads (ds_read_b128 lane groups of 4 + 4 + 8 lanes = 8 rows x 2
+// slots: banks mod 64) all land on distinct 4-bank groups (tools/lds_banks.py dwmf)
+template <int kDwMfP>
+__device__ __forceinline__ int dwmf_off(int r, int slot) {
+    if constexpr (kDwMfP == 32) return r * 32 + 8 * (slot ^ ((r >> 1) & 3));
+    else return r * kDwMfP + 8 * slot;
+}
+
 template <int kDwMfP>
 __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, int rows_per_chunk,
                                                        const float *__restrict__ dZ, int ldz,
@@ -1248,7 +1258,7 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             hsg_split_rne_pair(vz[2 * q], vz[2 * q + 1], a, bb, c);
             z0[q] = a; z1[q] = bb; z2[q] = c;
         }
-        const int o = sc * kDwMfP + 8 * sr;
+        const int o = dwmf_off<kDwMfP>(sc, sr);
         *reinterpret_cast<hsg_u32x4_t *>(&sX[b][0][o]) = x0;
         *reinterpret_cast<hsg_u32x4_t *>(&sX[b][1][o]) = x1;
         *reinterpret_cast<hsg_u32x4_t *>(&sX[b][2][o]) = x2;
@@ -1262,8 +1272,8 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
 #pragma unroll
     for (int k = 0; k < HM; ++k) acc[k] = f32x4v{0.f, 0.f, 0.f, 0.f};
     const int cl = lane & 15, ig = lane >> 4;
-    const int xo = (16 * w + cl) * kDwMfP + 8 * ig;               // B fragment: column 16w + cl, rows 8 ig ..
-    const int zo = (cl & 7) * kDwMfP + 8 * ig;                    // A fragment: output k*8 + (cl & 7)
+    const int xo = dwmf_off<kDwMfP>(16 * w + cl, ig);             // B fragment: column 16w + cl, rows 8 ig ..
+    const int zo = dwmf_off<kDwMfP>(cl & 7, ig);                  // A fragment: output k*8 + (cl & 7)
     if (rb < rend) gload(rb, vxs[0], vzs[0], vms[0]);
     if (rb + 32 < rend) gload(rb + 32, vxs[1], vzs[1], vms[1]);
     auto step = [&](int r0, int b) {                             // b = step parity (compile-time below)
@@ -1287,7 +1297,8 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             hsg_bf16x8_t az[3];
 #pragma unroll
             for (int l = 0; l < 3; ++l)
-                az[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sZ[b][l][k * 8 * kDwMfP + zo]);
+                az[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sZ[b][l][k * 8 * kDwMfP + zo]);  // (r >> 1) & 3 of
+                                                                  // row k*8 + c: that of c
             const hsg_bf16x8_t b0 = __builtin_bit_cast(hsg_bf16x8_t, bx[0] & M);
             const hsg_bf16x8_t b1 = __builtin_bit_cast(hsg_bf16x8_t, bx[1] & M);
             const hsg_bf16x8_t b2 = __builtin_bit_cast(hsg_bf16x8_t, bx[2] & M);
@@ -1816,9 +1827,12 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
         if (pe && atoi(pe) == 48)
             hipLaunchKernelGGL(k_hproj_dw_mf<48>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
                                ldz, X, ldx, bits, part);
+        else if (pe && atoi(pe) == 40)
+            hipLaunchKernelGGL(k_hproj_dw_mf<40>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
+                               ldz, X, ldx, bits, part);
         else
 #endif
-            hipLaunchKernelGGL(k_hproj_dw_mf<40>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
+            hipLaunchKernelGGL(k_hproj_dw_mf<32>, dim3((in + 63) / 64, g.chunks), dim3(256), 0, st, n, in, H, g.rows, dZ,
                                ldz, X, ldx, bits, part);
         if (int rc = status()) return rc;
         if (!dW) return 0;

@@ -66,6 +66,39 @@ def gemm5_b():
             for j in range(2) for s16 in range(2)]
 
 
+G128W = [list(range(i, i + 8)) for i in range(0, 64, 8)]       # ds_write_b128: 8 x 8 contiguous, banks mod 32
+
+
+def extra_write_cycles(addr):
+    """addr(lane) -> first dword of a ds_write_b128; extra LDS-array cycles (banks mod 32)."""
+    ex = 0
+    for g in G128W:
+        banks = {}
+        for lane in g:
+            for d in range(4):
+                b = (addr(lane) + d) % 32
+                banks[b] = banks.get(b, 0) + 1
+        ex += max(banks.values()) - 1
+    return ex
+
+
+def dwmf_off(p, r, slot):
+    """k_hproj_dw_mf image offset in dwords: pitch p bf16 (32 = the swizzled form)."""
+    if p == 32:
+        return (r * 32 + 8 * (slot ^ ((r >> 1) & 3))) // 2
+    return (r * p + 8 * slot) // 2
+
+
+def dwmf(p):
+    """k_hproj_dw_mf: the staging writes (lane = column / output row, slot = the wave's
+    8-row group), the B fragment reads (column 16 w + (l & 15), slot l >> 4) and the A
+    fragment reads (output 8 k + (l & 7), slot l >> 4)."""
+    writes = [extra_write_cycles(lambda l: dwmf_off(p, l, sr)) for sr in range(4)]
+    reads = [extra_cycles(lambda l: dwmf_off(p, 16 * w + (l & 15), l >> 4)) for w in range(4)]
+    reads += [extra_cycles(lambda l: dwmf_off(p, 8 * k + (l & 7), l >> 4)) for k in range(8)]
+    return writes, reads
+
+
 def main():
     rows = [
         ("k_gemm7 A, round-4 swz", gemm7_a(swz)),
@@ -77,6 +110,10 @@ def main():
     ]
     for name, ex in rows:
         print(f"{name:32s} reads {len(ex):3d}  extra LDS cycles per read {sum(ex) / len(ex):.2f}")
+    for p in (40, 48, 32):
+        w, r = dwmf(p)
+        print(f"k_hproj_dw_mf pitch {p:2d}{' (swizzled)' if p == 32 else '           '}   "
+              f"writes: extra {sum(w) / len(w):.2f} / instr   reads: extra {sum(r) / len(r):.2f} / instr")
 
 
 if __name__ == "__main__":
