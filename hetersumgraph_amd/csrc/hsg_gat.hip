@@ -450,7 +450,25 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
 // of its pieces in item order with its phantoms, exactly the online-softmax algebra of
 // a whole destination: M = max(max_p m_p, 0 if c > 0), L = sum_p l_p e^(m_p - M) +
 // c e^(-M), h = sum_p (l_p e^(m_p - M) / L) h_p, then elu(h) + origin and (m, l) = (M,
-// L).  Lane = feature (flat mapping, as k_gat_fwd); deterministic.
+// L).  Lane = feature (flat mapping, as k_gat_fwd); the piece count comes from one
+// ballot over the next 64 items, and the partials of kMergeBatch pieces are requested
+// together (one round trip per batch, not one per piece); deterministic.
+constexpr int kMergeBatch = 8;
+
+__device__ __forceinline__ int piece_count(const int32_t *__restrict__ work, int n_work, int item, int code,
+                                           int lane) {
+    int np = 1;
+    for (int base = item + 1;; base += 64) {
+        const int j = base + lane;
+        const unsigned long long same = __ballot(j < n_work && work[3 * j] == code);
+        if (~same == 0ull) {
+            np += 64;
+            continue;
+        }
+        return np + __builtin_ctzll(~same);        // the run of equal codes after this item
+    }
+}
+
 template <int NF>
 __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, const float *__restrict__ origin,
                                                        const float *__restrict__ pws, float *__restrict__ hout,
@@ -461,42 +479,84 @@ __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, 
     if (item >= R.n_dwork) return;
     const int code = R.dwork[3 * item];
     if (code >= 0 || (item > 0 && R.dwork[3 * (item - 1)] == code)) return;   // not a first piece
-    int last = item + 1;
-    while (last < R.n_dwork && R.dwork[3 * last] == code) ++last;
+    const int np = __builtin_amdgcn_readfirstlane(piece_count(R.dwork, R.n_dwork, item, code, lane));
     const int v = -code - 1, HD = H * D, W = HD + 2 * H;
     const float c = (float)R.phantom[v];
     const float *pw = pws + (size_t)item * W;
-    const int np = last - item;
-    // per head (lanes k < H, then the features' heads): M and L
-    auto head_ml = [&](int k, float &M, float &L) {
-        M = c > 0.f ? 0.f : -INFINITY;
-        for (int p = 0; p < np; ++p) M = fmaxf(M, pw[p * W + HD + k]);
-        L = c > 0.f ? c * __expf(-M) : 0.f;
-        for (int p = 0; p < np; ++p) L += pw[p * W + HD + H + k] * __expf(pw[p * W + HD + k] - M);
-    };
-    if (lane < H) {
-        float M, L;
-        head_ml(lane, M, L);
-        mout[v * H + lane] = M;
-        lout[v * H + lane] = L;
+    // per feature i (head k_i = f / D; lanes past HD take head 0 and store nothing):
+    // running max M, denominator L and weighted sum S, batch by batch
+    int kf[NF];
+    float M[NF], L[NF], S[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        kf[i] = f < HD ? f / D : 0;
+        M[i] = c > 0.f ? 0.f : -INFINITY;
+        L[i] = c > 0.f ? c : 0.f;                     // c e^(0 - M) with M = 0
+        S[i] = 0.f;
+    }
+    for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
+        float mv[NF][kMergeBatch], lv[NF][kMergeBatch], hv[NF][kMergeBatch];
+#pragma unroll
+        for (int j = 0; j < kMergeBatch; ++j) {
+            const int p = min(p0 + j, np - 1);          // clamped: weight 0 below
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                const int f = min(lane + 64 * i, HD - 1);
+                mv[i][j] = pw[p * W + HD + kf[i]];
+                lv[i][j] = pw[p * W + HD + H + kf[i]];
+                hv[i][j] = pw[p * W + f];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            float mb = M[i];
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j)
+                if (p0 + j < np) mb = fmaxf(mb, mv[i][j]);
+            const float sc = M[i] == -INFINITY ? 0.f : __expf(M[i] - mb);
+            L[i] *= sc;
+            S[i] *= sc;
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                if (p0 + j < np) {
+                    const float w = lv[i][j] * __expf(mv[i][j] - mb);
+                    L[i] += w;
+                    S[i] = fmaf(w, hv[i][j], S[i]);
+                }
+            }
+            M[i] = mb;
+        }
     }
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
         const int f = lane + 64 * i;
         if (f < HD) {
-            const int k = f / D;
-            float M, L;
-            head_ml(k, M, L);
-            const float inv = 1.f / L;
-            float h = 0.f;
-            for (int p = 0; p < np; ++p)
-                h = fmaf(pw[p * W + HD + H + k] * __expf(pw[p * W + HD + k] - M) * inv, pw[p * W + f], h);
+            const float h = S[i] / L[i];
             const size_t o = (size_t)v * HD + f;
             if (hout) hout[o] = h;
             if (origin) out[o] = elu1(h) + origin[o];
+            if (f == kf[i] * D) {                         // the head's first feature: its (m, l)
+                mout[v * H + kf[i]] = M[i];
+                lout[v * H + kf[i]] = L[i];
+            }
         }
     }
 }
+
+#ifdef HSG_DEV
+// Launch floor probe (dev, round 6): the same grid as the edge launch
+// it replaces, every wave reads its first index word and stores nothing, so the step
+// trace shows what dispatch, ramp and drain of that grid cost in the step.
+__global__ __launch_bounds__(256) void k_launch_floor(const int32_t *__restrict__ p, int n, int32_t *__restrict__ sink) {
+    const int i = (int)blockIdx.x;
+    if (i < n && p[i] == -0x7fffffff && sink) sink[0] = i;      // never true: no store
+}
+int launch_floor_mode() {
+    const char *e = HSG_DEV_ENV("HSG_GAT_FLOOR");               // 1: W2S forward, 2: W2S backward
+    return e ? atoi(e) : 0;
+}
+#endif
 
 // ------------------------------------------------ forward, single pass (round 5) ----
 // Narrow rows (H * D <= 64: the W2S sentence destinations, ~36 word in-edges each at
@@ -1710,7 +1770,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
 
 // Merge of the pieces of long sources (round 6; after k_gat_bwd_src_g with a CSC work
 // list).  One wave per work item; the wave of a source's FIRST piece sums its pieces'
-// partials in item order: dsigma_u,k = sum_p ds_p,k, dZ_u = sum_p dZ_p + dsigma_u * a1.
+// partials in item order: dsigma_u,k = sum_p ds_p,k, dZ_u = sum_p dZ_p + dsigma_u * a1
+// (the partials of kMergeBatch pieces requested together).
 template <int NF>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_g_merge(RelPtrs R, int H, int D, const float *__restrict__ pws,
                                                              const float *__restrict__ a1, float *__restrict__ dZ,
@@ -1720,24 +1781,44 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_g_merge(RelPtrs R, int H, i
     if (item >= R.n_swork) return;
     const int code = R.swork[3 * item];
     if (code >= 0 || (item > 0 && R.swork[3 * (item - 1)] == code)) return;   // not a first piece
-    int last = item + 1;
-    while (last < R.n_swork && R.swork[3 * last] == code) ++last;
-    const int u = -code - 1, HD = H * D, W = HD + H, np = last - item;
+    const int np = __builtin_amdgcn_readfirstlane(piece_count(R.swork, R.n_swork, item, code, lane));
+    const int u = -code - 1, HD = H * D, W = HD + H;
     const float *pw = pws + (size_t)item * W;
-    auto head_ds = [&](int k) {
-        float ds = 0.f;
-        for (int p = 0; p < np; ++p) ds += pw[p * W + HD + k];
-        return ds;
-    };
-    if (dsigma && lane < H) dsigma[u * H + lane] = head_ds(lane);
+    int kf[NF];
+    float A[NF], DS[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        kf[i] = f < HD ? f / D : 0;
+        A[i] = 0.f;
+        DS[i] = 0.f;
+    }
+    for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
+        float av[NF][kMergeBatch], dv[NF][kMergeBatch];
+#pragma unroll
+        for (int j = 0; j < kMergeBatch; ++j) {
+            const int p = min(p0 + j, np - 1);
+#pragma unroll
+            for (int i = 0; i < NF; ++i) {
+                av[i][j] = pw[p * W + min(lane + 64 * i, HD - 1)];
+                dv[i][j] = pw[p * W + HD + kf[i]];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i)
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j)
+                if (p0 + j < np) {
+                    A[i] += av[i][j];
+                    DS[i] += dv[i][j];
+                }
+    }
 #pragma unroll
     for (int i = 0; i < NF; ++i) {
         const int f = lane + 64 * i;
         if (f < HD) {
-            float a = 0.f;
-            for (int p = 0; p < np; ++p) a += pw[p * W + f];
-            if (a1) a = fmaf(head_ds(f / D), a1[f], a);
-            dZ[(size_t)u * HD + f] = a;
+            dZ[(size_t)u * HD + f] = a1 ? fmaf(DS[i], a1[f], A[i]) : A[i];
+            if (dsigma && f == kf[i] * D) dsigma[u * H + kf[i]] = DS[i];
         }
     }
 }
@@ -2290,6 +2371,13 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
 #endif
     const int nf = (H * D + 63) / 64;
     const int wpn = dst_wpn(rel);
+#ifdef HSG_DEV
+    if (launch_floor_mode() == 1 && wpn == 4 && nf == 1) {      // dev probe: the W2S forward's grid, no work
+        HSG_KLAUNCH(true, true, k_launch_floor, dim3(grid_nodes(rel->n_dst, 4, kFwdGridCap)), dim3(256), st,
+                    rel->indptr, rel->n_dst, (int32_t *)nullptr);
+        return launch_status();
+    }
+#endif
     if (nf == 1 && fwd_sp() && tau_mode == HSG_TAU_TABLE &&
         (long)rel->n_src * H * D * 4 < 0x7fffffffL) {  // narrow rows: one single-pass wave per destination
         const dim3 g(grid_nodes(rel->n_dst, 1, kFwdGridCap));
@@ -2651,6 +2739,12 @@ int hsg_gat_bwd_src_g_ws(const hsg_rel *rel, int H, int D, float slope, const fl
                 return HSG_EINVAL;
             return (int)hipMemsetAsync(dtau_part, 0, sizeof(float) * HSG_NT * H * grid.x, st);
         }
+#ifdef HSG_DEV
+        if (launch_floor_mode() == 2) {                         // dev probe: the W2S backward's grid, no work
+            HSG_KLAUNCH(true, true, k_launch_floor, grid, dim3(256), st, rel->cindptr, rel->n_src, (int32_t *)nullptr);
+            return launch_status();
+        }
+#endif
         HSG_KLAUNCH(true, true, (k_gat_bwd_src_hl<8, HSG_TAU_TABLE, true>), grid, dim3(256), st, R, H, D,
                     next_pow2(H), slope, sigma, tau, m, l, G, nullptr, a1, Z, dZ, dsigma, da1_part, rho, dtau_part);
         return launch_status();

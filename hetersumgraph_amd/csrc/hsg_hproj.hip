@@ -780,15 +780,14 @@ __device__ __forceinline__ float cvt_ubyte(uint32_t y) {
 }
 
 template <int HH, int HG, bool SPREAD = true>
-__global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const float *__restrict__ dZ, int ldz,
-                                                     const float *__restrict__ W,
-                                                     const uint32_t *__restrict__ bits, float scale,
-                                                     float *__restrict__ dX, int ldx, int accumulate) {
+__device__ __forceinline__ void hproj_dx_n8_tile(int task, int n, int in, int H, const float *__restrict__ dZ,
+                                                 int ldz, const float *__restrict__ W,
+                                                 const uint32_t *__restrict__ bits, float scale,
+                                                 float *__restrict__ dX, int ldx, int accumulate) {
     constexpr int D = 8;
     typedef float f32x2v __attribute__((ext_vector_type(2)));
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int nct = (in + 63) / 64;
-    const int task = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int rt = task / nct, ctile = task - rt * nct;
     const int i0 = rt * 16;
     if (i0 >= n) return;
@@ -867,6 +866,15 @@ __global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const
         if (accumulate) v += *o;
         *o = v;
     }
+}
+
+template <int HH, int HG, bool SPREAD = true>
+__global__ __launch_bounds__(256) void k_hproj_dx_n8(int n, int in, int H, const float *__restrict__ dZ, int ldz,
+                                                     const float *__restrict__ W,
+                                                     const uint32_t *__restrict__ bits, float scale,
+                                                     float *__restrict__ dX, int ldx, int accumulate) {
+    hproj_dx_n8_tile<HH, HG, SPREAD>((int)(blockIdx.x * 4 + (threadIdx.x >> 6)), n, in, H, dZ, ldz, W, bits, scale,
+                                     dX, ldx, accumulate);
 }
 
 // dX with one wave per head (wide heads, e.g. S2W: H = 6, D = 50, few rows): block =
@@ -1201,23 +1209,26 @@ __device__ __forceinline__ int dwmf_off(int r, int slot) {
     else return r * kDwMfP + 8 * slot;
 }
 
-template <int kDwMfP>
-__global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, int rows_per_chunk,
-                                                       const float *__restrict__ dZ, int ldz,
-                                                       const float *__restrict__ X, int ldx,
-                                                       const uint32_t *__restrict__ bits, float *__restrict__ part) {
+// NB: LDS image buffers (2: double-buffered, the launch of its own; 1: the merged W2S
+// backward k_hproj_bwd_n8, whose dX blocks need the CU's LDS for occupancy -- one more
+// barrier per step, 26.6 instead of 53 KB).  bl / ctiles / chunks: the logical block
+// and grid (the merged kernel's dW blocks follow its dX blocks).
+template <int kDwMfP, int NB = 2>
+__device__ __forceinline__ void hproj_dw_mf_block(int bl, int ctiles, int chunks, int n, int in, int H,
+                                                  int rows_per_chunk, const float *__restrict__ dZ, int ldz,
+                                                  const float *__restrict__ X, int ldx,
+                                                  const uint32_t *__restrict__ bits, float *__restrict__ part) {
     constexpr int HM = 8;
-    __shared__ __attribute__((aligned(16))) __bf16 sX[2][3][64 * kDwMfP];    // X limbs [column][row]
-    __shared__ __attribute__((aligned(16))) __bf16 sZ[2][3][64 * kDwMfP];    // dZ limbs [output][row]
-    __shared__ uint32_t sM[2][HM][64];                                       // keep words [head][column]
+    __shared__ __attribute__((aligned(16))) __bf16 sX[NB][3][64 * kDwMfP];   // X limbs [column][row]
+    __shared__ __attribute__((aligned(16))) __bf16 sZ[NB][3][64 * kDwMfP];   // dZ limbs [output][row]
+    __shared__ uint32_t sM[NB][HM][64];                                      // keep words [head][column]
     const int NWI = (n + 31) / 32, LDC = mask_ldc(in);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     // XCD-aware order: workgroup b runs on XCD b % 8, so logical block L = xcd_order(b)
     // puts the column tiles of one row chunk on one XCD and their dZ rows (re-read by
     // every column tile) come from its L2 instead of HBM
-    const int ctiles = (int)gridDim.x, total = ctiles * (int)gridDim.y;
-    const int bl = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+    const int total = ctiles * chunks;
     const int L = (bl & 7) * (total >> 3) + min(bl & 7, total & 7) + (bl >> 3);     // a bijection
     const int chunk = L / ctiles;
     const int c0 = (L % ctiles) * 64;
@@ -1277,19 +1288,24 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
     if (rb < rend) gload(rb, vxs[0], vzs[0], vms[0]);
     if (rb + 32 < rend) gload(rb + 32, vxs[1], vzs[1], vms[1]);
     auto step = [&](int r0, int b) {                             // b = step parity (compile-time below)
-        lstore(b, vxs[b], vzs[b], vms[b]);
+        constexpr int ib = 0;                                     // (NB == 1: the one image)
+        const int bi = NB == 1 ? ib : b;
+        if constexpr (NB == 1) {
+            if (r0 != rb) __syncthreads();                        // every wave done with the last step's image
+        }
+        lstore(bi, vxs[b], vzs[b], vms[b]);
         __syncthreads();
         if (r0 + 64 < rend) gload(r0 + 64, vxs[b], vzs[b], vms[b]);
         hsg_u32x4_t bx[3];
 #pragma unroll
-        for (int l = 0; l < 3; ++l) bx[l] = *reinterpret_cast<const hsg_u32x4_t *>(&sX[b][l][xo]);
+        for (int l = 0; l < 3; ++l) bx[l] = *reinterpret_cast<const hsg_u32x4_t *>(&sX[bi][l][xo]);
 #pragma unroll
         for (int k = 0; k < HM; ++k) {
             if (k >= H) break;                                    // wave-uniform
             // the lane's 8 rows are bits 8 ig .. 8 ig + 7 of the word: pair q's mask from
             // bits 2q / 2q + 1 shifted to 15 / 31 and v_perm_b32's sign-byte selectors (a
             // 256-entry LDS table here cost 2.3e6 bank-conflict cycles per launch: random rows)
-            const uint32_t x = sM[b][k][16 * w + cl] >> (8 * ig);
+            const uint32_t x = sM[bi][k][16 * w + cl] >> (8 * ig);
             hsg_u32x4_t M;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
@@ -1297,7 +1313,7 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             hsg_bf16x8_t az[3];
 #pragma unroll
             for (int l = 0; l < 3; ++l)
-                az[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sZ[b][l][k * 8 * kDwMfP + zo]);  // (r >> 1) & 3 of
+                az[l] = *reinterpret_cast<const hsg_bf16x8_t *>(&sZ[bi][l][k * 8 * kDwMfP + zo]);  // (r >> 1) & 3 of
                                                                   // row k*8 + c: that of c
             const hsg_bf16x8_t b0 = __builtin_bit_cast(hsg_bf16x8_t, bx[0] & M);
             const hsg_bf16x8_t b1 = __builtin_bit_cast(hsg_bf16x8_t, bx[1] & M);
@@ -1326,6 +1342,35 @@ __global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, in
             for (int e = 0; e < 4; ++e) dst[(size_t)(k * 8 + 4 * ig + e) * in] = acc[k][e];
         }
     }
+}
+
+template <int kDwMfP>
+__global__ __launch_bounds__(256, 2) void k_hproj_dw_mf(int n, int in, int H, int rows_per_chunk,
+                                                       const float *__restrict__ dZ, int ldz,
+                                                       const float *__restrict__ X, int ldx,
+                                                       const uint32_t *__restrict__ bits, float *__restrict__ part) {
+    hproj_dw_mf_block<kDwMfP>((int)(blockIdx.y * gridDim.x + blockIdx.x), (int)gridDim.x, (int)gridDim.y, n, in, H,
+                              rows_per_chunk, dZ, ldz, X, ldx, bits, part);
+}
+
+// The narrow-head (W2S) backward of one projection in ONE launch (round 6): blocks [0,
+// dx_blocks) are k_hproj_dx_n8 tiles (4 waves = 4 tasks each), the rest k_hproj_dw_mf
+// blocks on a single LDS image (NB = 1), the same row chunks and partial slabs -- dX
+// and the slabs are bitwise those of the two launches.  The dX tiles (~1,500 blocks of
+// short chains) and the dW blocks (500 blocks of six 32-row steps) were two latency-bound
+// launches back to back; here the dW blocks run beside the dX tiles.
+__global__ __launch_bounds__(256) void k_hproj_bwd_n8(int n, int in, int H, const float *__restrict__ dZ, int ldz,
+                                                     const float *__restrict__ W, const uint32_t *__restrict__ bits,
+                                                     float scale, float *__restrict__ dX, int ldxo, int accumulate,
+                                                     const float *__restrict__ X, int ldx, int rows_per_chunk,
+                                                     float *__restrict__ part, int dx_blocks, int ctiles, int chunks) {
+    const int b = (int)blockIdx.x;
+    if (b < dx_blocks) {
+        hproj_dx_n8_tile<8, 2>(b * 4 + (int)(threadIdx.x >> 6), n, in, H, dZ, ldz, W, bits, scale, dX, ldxo,
+                               accumulate);
+        return;
+    }
+    hproj_dw_mf_block<32, 1>(b - dx_blocks, ctiles, chunks, n, in, H, rows_per_chunk, dZ, ldz, X, ldx, bits, part);
 }
 
 // ------------------------------------------------- dW, narrow heads, 4x4x1 ----
@@ -1785,6 +1830,21 @@ int hsg_hproj_bwd(int n, int in, int H, int D, const float *dZ, int ldz, const f
                      aligned16(dZ);
     const bool merge = (!me || atoi(me) != 0) && (!pe || atoi(pe) == 1) && wide < 2048 && H <= 16 && D <= 64 &&
                        !dw_mf_shape(in, H, D) && !dw_m4_shape(in, H, D) && dw_slots() == 4 && !vec;
+    // the narrow-head (W2S) pair in one launch (round 6): where the two-launch path would
+    // run k_hproj_dx_n8 and k_hproj_dw_mf; dev A/B: HSG_HPROJ_BWD_N8=0
+    const char *ne = HSG_DEV_ENV("HSG_HPROJ_BWD_N8");
+    const bool merge_n8 = (!ne || atoi(ne) != 0) && (!me || atoi(me) != 0) && (!pe || atoi(pe) == 1) &&
+                          wide >= 2048 && H <= 8 && D == 8 && in % 4 == 0 && ldxo % 4 == 0 && ldz % 2 == 0 &&
+                          aligned16(dX) && ((uintptr_t)dZ & 7) == 0 && aligned16(W) && dw_mf_shape(in, H, D) &&
+                          !HSG_DEV_ENV("HSG_HPROJ_DX_SEL") && !HSG_DEV_ENV("HSG_HPROJ_DWMF_P");
+    if (merge_n8) {
+        const DwGeom g = dw_geom(n, in, H, D);
+        const int ctiles = (in + 63) / 64, dx_blocks = (int)((wide + 3) / 4);
+        const unsigned total = (unsigned)(dx_blocks + ctiles * g.chunks);
+        hipLaunchKernelGGL(k_hproj_bwd_n8, dim3(total), dim3(256), 0, (hipStream_t)stream, n, in, H, dZ, ldz, W, bits,
+                           drop_scale(p), dX, ldxo, accumulate, X, ldx, g.rows, part, dx_blocks, ctiles, g.chunks);
+        return status();
+    }
     if (!merge) {
         int rc = hsg_hproj_dx(n, in, H, D, dZ, ldz, W, bits, p, dX, ldxo, accumulate, stream);
         if (rc) return rc;

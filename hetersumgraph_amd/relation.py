@@ -103,9 +103,11 @@ class Relation:
 # longer than P = max(PIECE_MIN, PIECE_MULT * ceil(mean segment)) is walked as near-equal
 # pieces, so the HDSG doc supernodes (~250 word edges each, dataloader.py:387-400, next
 # to ~20 per sentence) no longer set the edge kernels' critical path.  cfg2 / cfg5 have
-# no such node (no list: the kernels walk the nodes as before).
+# no such node (no list: the kernels walk the nodes as before).  cfg4 step traces
+# (profiles/r06/ab_pieces_cfg4/): no lists 1,357-1,365 us, PIECE_MULT 2 (4 pieces of ~63
+# edges per doc) 1,311-1,317, PIECE_MULT 1 (8 of ~31) 1,303-1,308.
 PIECE_MIN = 32
-PIECE_MULT = 2
+PIECE_MULT = 1
 
 
 def _work_list(lib, n, indptr, n_edges, stream):

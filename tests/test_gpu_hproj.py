@@ -140,6 +140,33 @@ def test_hproj_bwd_one_launch_equals_two(monkeypatch, n, d_in, H, D):
     assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("n,d_in,H,D,acc", [(19200, 300, 8, 8, 1), (19200, 300, 8, 8, 0), (4800, 300, 8, 8, 1),
+                                             (2570, 300, 5, 8, 0), (1001, 68, 8, 8, 1)])
+def test_narrow_bwd_one_launch_equals_dx_and_dw(n, d_in, H, D, acc):
+    """hsg_hproj_bwd on the narrow-head (W2S) shape runs dX and the dW slabs in ONE
+    launch (round 6, k_hproj_bwd_n8: the k_hproj_dx_n8 tiles and single-image
+    k_hproj_dw_mf blocks) -- bitwise equal to hsg_hproj_dx + hsg_hproj_dw (product
+    library: those entries launch the separate kernels)."""
+    from hetersumgraph_amd._lib import load, ptr
+    from hetersumgraph_amd.hproj import dropmask_bits
+    lib = load()
+    torch.manual_seed(n + H)
+    X = torch.randn(n, d_in, device="cuda")
+    W = torch.randn(H * D, d_in, device="cuda") / d_in ** 0.5
+    dZ = torch.randn(n, H * D, device="cuda")
+    bits = dropmask_bits(X, H, 0.1)
+    chunks = lib.hsg_hproj_dw_chunks(n, d_in, H, D)
+    dX1, dX2 = torch.full_like(X, 0.5), torch.full_like(X, 0.5)
+    p1, p2 = X.new_empty(chunks * H * D * d_in), X.new_empty(chunks * H * D * d_in)
+    assert lib.hsg_hproj_bwd(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(X), d_in, ptr(bits), 0.1, ptr(dX1), d_in,
+                             acc, ptr(p1), None) == 0
+    assert lib.hsg_hproj_dx(n, d_in, H, D, ptr(dZ), H * D, ptr(W), ptr(bits), 0.1, ptr(dX2), d_in, acc, None) == 0
+    assert lib.hsg_hproj_dw(n, d_in, H, D, ptr(dZ), H * D, ptr(X), d_in, ptr(bits), 0.1, ptr(p2), None, 0, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(dX1, dX2)
+    assert torch.equal(p1, p2)
+
+
 @pytest.mark.parametrize("n,d_in,H,D", [(19200, 300, 8, 8), (1000, 64, 16, 4), (257, 128, 3, 16), (70, 300, 8, 8)])
 def test_dw_4x4x1_equals_16x16x4_kernel(monkeypatch, n, d_in, H, D):
     """The unpadded 4x4x1 dW kernel (k_hproj_dw_m4, round 5) against the 16x16x4 slot

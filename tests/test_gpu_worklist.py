@@ -26,7 +26,7 @@ from helpers import build_graph, synth_fixture
 pytestmark = pytest.mark.gpu
 
 
-def host_work_list(indptr, pmin=32, mult=2):
+def host_work_list(indptr, pmin=32, mult=1):
     """Restatement of hsg_rel_work (include/hsg.h): P = max(pmin, mult * ceil(E / n));
     a node with deg > P -> ceil(deg / P) near-equal pieces (the first deg % k one
     longer), coded -(v + 1); others one item; empty list when no node is long."""
