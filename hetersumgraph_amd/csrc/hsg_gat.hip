@@ -90,8 +90,8 @@ struct RelPtrs {
     const int32_t *__restrict__ cperm;
     int xcd;                 // 1: XCD-local node order (work_range)
     int n_dwork, n_swork;    // work lists (hsg_rel.dwork / swork; round 6), 0 = none
-    const int32_t *__restrict__ dwork;
-    const int32_t *__restrict__ swork;
+    int32_t *dwork;          // [n][4] items, then [n] arrival counters
+    int32_t *swork;
 };
 
 // XCD-local node order (round 4).  The batched graph is a disjoint union of documents
@@ -169,6 +169,110 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
     }
 }
 
+// Merge of the pieces of long destinations (round 6).  The wave that merges a
+// destination v (pieces first .. first + np - 1, in item order) combines their partials
+// with v's phantoms -- exactly the online-softmax algebra of a whole destination: M =
+// max(max_p m_p, 0 if c > 0), L = sum_p l_p e^(m_p - M) + c e^(-M), h = sum_p (l_p
+// e^(m_p - M) / L) h_p, then elu(h) + origin and (m, l) = (M, L).  Lane = feature (flat
+// mapping, as k_gat_fwd); the partials of kMergeBatch pieces are requested together (one
+// round trip per batch).  Deterministic: the order is the items', whichever block merges.
+// In the forward kernel the last piece block of v to arrive merges (in-kernel, below);
+// the launch k_gat_fwd_merge (dev, HSG_PIECE_INLINE=0) does it as a second kernel.
+constexpr int kMergeBatch = 8;
+
+// the run of items with this code from `item` on (wave-wide: one ballot per 64 items)
+__device__ __forceinline__ int piece_count(const int32_t *__restrict__ work, int n_work, int item, int code,
+                                           int lane) {
+    int np = 1;
+    for (int base = item + 1;; base += 64) {
+        const int j = base + lane;
+        const unsigned long long same = __ballot(j < n_work && work[4 * j] == code);
+        if (~same == 0ull) {
+            np += 64;
+            continue;
+        }
+        return np + __builtin_ctzll(~same);
+    }
+}
+
+// block-cooperative: thread t takes features t, t + 256, ... one at a time (a loop,
+// so the merge adds few registers to the kernels that call it in-kernel)
+__device__ __forceinline__ void fwd_merge_block(const RelPtrs &R, int H, int D, const float *__restrict__ origin,
+                                                const float *__restrict__ pws, int first, int np, int v,
+                                                float *__restrict__ hout, float *__restrict__ out,
+                                                float *__restrict__ mout, float *__restrict__ lout) {
+    const int HD = H * D, W = HD + 2 * H;
+    const float c = (float)R.phantom[v];
+    const float *pw = pws + (size_t)first * W;
+#pragma unroll 1
+    for (int f = threadIdx.x; f < HD; f += blockDim.x) {
+        const int k = f / D;
+        // running max M, denominator L and weighted sum S of head k, batch by batch
+        float M = c > 0.f ? 0.f : -INFINITY, L = c > 0.f ? c : 0.f, S = 0.f;     // c e^(0 - M), M = 0
+#pragma unroll 1
+        for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
+            float mv[kMergeBatch], lv[kMergeBatch], hv[kMergeBatch];
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                const int p = min(p0 + j, np - 1);      // clamped: weight 0 below
+                mv[j] = pw[p * W + HD + k];
+                lv[j] = pw[p * W + HD + H + k];
+                hv[j] = pw[p * W + f];
+            }
+            float mb = M;
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j)
+                if (p0 + j < np) mb = fmaxf(mb, mv[j]);
+            const float sc = M == -INFINITY ? 0.f : __expf(M - mb);
+            L *= sc;
+            S *= sc;
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                if (p0 + j < np) {
+                    const float w = lv[j] * __expf(mv[j] - mb);
+                    L += w;
+                    S = fmaf(w, hv[j], S);
+                }
+            }
+            M = mb;
+        }
+        const float h = S / L;
+        const size_t o = (size_t)v * HD + f;
+        if (hout) hout[o] = h;
+        if (origin) out[o] = elu1(h) + origin[o];
+        if (f == k * D) {                                 // the head's first feature: its (m, l)
+            mout[v * H + k] = M;
+            lout[v * H + k] = L;
+        }
+    }
+}
+
+// Piece hand-off (round 6): the partials are stored write-through (sc1: relaxed
+// agent-scope atomic stores), every storing wave drains them (vmcnt(0)), the block
+// meets at a barrier, and one lane adds to the node's arrival counter (relaxed, agent
+// scope).  The block whose add completes a multiple of np merges, after an agent-scope
+// acquire and a barrier (cdna_hip_programming.md §6 Guideline 16 R1: write-through
+// stores + counter, the reducer reading them behind an acquire).  The counters start
+// at 0 (hsg_rel_work) and every launch adds exactly np per node, so no reset is needed.
+__device__ __forceinline__ void st_sc1(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0 of the block: arrive; returns (block-wide, through *flag) whether it merges
+__device__ __forceinline__ bool piece_arrive(int32_t *cnt, int np, int *flag) {
+    __syncthreads();                                      // every wave's stores drained (vmcnt(0) before)
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = old % np == np - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+
 // ---------------------------------------------------------------- forward ----
 // PF (one destination per wave only): the next destination's indptr / phantom are
 // requested one iteration ahead (vector loads, consumed by readfirstlane), and the
@@ -177,7 +281,7 @@ __device__ __forceinline__ void gather_rows(const float *__restrict__ X, int HD,
 // destination's score phase, their (sigma, tau) after its gather, before its stores
 // (vmcnt retires in issue order: the next score phase then waits for neither the
 // stores nor the next residual row) -- so its score phase starts with the scores.
-template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0>
+template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0, bool WL = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
@@ -185,8 +289,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                                                 const float *__restrict__ origin,
                                                 float *__restrict__ hout, float *__restrict__ out,
                                                 float *__restrict__ mout, float *__restrict__ lout,
-                                                float *__restrict__ pws) {
+                                                float *__restrict__ pws, int pinline) {
     constexpr int NPB = HSG_WAVES / WPN;
+    __shared__ int s_flag[1];
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
     __shared__ int s_nb[HSG_WAVES][HSG_CHUNK];
     __shared__ float s_ml[HSG_WAVES][2 * HSG_HMAX];
@@ -214,7 +319,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
     // round 6: with the relation's CSR work list (and the piece scratch pws) the loop
     // walks its items -- whole destinations, and pieces of the long ones, whose (max,
     // sum, partial h) go to pws for k_gat_fwd_merge (multi-wave form only)
-    const bool wl = WPN > 1 && pws != nullptr && R.n_dwork > 0;
+    // (WL: a template flag, so the kernel without a list keeps its registers)
+    constexpr bool wl = WL && WPN > 1;
     const WorkRange wr = work_range(wl ? R.n_dwork : R.n_dst, NPB, wid / WPN, R.xcd);
     const int vstride = wr.stride;
     int pf_beg = 0, pf_end = 0, pf_c = 0;
@@ -272,9 +378,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
             const int vn = v_ + vstride;
             if (vn < wr.end) { pf_beg = R.indptr[vn]; pf_end = R.indptr[vn + 1]; pf_c = R.phantom[vn]; }
         } else if (wl) {
-            const int code = R.dwork[3 * item];
-            beg = R.dwork[3 * item + 1];
-            end = R.dwork[3 * item + 2];
+            const int code = R.dwork[4 * item];
+            beg = R.dwork[4 * item + 1];
+            end = R.dwork[4 * item + 2];
             piece = code < 0;
             v = piece ? -code - 1 : code;
             c = piece ? 0 : R.phantom[v];                      // a piece's phantoms: in the merge
@@ -416,14 +522,27 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
         // by its own sum), max and sum, [HD | H | H] per item
         if (writer && piece) {
             float *pw = pws + (size_t)item * (HD + 2 * H);
+            if (pinline) {                                // write-through: the hand-off below
 #pragma unroll
-            for (int i = 0; i < NF; ++i) {
-                const int f = lane + 64 * i;
-                if (f < HD) pw[f] = acc[i];
-            }
-            if (kact && l == 0) {
-                pw[HD + k] = mx;
-                pw[HD + H + k] = sm;
+                for (int i = 0; i < NF; ++i) {
+                    const int f = lane + 64 * i;
+                    if (f < HD) st_sc1(&pw[f], acc[i]);
+                }
+                if (kact && l == 0) {
+                    st_sc1(&pw[HD + k], mx);
+                    st_sc1(&pw[HD + H + k], sm);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+#pragma unroll
+                for (int i = 0; i < NF; ++i) {
+                    const int f = lane + 64 * i;
+                    if (f < HD) pw[f] = acc[i];
+                }
+                if (kact && l == 0) {
+                    pw[HD + k] = mx;
+                    pw[HD + H + k] = sm;
+                }
             }
         } else if (writer) {
 #pragma unroll
@@ -441,107 +560,35 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 lout[v * H + k] = any ? sm : 1.f;
             }
         }
-        if constexpr (WPN > 1) __syncthreads();          // s_ml / s_acc are reused
-    }
-}
-
-// Merge of the pieces of long destinations (round 6; after k_gat_fwd with a CSR work
-// list).  One wave per work item; the wave of a destination's FIRST piece merges all
-// of its pieces in item order with its phantoms, exactly the online-softmax algebra of
-// a whole destination: M = max(max_p m_p, 0 if c > 0), L = sum_p l_p e^(m_p - M) +
-// c e^(-M), h = sum_p (l_p e^(m_p - M) / L) h_p, then elu(h) + origin and (m, l) = (M,
-// L).  Lane = feature (flat mapping, as k_gat_fwd); the piece count comes from one
-// ballot over the next 64 items, and the partials of kMergeBatch pieces are requested
-// together (one round trip per batch, not one per piece); deterministic.
-constexpr int kMergeBatch = 8;
-
-__device__ __forceinline__ int piece_count(const int32_t *__restrict__ work, int n_work, int item, int code,
-                                           int lane) {
-    int np = 1;
-    for (int base = item + 1;; base += 64) {
-        const int j = base + lane;
-        const unsigned long long same = __ballot(j < n_work && work[3 * j] == code);
-        if (~same == 0ull) {
-            np += 64;
-            continue;
+        if constexpr (WPN > 1) {
+            // a piece, merged in-kernel (round 6): the last of v's pieces to arrive merges
+            // them (wave 0); item, piece and the node are block-uniform here
+            if (wl && piece && pinline) {
+                const int first = R.dwork[4 * item + 3];
+                const int np = __builtin_amdgcn_readfirstlane(piece_count(R.dwork, R.n_dwork, first,
+                                                                          R.dwork[4 * first], lane));
+                if (piece_arrive(R.dwork + 4 * R.n_dwork + first, np, &s_flag[0]))
+                    fwd_merge_block(R, H, D, origin, pws, first, np, v, hout, out, mout, lout);
+            }
+            __syncthreads();                              // s_ml / s_acc / s_flag are reused
         }
-        return np + __builtin_ctzll(~same);        // the run of equal codes after this item
     }
 }
 
-template <int NF>
 __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, const float *__restrict__ origin,
                                                        const float *__restrict__ pws, float *__restrict__ hout,
                                                        float *__restrict__ out, float *__restrict__ mout,
                                                        float *__restrict__ lout) {
-    const int lane = threadIdx.x & 63;
-    const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * HSG_WAVES + (threadIdx.x >> 6)));
-    if (item >= R.n_dwork) return;
-    const int code = R.dwork[3 * item];
-    if (code >= 0 || (item > 0 && R.dwork[3 * (item - 1)] == code)) return;   // not a first piece
-    const int np = __builtin_amdgcn_readfirstlane(piece_count(R.dwork, R.n_dwork, item, code, lane));
-    const int v = -code - 1, HD = H * D, W = HD + 2 * H;
-    const float c = (float)R.phantom[v];
-    const float *pw = pws + (size_t)item * W;
-    // per feature i (head k_i = f / D; lanes past HD take head 0 and store nothing):
-    // running max M, denominator L and weighted sum S, batch by batch
-    int kf[NF];
-    float M[NF], L[NF], S[NF];
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-        const int f = lane + 64 * i;
-        kf[i] = f < HD ? f / D : 0;
-        M[i] = c > 0.f ? 0.f : -INFINITY;
-        L[i] = c > 0.f ? c : 0.f;                     // c e^(0 - M) with M = 0
-        S[i] = 0.f;
+    const int item = (int)blockIdx.x;                     // one block per item (dev: HSG_PIECE_INLINE=0)
+    const int code = R.dwork[4 * item];
+    if (code >= 0 || R.dwork[4 * item + 3] != item) return;   // not a first piece
+    __shared__ int s_np;
+    if (threadIdx.x < 64) {
+        const int np = piece_count(R.dwork, R.n_dwork, item, code, (int)threadIdx.x);
+        if (threadIdx.x == 0) s_np = np;
     }
-    for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
-        float mv[NF][kMergeBatch], lv[NF][kMergeBatch], hv[NF][kMergeBatch];
-#pragma unroll
-        for (int j = 0; j < kMergeBatch; ++j) {
-            const int p = min(p0 + j, np - 1);          // clamped: weight 0 below
-#pragma unroll
-            for (int i = 0; i < NF; ++i) {
-                const int f = min(lane + 64 * i, HD - 1);
-                mv[i][j] = pw[p * W + HD + kf[i]];
-                lv[i][j] = pw[p * W + HD + H + kf[i]];
-                hv[i][j] = pw[p * W + f];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            float mb = M[i];
-#pragma unroll
-            for (int j = 0; j < kMergeBatch; ++j)
-                if (p0 + j < np) mb = fmaxf(mb, mv[i][j]);
-            const float sc = M[i] == -INFINITY ? 0.f : __expf(M[i] - mb);
-            L[i] *= sc;
-            S[i] *= sc;
-#pragma unroll
-            for (int j = 0; j < kMergeBatch; ++j) {
-                if (p0 + j < np) {
-                    const float w = lv[i][j] * __expf(mv[i][j] - mb);
-                    L[i] += w;
-                    S[i] = fmaf(w, hv[i][j], S[i]);
-                }
-            }
-            M[i] = mb;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-        const int f = lane + 64 * i;
-        if (f < HD) {
-            const float h = S[i] / L[i];
-            const size_t o = (size_t)v * HD + f;
-            if (hout) hout[o] = h;
-            if (origin) out[o] = elu1(h) + origin[o];
-            if (f == kf[i] * D) {                         // the head's first feature: its (m, l)
-                mout[v * H + kf[i]] = M[i];
-                lout[v * H + kf[i]] = L[i];
-            }
-        }
-    }
+    __syncthreads();
+    fwd_merge_block(R, H, D, origin, pws, item, s_np, -code - 1, hout, out, mout, lout);
 }
 
 #ifdef HSG_DEV
@@ -1569,6 +1616,41 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
     }
 }
 
+// Merge of the pieces of long sources (round 6): the merging wave sums the pieces'
+// partials in item order: dsigma_u,k = sum_p ds_p,k, dZ_u = sum_p dZ_p + dsigma_u * a1
+// (the partials of kMergeBatch pieces requested together).  In-kernel by the last piece
+// block to arrive (k_gat_bwd_src_g), or k_gat_bwd_src_g_merge as a second launch (dev).
+// block-cooperative, one feature per thread per iteration (see fwd_merge_block)
+__device__ __forceinline__ void bwd_merge_block(int H, int D, const float *__restrict__ pws, int first, int np, int u,
+                                                const float *__restrict__ a1, float *__restrict__ dZ,
+                                                float *__restrict__ dsigma) {
+    const int HD = H * D, W = HD + H;
+    const float *pw = pws + (size_t)first * W;
+#pragma unroll 1
+    for (int f = threadIdx.x; f < HD; f += blockDim.x) {
+        const int k = f / D;
+        float A = 0.f, DS = 0.f;
+#pragma unroll 1
+        for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
+            float av[kMergeBatch], dv[kMergeBatch];
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j) {
+                const int p = min(p0 + j, np - 1);
+                av[j] = pw[p * W + f];
+                dv[j] = pw[p * W + HD + k];
+            }
+#pragma unroll
+            for (int j = 0; j < kMergeBatch; ++j)
+                if (p0 + j < np) {
+                    A += av[j];
+                    DS += dv[j];
+                }
+        }
+        dZ[(size_t)u * HD + f] = a1 ? fmaf(DS, a1[f], A) : A;
+        if (dsigma && f == k * D) dsigma[u * H + k] = DS;
+    }
+}
+
 // ------------------------------------ backward: one source-centric pass (S2W) ----
 // (round 4) The edge backward without its destination pass.  The softmax backward of
 // edge e = (u -> v), head k, needs rho_v,k = G_v,k . h_v,k (G = dOut * elu'(h), h the
@@ -1585,7 +1667,7 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src(RelPtrs R, int H, int 
 // hsg_gat_bwd_dst_g + hsg_gat_bwd_src pair (G read once, no dpre round trip).
 // GBF (round 5, the bf16 GEMM mode): G comes as bf16 rows (hsg_gemm_bf16_psw_elug_rho_a16
 // with g_bf16), held raw until the edge uses them.
-template <int NE, int OCC = 1, int EQ = 4, bool GBF = false, bool WL = false>
+template <int NE, int OCC = 1, int EQ = 4, bool GBF = false, bool WL = false, bool PIN = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, int D, int lph, float slope,
                                                       const float *__restrict__ sigma,
                                                       const float *__restrict__ tau,
@@ -1598,8 +1680,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
                                                       float *__restrict__ dZ, float *__restrict__ dsigma,
                                                       float *__restrict__ da1_part,
                                                       float *__restrict__ dtau_part,
-                                                      float *__restrict__ pws) {
+                                                      float *__restrict__ pws, int pinline) {
     constexpr int WPN = HSG_WAVES;
+    __shared__ int s_flag[1];
     __shared__ float s_acc[HSG_WAVES][512];
     __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
     __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
@@ -1638,9 +1721,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
         int u = item, beg, end;
         bool piece = false;
         if (wl) {
-            const int code = R.swork[3 * item];
-            beg = R.swork[3 * item + 1];
-            end = R.swork[3 * item + 2];
+            const int code = R.swork[4 * item];
+            beg = R.swork[4 * item + 1];
+            end = R.swork[4 * item + 2];
             piece = code < 0;
             u = piece ? -code - 1 : code;
         } else {
@@ -1727,10 +1810,15 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
             for (int w = 0; w < WPN; ++w) ds += s_dsig[w][kc];
             // a piece: its dZ partial without the ds * a1 term and its ds to pws
             // ([HD | H] per item), for the merge; its ds * Z_u into d a1 as any source's
+            // (written through, sc1, when the last piece block merges in-kernel)
             float *pw = piece ? pws + (size_t)item * (HD + H) : nullptr;
             if (kact && l == 0) {
-                if (piece) pw[HD + k] = ds;
-                else if (dsigma) dsigma[u * H + k] = ds;
+                if (piece) {
+                    if (pinline) st_sc1(&pw[HD + k], ds);
+                    else pw[HD + k] = ds;
+                } else if (dsigma) {
+                    dsigma[u * H + k] = ds;
+                }
             }
 #pragma unroll
             for (int i = 0; i < NE; ++i) {
@@ -1740,7 +1828,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
 #pragma unroll
                     for (int w = 0; w < WPN; ++w) a += s_acc[w][f];
                     if (piece) {
-                        pw[f] = a;
+                        if (pinline) st_sc1(&pw[f], a);
+                        else pw[f] = a;
                     } else {
                         if (a1) a = fmaf(ds, a1[f], a);
                         dZ[(size_t)u * HD + f] = a;
@@ -1748,8 +1837,20 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
                     da1[i] = fmaf(ds, zk[i], da1[i]);
                 }
             }
+            if (piece && pinline) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __syncthreads();                                   // s_acc / s_dsig reused by the next source
+        if constexpr (WL && PIN) {
+            // a piece, merged in-kernel (round 6): the last of u's pieces to arrive sums them
+            // (wave 0); item and piece are block-uniform
+            if (piece && pinline) {
+                const int first = R.swork[4 * item + 3];
+                const int np = __builtin_amdgcn_readfirstlane(piece_count(R.swork, R.n_swork, first,
+                                                                          R.swork[4 * first], lane));
+                if (piece_arrive(R.swork + 4 * R.n_swork + first, np, &s_flag[0]))
+                    bwd_merge_block(H, D, pws, first, np, u, a1, dZ, dsigma);
+            }
+        }
+        __syncthreads();                                   // s_acc / s_dsig / s_flag reused by the next source
     }
     if (wid == 0 && da1_part) {                            // block partial of d a1
 #pragma unroll
@@ -1768,59 +1869,19 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
     }
 }
 
-// Merge of the pieces of long sources (round 6; after k_gat_bwd_src_g with a CSC work
-// list).  One wave per work item; the wave of a source's FIRST piece sums its pieces'
-// partials in item order: dsigma_u,k = sum_p ds_p,k, dZ_u = sum_p dZ_p + dsigma_u * a1
-// (the partials of kMergeBatch pieces requested together).
-template <int NF>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_g_merge(RelPtrs R, int H, int D, const float *__restrict__ pws,
                                                              const float *__restrict__ a1, float *__restrict__ dZ,
                                                              float *__restrict__ dsigma) {
-    const int lane = threadIdx.x & 63;
-    const int item = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * HSG_WAVES + (threadIdx.x >> 6)));
-    if (item >= R.n_swork) return;
-    const int code = R.swork[3 * item];
-    if (code >= 0 || (item > 0 && R.swork[3 * (item - 1)] == code)) return;   // not a first piece
-    const int np = __builtin_amdgcn_readfirstlane(piece_count(R.swork, R.n_swork, item, code, lane));
-    const int u = -code - 1, HD = H * D, W = HD + H;
-    const float *pw = pws + (size_t)item * W;
-    int kf[NF];
-    float A[NF], DS[NF];
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-        const int f = lane + 64 * i;
-        kf[i] = f < HD ? f / D : 0;
-        A[i] = 0.f;
-        DS[i] = 0.f;
+    const int item = (int)blockIdx.x;                     // one block per item (dev: HSG_PIECE_INLINE=0)
+    const int code = R.swork[4 * item];
+    if (code >= 0 || R.swork[4 * item + 3] != item) return;   // not a first piece
+    __shared__ int s_np;
+    if (threadIdx.x < 64) {
+        const int np = piece_count(R.swork, R.n_swork, item, code, (int)threadIdx.x);
+        if (threadIdx.x == 0) s_np = np;
     }
-    for (int p0 = 0; p0 < np; p0 += kMergeBatch) {
-        float av[NF][kMergeBatch], dv[NF][kMergeBatch];
-#pragma unroll
-        for (int j = 0; j < kMergeBatch; ++j) {
-            const int p = min(p0 + j, np - 1);
-#pragma unroll
-            for (int i = 0; i < NF; ++i) {
-                av[i][j] = pw[p * W + min(lane + 64 * i, HD - 1)];
-                dv[i][j] = pw[p * W + HD + kf[i]];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < NF; ++i)
-#pragma unroll
-            for (int j = 0; j < kMergeBatch; ++j)
-                if (p0 + j < np) {
-                    A[i] += av[i][j];
-                    DS[i] += dv[i][j];
-                }
-    }
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-        const int f = lane + 64 * i;
-        if (f < HD) {
-            dZ[(size_t)u * HD + f] = a1 ? fmaf(DS[i], a1[f], A[i]) : A[i];
-            if (dsigma && f == kf[i] * D) dsigma[u * H + kf[i]] = DS[i];
-        }
-    }
+    __syncthreads();
+    bwd_merge_block(H, D, pws, item, s_np, -code - 1, a1, dZ, dsigma);
 }
 
 // Head-lane src pass for narrow heads (D = DV = 8, short CSC segments: the W2S word
@@ -2079,14 +2140,14 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
         }                                                                                                   \
     } while (0)
 
-template <int TAU, int WPN, int OCC = 1, int PF = 0>
+template <int TAU, int WPN, int OCC = 1, int PF = 0, bool WL = false>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
-                 float *out, float *m, float *l, float *pws = nullptr, bool last = true) {
+                 float *out, float *m, float *l, float *pws = nullptr, bool last = true, int pinline = 0) {
 #define HSG_FWD(NF_)                                                                                     \
     case NF_:                                                                                            \
-        HSG_KLAUNCH(true, last, (k_gat_fwd<NF_, TAU, WPN, OCC, PF>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
-                    sg, tau, org, h, out, m, l, pws);                                                    \
+        HSG_KLAUNCH(true, last, (k_gat_fwd<NF_, TAU, WPN, OCC, PF, WL>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
+                    sg, tau, org, h, out, m, l, pws, pinline);                                           \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
@@ -2215,6 +2276,14 @@ bool bwd_occ() {
 // launch in step traces, 16.2 vs 16.0 back to back -- the residual row is not what the
 // forward waits on (without any residual read, h instead of out: 14.0 us).  The score
 // lanes per head (HSG_GAT_FWD_LPH, dev) at 8 / 4 / 2 / 1: 15.6 / 15.9 / 17.2 / 19.6 us.
+// the pieces of long nodes merged in-kernel by their last arrival (round 6, default) or by
+// a second launch (dev A/B: HSG_PIECE_INLINE=0)
+// bit 0: the forward, bit 1: the backward (default 1: the forward merges in-kernel)
+int piece_inline() {
+    const char *e = HSG_DEV_ENV("HSG_PIECE_INLINE");
+    return e ? atoi(e) : 1;
+}
+
 int fwd_pf() {
     const char *e = HSG_DEV_ENV("HSG_GAT_FWD_PF");
     return e ? (atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : atoi(e) == 3 ? 3 : 2) : 2;
@@ -2478,22 +2547,20 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
     const bool wl = ws && R.n_dwork > 0;
     const dim3 g4(grid_nodes(wl ? R.n_dwork : rel->n_dst, 4, fcap));
     float *pws = wl ? ws : nullptr;
-    const int rc = tau_mode == HSG_TAU_TABLE
-                       ? fwd_dispatch<HSG_TAU_TABLE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out,
-                                                        m, l, pws, !wl)
-                       : fwd_dispatch<HSG_TAU_PER_EDGE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin, h,
-                                                           out, m, l, pws, !wl);
-    if (rc != 0 || !wl) return rc;
-    const dim3 gm((unsigned)((R.n_dwork + HSG_WAVES - 1) / HSG_WAVES));
-#define HSG_FM(NF_)                                                                                          \
-    case NF_:                                                                                                \
-        HSG_KLAUNCH(false, true, (k_gat_fwd_merge<NF_>), gm, dim3(256), st, R, H, D, origin, pws, h, out, m, l); \
-        break;
-    switch (nf) {
-        HSG_FM(1) HSG_FM(2) HSG_FM(3) HSG_FM(4) HSG_FM(5) HSG_FM(6) HSG_FM(7) HSG_FM(8)
-        default: return HSG_EINVAL;
-    }
-#undef HSG_FM
+    const int pin = piece_inline() & 1;
+    const int rc = !wl ? (tau_mode == HSG_TAU_TABLE
+                              ? fwd_dispatch<HSG_TAU_TABLE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin,
+                                                               h, out, m, l)
+                              : fwd_dispatch<HSG_TAU_PER_EDGE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                  origin, h, out, m, l))
+                 : tau_mode == HSG_TAU_TABLE
+                       ? fwd_dispatch<HSG_TAU_TABLE, 4, 6, 0, true>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                    origin, h, out, m, l, pws, pin, pin)
+                       : fwd_dispatch<HSG_TAU_PER_EDGE, 4, 6, 0, true>(nf, g4, st, R, H, D, lph, slope, Z, sigma,
+                                                                       tau, origin, h, out, m, l, pws, pin, pin);
+    if (rc != 0 || !wl || pin) return rc;
+    HSG_KLAUNCH(false, true, k_gat_fwd_merge, dim3((unsigned)R.n_dwork), dim3(256), st, R, H, D, origin, pws, h, out,
+                m, l);
     return launch_status();
 }
 
@@ -2759,17 +2826,31 @@ int hsg_gat_bwd_src_g_ws(const hsg_rel *rel, int H, int D, float slope, const fl
     // the CSC work list with its scratch: pieces of the long sources, merged below (round 6)
     const bool wl = ws && R.n_swork > 0;
     float *pws = wl ? ws : nullptr;
-#define HSG_SG1(NE_, OCC_, EQ_, GBF_, WL_)                                                                   \
-    HSG_KLAUNCH(true, !wl, (k_gat_bwd_src_g<NE_, OCC_, EQ_, GBF_, WL_>), grid, dim3(256), st, R, H, D, lph,    \
-                slope, sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part, pws)
+    // the backward's pieces: a second launch merges them by default (the in-kernel
+    // hand-off cost its kernel two spills and the fences: 31.0 vs 25.0 + 5.0 us per cfg4
+    // application, profiles/r06/ab_piece_inline_cfg4/); dev HSG_PIECE_INLINE=3: in-kernel
+    const int pin = piece_inline() >= 2 ? 1 : 0;
+#define HSG_SG1(NE_, OCC_, EQ_, GBF_, WL_, PIN_)                                                             \
+    HSG_KLAUNCH(true, !wl || pin, (k_gat_bwd_src_g<NE_, OCC_, EQ_, GBF_, WL_, PIN_>), grid, dim3(256), st, R, H, \
+                D, lph, slope, sigma, tau, m, l, G, rho, rho_groups, rgw, a1, Z, dZ, dsigma, da1_part, dtau_part,  \
+                pws, pin)
+#ifdef HSG_DEV
+#define HSG_SGW(NE_, OCC_, EQ_, GBF_)                                                                        \
+    do {                                                                                                     \
+        if (pin) HSG_SG1(NE_, OCC_, EQ_, GBF_, true, true);                                                  \
+        else HSG_SG1(NE_, OCC_, EQ_, GBF_, true, false);                                                     \
+    } while (0)
+#else
+#define HSG_SGW(NE_, OCC_, EQ_, GBF_) HSG_SG1(NE_, OCC_, EQ_, GBF_, true, false)
+#endif
 #define HSG_SG(NE_, OCC_, EQ_)                                                                               \
     do {                                                                                                     \
         if (g_bf16) {                                                                                        \
-            if (wl) HSG_SG1(NE_, OCC_, EQ_, true, true);                                                     \
-            else HSG_SG1(NE_, OCC_, EQ_, true, false);                                                       \
+            if (wl) HSG_SGW(NE_, OCC_, EQ_, true);                                                           \
+            else HSG_SG1(NE_, OCC_, EQ_, true, false, false);                                                \
         } else {                                                                                             \
-            if (wl) HSG_SG1(NE_, OCC_, EQ_, false, true);                                                    \
-            else HSG_SG1(NE_, OCC_, EQ_, false, false);                                                      \
+            if (wl) HSG_SGW(NE_, OCC_, EQ_, false);                                                          \
+            else HSG_SG1(NE_, OCC_, EQ_, false, false, false);                                               \
         }                                                                                                    \
     } while (0)
     // EQ: destination rows in flight per wave, as many as fit 5 blocks per CU unspilled
@@ -2783,20 +2864,12 @@ int hsg_gat_bwd_src_g_ws(const hsg_rel *rel, int H, int D, float slope, const fl
     else if (ne <= 7) HSG_SG(7, 5, 2);
     else HSG_SG(8, 5, 1);
 #undef HSG_SG
+#undef HSG_SGW
 #undef HSG_SG1
     const int rc = launch_status();
-    if (rc != 0 || !wl) return rc;
-    const int nf = (H * D + 63) / 64;
-    const dim3 gm((unsigned)((R.n_swork + HSG_WAVES - 1) / HSG_WAVES));
-#define HSG_SM(NF_)                                                                                           \
-    case NF_:                                                                                                 \
-        HSG_KLAUNCH(false, true, (k_gat_bwd_src_g_merge<NF_>), gm, dim3(256), st, R, H, D, pws, a1, dZ, dsigma); \
-        break;
-    switch (nf) {
-        HSG_SM(1) HSG_SM(2) HSG_SM(3) HSG_SM(4) HSG_SM(5) HSG_SM(6) HSG_SM(7) HSG_SM(8)
-        default: return HSG_EINVAL;
-    }
-#undef HSG_SM
+    if (rc != 0 || !wl || pin) return rc;
+    HSG_KLAUNCH(false, true, k_gat_bwd_src_g_merge, dim3((unsigned)R.n_swork), dim3(256), st, R, H, D, pws, a1, dZ,
+                dsigma);
     return launch_status();
 }
 

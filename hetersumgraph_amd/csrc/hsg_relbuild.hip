@@ -192,8 +192,10 @@ __global__ void k_node_fill(int n, const int32_t *__restrict__ fs, const int32_t
 // Work list of one CSR / CSC (hsg_rel_work, round 6).  One block of kWorkThreads walks
 // the nodes in tiles: per node k(v) = deg > P ? ceil(deg / P) : 1 items, an exclusive
 // block scan of k over the tile (+ the running offset) places them, and the pieces of
-// a long node split its segment into k near-equal runs.  *count = items, or 0 when no
-// node is long (nothing to balance: the kernels then walk the nodes).
+// a long node split its segment into k near-equal runs.  Items are 4 int32 (node code,
+// beg, end, first item of the node); after the n items come n zeroed arrival counters
+// (the pieces' in-kernel merge).  *count = items, or 0 when no node is long (nothing to
+// balance: the kernels then walk the nodes).
 constexpr int kWorkThreads = 1024;
 
 __global__ __launch_bounds__(kWorkThreads) void k_rel_work(int n, const int32_t *__restrict__ indptr, int min_len,
@@ -228,28 +230,25 @@ __global__ __launch_bounds__(kWorkThreads) void k_rel_work(int n, const int32_t 
         }
         const int first = base + s_scan[t] - k;
         if (v < n) {
-            if (k == 1) {
-                if (first < max_items) {
-                    work[3 * first] = v;
-                    work[3 * first + 1] = beg;
-                    work[3 * first + 2] = beg + deg;
-                }
-            } else {
-                for (int p = 0; p < k; ++p) {            // near-equal runs: the first deg % k one longer
-                    const int q = deg / k, r = deg % k;
-                    const int b = beg + p * q + min(p, r), e = b + q + (p < r ? 1 : 0);
-                    if (first + p < max_items) {
-                        work[3 * (first + p)] = -(v + 1);
-                        work[3 * (first + p) + 1] = b;
-                        work[3 * (first + p) + 2] = e;
-                    }
+            for (int p = 0; p < k; ++p) {                  // near-equal runs: the first deg % k one longer
+                const int q = deg / k, r = deg % k;
+                const int b = beg + p * q + min(p, r), e = b + q + (p < r ? 1 : 0);
+                if (first + p < max_items) {
+                    int32_t *w = work + 4 * (first + p);
+                    w[0] = k == 1 ? v : -(v + 1);
+                    w[1] = b;
+                    w[2] = e;
+                    w[3] = first;
                 }
             }
         }
         base += s_scan[kWorkThreads - 1];
         __syncthreads();                                 // s_scan reused by the next tile
     }
-    if (t == 0) *count = (s_any && base <= max_items) ? base : 0;
+    const bool ok = s_any && base <= max_items;
+    if (ok)
+        for (int i = t; i < base; i += kWorkThreads) work[4 * base + i] = 0;   // arrival counters
+    if (t == 0) *count = ok ? base : 0;
 }
 
 }  // namespace

@@ -88,13 +88,13 @@ class Relation:
         if self._cstruct is None:
             from ._lib import HsgRel
             d = self.dev
-            dw, sw = d.get("dwork"), d.get("swork")
+            dw, sw = d.get("dwork"), d.get("swork")        # flat: [n][4] items + [n] counters
             self._cstruct = HsgRel(
                 self.n_src, self.n_dst, self.n_typed,
                 d["indptr"].data_ptr(), d["src"].data_ptr(), d["tf"].data_ptr(),
                 d["phantom"].data_ptr(), d["cindptr"].data_ptr(), d["cdst"].data_ptr(),
                 d["cperm"].data_ptr(),
-                dw.shape[0] if dw is not None else 0, sw.shape[0] if sw is not None else 0,
+                dw.numel() // 5 if dw is not None else 0, sw.numel() // 5 if sw is not None else 0,
                 dw.data_ptr() if dw is not None else None, sw.data_ptr() if sw is not None else None)
         return self._cstruct
 
@@ -111,15 +111,16 @@ PIECE_MULT = 1
 
 
 def _work_list(lib, n, indptr, n_edges, stream):
-    """(work [items, 3] int32 tensor, or None) of one CSR / CSC: launched here, its item
-    count read back by the caller (``count``)."""
+    """(work: flat int32 [5 * cap] -- items of 4 int32, then the arrival counters -- or
+    None) of one CSR / CSC: launched here, its item count read back by the caller
+    (``count``)."""
     from . import _lib
     pmin = int(_lib.path_option("HSG_PIECE_MIN", str(PIECE_MIN)))      # dev A/B (0: no lists)
     mult = int(_lib.path_option("HSG_PIECE_MULT", str(PIECE_MULT)))
     if n <= 0 or pmin <= 0:
         return None, None
     cap = n + 2 * n_edges // pmin + 1
-    work = torch.empty(cap, 3, dtype=torch.int32, device=indptr.device)
+    work = torch.empty(5 * cap, dtype=torch.int32, device=indptr.device)     # items (4 int32) + counters
     count = torch.zeros(1, dtype=torch.int32, device=indptr.device)
     _lib.check(lib.hsg_rel_work(n, _lib.ptr(indptr), pmin, mult, _lib.ptr(work), cap, _lib.ptr(count), stream),
                "hsg_rel_work")
@@ -195,9 +196,9 @@ def attach_work_lists(d, n_src, n_dst, n_typed):
         got = iter(torch.cat(cs).tolist() if cs else [])                 # one readback per batch
         cnt = [next(got) if c is not None else 0 for c in (dc, sc)]
     if cnt[0] > 0:
-        d["dwork"] = dw[:cnt[0]]
+        d["dwork"] = dw[:5 * cnt[0]]
     if cnt[1] > 0:
-        d["swork"] = sw[:cnt[1]]
+        d["swork"] = sw[:5 * cnt[1]]
 
 
 def _structure(g):

@@ -45,15 +45,19 @@ typedef struct hsg_rel {
     const int32_t *cdst;      /* [E_T]     destination rank per CSC edge            */
     const int32_t *cperm;     /* [E_T]     CSR position of each CSC edge            */
     /* Work lists for degree-skewed relations (round 6; hsg_rel_work): 0 / NULL = none.
-     * Items in node order, [n][3] = (node, beg, end): node >= 0 is a whole node, node =
-     * -(v + 1) one piece [beg, end) of a long segment of node v (the HDSG doc supernodes'
-     * ~250 word edges, dataloader.py:387-400, next to ~20 per sentence).  dwork splits
-     * the CSR (destinations: hsg_gat_fwd_ws), swork the CSC (sources:
-     * hsg_gat_bwd_src_g_ws); the pieces' partial results are merged in a fixed order. */
+     * Items in node order, [n][4] = (node, beg, end, first): node >= 0 is a whole node,
+     * node = -(v + 1) one piece [beg, end) of a long segment of node v (the HDSG doc
+     * supernodes' ~250 word edges, dataloader.py:387-400, next to ~20 per sentence),
+     * first = the item index of v's first piece; then [n] arrival counters (zero, or a
+     * multiple of v's piece count at the first piece's slot, between launches).  dwork
+     * splits the CSR (destinations: hsg_gat_fwd_ws), swork the CSC (sources:
+     * hsg_gat_bwd_src_g_ws); the pieces' partial results are merged in a fixed order.
+     * The counters make launches that use one work list stream-ordered: do not run
+     * two such launches on one relation concurrently. */
     int32_t n_dwork;          /* items of dwork (0: no CSR work list)               */
     int32_t n_swork;          /* items of swork (0: no CSC work list)               */
-    const int32_t *dwork;     /* [n_dwork][3]                                        */
-    const int32_t *swork;     /* [n_swork][3]                                        */
+    int32_t *dwork;           /* [n_dwork][4] items + [n_dwork] counters             */
+    int32_t *swork;           /* [n_swork][4] items + [n_swork] counters             */
 } hsg_rel;
 
 /* tau addressing: HSG_TAU_TABLE -> tau is [11, H] indexed by rel->tf (tf-idf box
@@ -591,10 +595,10 @@ int hsg_hproj_dw(int n, int in, int H, int D, const float *dZ, int ldz, const fl
 /* Work list of one CSR / CSC (round 6, hsg_rel.dwork / swork): with mean segment m =
  * indptr[n] / n, the piece length is P = max(min_len, mult * ceil(m)); a node with more
  * than P edges becomes ceil(deg / P) near-equal pieces, every other node one item, in
- * node order.  work holds max_items >= n + 2 * indptr[n] / min_len + 1 items of 3
- * int32; *count receives the item count, or 0 when no node is longer than P (then the
- * kernels walk the nodes as before).  min_len <= 0: *count = 0.  One block; once per
- * batch (the relation build). */
+ * node order.  work holds 5 * max_items int32, max_items >= n + 2 * indptr[n] / min_len
+ * + 1: the items (4 int32 each) and after them the zeroed counters; *count receives the
+ * item count, or 0 when no node is longer than P (then the kernels walk the nodes as
+ * before).  min_len <= 0: *count = 0.  One block; once per batch (the relation build). */
 int hsg_rel_work(int n, const int32_t *indptr, int min_len, int mult, int32_t *work, int max_items,
                  int32_t *count, void *stream);
 size_t hsg_rel_build_workspace_bytes(int n_nodes, int n_edges);

@@ -29,7 +29,8 @@ pytestmark = pytest.mark.gpu
 def host_work_list(indptr, pmin=32, mult=1):
     """Restatement of hsg_rel_work (include/hsg.h): P = max(pmin, mult * ceil(E / n));
     a node with deg > P -> ceil(deg / P) near-equal pieces (the first deg % k one
-    longer), coded -(v + 1); others one item; empty list when no node is long."""
+    longer), coded -(v + 1); others one item; each item (code, beg, end, first item of
+    the node); empty list when no node is long."""
     n = len(indptr) - 1
     E = int(indptr[-1])
     P = max(pmin, mult * (-(-E // n)))
@@ -37,16 +38,24 @@ def host_work_list(indptr, pmin=32, mult=1):
     for v in range(n):
         b, e = int(indptr[v]), int(indptr[v + 1])
         deg = e - b
+        first = len(items)
         if deg > P:
             long_ = True
             k = -(-deg // P)
             q, r = divmod(deg, k)
             for p in range(k):
                 pb = b + p * q + min(p, r)
-                items.append((-(v + 1), pb, pb + q + (1 if p < r else 0)))
+                items.append((-(v + 1), pb, pb + q + (1 if p < r else 0), first))
         else:
-            items.append((v, b, e))
-    return np.array(items, np.int32).reshape(-1, 3) if long_ else np.zeros((0, 3), np.int32)
+            items.append((v, b, e, first))
+    return np.array(items, np.int32).reshape(-1, 4) if long_ else np.zeros((0, 4), np.int32)
+
+
+def dev_items(t):
+    """(items [n, 4], counters [n]) of a relation's flat device work list."""
+    a = t.cpu().numpy()
+    n = len(a) // 5
+    return a[:4 * n].reshape(n, 4), a[4 * n:]
 
 
 def cfg4_relations():
@@ -62,14 +71,15 @@ def test_cfg4_work_lists_match_host_restatement():
     for rel, key, ptr_key in ((rw, "dwork", "indptr"), (rs, "swork", "cindptr")):
         ref = host_work_list(rel.dev[ptr_key].cpu().numpy())
         assert len(ref) > 0
-        got = rel.dev[key].cpu().numpy()
+        got, cnt = dev_items(rel.dev[key])
         assert np.array_equal(got, ref)
+        assert not cnt.any()                                  # arrival counters start at 0
         n_long = len(set(-c - 1 for c in ref[:, 0] if c < 0))
         assert n_long == 96                                   # 32 examples x 3 docs
     # the other directions have no long segment (words: <= 9 edges)
     assert "swork" not in rw.dev and "dwork" not in rs.dev
     c = rw.cstruct()
-    assert c.n_dwork == len(rw.dev["dwork"]) and c.n_swork == 0
+    assert c.n_dwork == len(rw.dev["dwork"]) // 5 and c.n_swork == 0
 
 
 def test_no_work_list_without_skew():
@@ -99,6 +109,19 @@ def _fwd(rel, H, D, Z, sigma, tau, origin, ws):
     return h, out, m, l
 
 
+def check_counters(t):
+    """The arrival counters of the in-kernel piece merge after complete launches: at a
+    long node's first-piece slot a positive multiple of its piece count, 0 elsewhere."""
+    items, cnt = dev_items(t)
+    firsts = items[:, 3]
+    for i in range(len(items)):
+        if items[i, 0] < 0 and firsts[i] == i:
+            np_ = int((items[:, 0] == items[i, 0]).sum())
+            assert cnt[i] > 0 and cnt[i] % np_ == 0, (i, cnt[i], np_)
+        else:
+            assert cnt[i] == 0, (i, cnt[i])
+
+
 def _check_fwd(rel, H, D, seed):
     g = torch.Generator(device="cuda").manual_seed(seed)
     Z = torch.randn(rel.n_src, H * D, device="cuda", generator=g)
@@ -112,6 +135,7 @@ def _check_fwd(rel, H, D, seed):
         assert torch.equal(y, y2), name                       # deterministic
         err = ((x - y).abs() / (x.abs() + 1)).max().item()
         assert err <= 2e-6, (name, err)
+    check_counters(rel.dev["dwork"])
 
 
 def test_pieced_forward_equals_whole_nodes_cfg4():
@@ -149,8 +173,8 @@ def skewed_relation():
 
 def test_pieced_forward_equals_whole_nodes_ragged():
     rel, indptr, cindptr = skewed_relation()
-    assert np.array_equal(rel.dev["dwork"].cpu().numpy(), host_work_list(indptr))
-    assert np.array_equal(rel.dev["swork"].cpu().numpy(), host_work_list(cindptr))
+    assert np.array_equal(dev_items(rel.dev["dwork"])[0], host_work_list(indptr))
+    assert np.array_equal(dev_items(rel.dev["swork"])[0], host_work_list(cindptr))
     for H, D in ((8, 8), (6, 50), (4, 16)):
         _check_fwd(rel, H, D, H * D)
 
@@ -194,6 +218,7 @@ def _check_bwd(rel, H, D, seed, g_bf16=False):
         assert torch.equal(y, y2), name
         err = ((x - y).abs().max() / (x.abs().max() + 1e-6)).item()
         assert err <= (2e-6 if name in ("dZ", "dsigma") else 1e-5), (name, err)   # block sums: other order
+    check_counters(rel.dev["swork"])
 
 
 @pytest.mark.parametrize("g_bf16", [False, True])
@@ -206,3 +231,29 @@ def test_pieced_backward_equals_whole_sources_ragged():
     rel, _, _ = skewed_relation()
     for H, D in ((6, 50), (8, 32), (2, 64)):
         _check_bwd(rel, H, D, H + D)
+
+
+@pytest.mark.parametrize("mode", ["0", "3"])
+def test_piece_merge_modes_bitwise_equal(monkeypatch, mode):
+    """The pieces merged by a second launch (HSG_PIECE_INLINE=0), in-kernel by the last
+    arriving block in both directions (3), and the default (forward in-kernel, backward
+    second launch) run the same merge code in the same piece order: bitwise equal
+    outputs (dev library: the switch is read there only)."""
+    from helpers import skip_unless_dev
+    skip_unless_dev(False)
+    _, rs = cfg4_relations()
+    rw, _ = cfg4_relations()
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    rn = lambda *s: torch.randn(*s, device="cuda", generator=gen)
+    fa = (rn(rw.n_src, 64), rn(rw.n_src, 8), rn(11, 8), rn(rw.n_dst, 64))
+    HD, groups = 300, 5
+    ba = (rn(rs.n_src, 6), rn(11, 6), rn(rs.n_dst, 6), rn(rs.n_dst, 6).abs() + 1.0, rn(rs.n_dst, HD),
+          rn(rs.n_dst, groups, 3), groups, rn(6, 50), rn(rs.n_src, HD))
+    ref = (_fwd(rw, 8, 8, *fa, ws=True), _bwd(rs, 6, 50, ba, ws=True))
+    monkeypatch.setenv("HSG_PIECE_INLINE", mode)
+    got = (_fwd(rw, 8, 8, *fa, ws=True), _bwd(rs, 6, 50, ba, ws=True))
+    for r, g in zip(ref, got):
+        for x, y in zip(r, g):
+            assert torch.equal(x, y)
+    check_counters(rw.dev["dwork"])
+    check_counters(rs.dev["swork"])
