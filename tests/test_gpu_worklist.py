@@ -109,15 +109,16 @@ def _fwd(rel, H, D, Z, sigma, tau, origin, ws):
     return h, out, m, l
 
 
-def check_counters(t):
+def check_counters(t, inline=True):
     """The arrival counters of the in-kernel piece merge after complete launches: at a
-    long node's first-piece slot a positive multiple of its piece count, 0 elsewhere."""
+    long node's first-piece slot a multiple of its piece count (positive when the
+    launches merged in-kernel), 0 elsewhere."""
     items, cnt = dev_items(t)
     firsts = items[:, 3]
     for i in range(len(items)):
         if items[i, 0] < 0 and firsts[i] == i:
             np_ = int((items[:, 0] == items[i, 0]).sum())
-            assert cnt[i] > 0 and cnt[i] % np_ == 0, (i, cnt[i], np_)
+            assert cnt[i] % np_ == 0 and (cnt[i] > 0) == inline, (i, cnt[i], np_)
         else:
             assert cnt[i] == 0, (i, cnt[i])
 
@@ -218,7 +219,7 @@ def _check_bwd(rel, H, D, seed, g_bf16=False):
         assert torch.equal(y, y2), name
         err = ((x - y).abs().max() / (x.abs().max() + 1e-6)).item()
         assert err <= (2e-6 if name in ("dZ", "dsigma") else 1e-5), (name, err)   # block sums: other order
-    check_counters(rel.dev["swork"])
+    check_counters(rel.dev["swork"], inline=False)      # the backward's pieces: merged by a second launch
 
 
 @pytest.mark.parametrize("g_bf16", [False, True])
@@ -256,4 +257,4 @@ def test_piece_merge_modes_bitwise_equal(monkeypatch, mode):
         for x, y in zip(r, g):
             assert torch.equal(x, y)
     check_counters(rw.dev["dwork"])
-    check_counters(rs.dev["swork"])
+    check_counters(rs.dev["swork"], inline=mode == "3")
