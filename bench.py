@@ -746,11 +746,14 @@ def main(backend_cls=HipBench):
         "config": {"workload": f"{args.config}: {model_name(args.config)} WSWGAT stack W2S + {args.n_iter}x(S2W, W2S) "
                                f"fwd+bwd, train mode, {workload_shape(args.config)}",
                    "gemm_operands": args.dtype,
-                   "bf16_rows": ("wide (S2W) FFN hidden H, its output y (LayerNorm input), dY, dH and the "
-                                 "edge gate G rows; one RNE rounding each, GEMM operands rounded anyway"
+                   "bf16_rows": ("S2W edge-layer output x = elu(h) + origin (the wide FFN's input: "
+                                 "GEMM A operand, LayerNorm residual, dW1 operand), wide (S2W) FFN hidden H, "
+                                 "its output y (LayerNorm input), dY, dH and the edge gate G rows; one RNE "
+                                 "rounding each, GEMM operands rounded anyway"
                                  if args.dtype == "bf16" else "none"),
-                   "f32_rows": ("node states, edge softmax state (sigma, m, l), head projection, narrow "
-                                "(W2S) FFN, LayerNorm statistics, parameters and gradients"
+                   "f32_rows": ("LayerNorm outputs (the word / sentence states between applications), edge "
+                                "softmax state (sigma, m, l), head projection, narrow (W2S) FFN, LayerNorm "
+                                "statistics, parameters and gradients"
                                 if args.dtype == "bf16" else "all"),
                    "docs_per_gpu": len(docs), "graph_edges_per_gpu": E_total,
                    "typed_edges_per_direction": be.n_typed,

@@ -36,7 +36,8 @@ EXPORTS = ("hsg_gat_fwd", "hsg_gat_bwd_dst", "hsg_gat_bwd_blocks", "hsg_gat_bwd_
            "hsg_gat_bwd_src_g_supported", "hsg_gat_bwd_src_g", "hsg_gemm_psw_elug_rho", "hsg_ffn_small_bwd_gate",
            "hsg_gat_bwd_src_g_blocks", "hsg_gemm_bf16_psw_io", "hsg_gemm_bf16_psw_elug_rho_a16", "hsg_gemm_psw_elug_rho_gw", "hsg_ln_bwd_dy16",
            "hsg_gemm_dw_slabs_io", "hsg_ln_fwd_y16", "hsg_gat_bwd_src_g_io", "hsg_rel_work", "hsg_gat_fwd_ws_floats",
-           "hsg_gat_fwd_ws", "hsg_gat_bwd_src_g_ws_floats", "hsg_gat_bwd_src_g_ws")
+           "hsg_gat_fwd_ws", "hsg_gat_bwd_src_g_ws_floats", "hsg_gat_bwd_src_g_ws", "hsg_gat_fwd_ws16",
+           "hsg_gemm_bf16_psw_elug_rho_x16", "hsg_ln_fwd_x16", "hsg_ln_bwd_x16")
 
 HSG_EPI_STORE = 0
 HSG_EPI_RELU_BWD = 1
@@ -154,6 +155,10 @@ _SIGS = {
     "hsg_rel_work": [_I, _P, _I, _I, _P, _I, _P, _P],
     "hsg_gat_fwd_ws_floats": [_RELP, _I, _I],
     "hsg_gat_fwd_ws": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P],
+    "hsg_gat_fwd_ws16": [_RELP, _I, _I, _I, _F, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
+    "hsg_gemm_bf16_psw_elug_rho_x16": [_I, _I, _I, _P, _I, _P, _P, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P],
+    "hsg_ln_fwd_x16": [_I, _I, _P, _P, _I, _P, _P, _F, _F, _P, ctypes.c_uint32, _P, _P, _P, _P],
+    "hsg_ln_bwd_x16": [_I, _I, _P, _P, _P, _I, _P, _P, _P, _F, _P, ctypes.c_uint32, _P, _I, _P, _P, _P],
     "hsg_gat_bwd_src_g_ws_floats": [_RELP, _I, _I],
     "hsg_gat_bwd_src_g_ws": [_RELP, _I, _I, _F, _P, _P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P],
 }

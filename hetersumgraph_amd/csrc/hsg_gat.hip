@@ -200,7 +200,8 @@ __device__ __forceinline__ int piece_count(const int32_t *__restrict__ work, int
 __device__ __forceinline__ void fwd_merge_block(const RelPtrs &R, int H, int D, const float *__restrict__ origin,
                                                 const float *__restrict__ pws, int first, int np, int v,
                                                 float *__restrict__ hout, float *__restrict__ out,
-                                                float *__restrict__ mout, float *__restrict__ lout) {
+                                                float *__restrict__ mout, float *__restrict__ lout,
+                                                __bf16 *__restrict__ out16 = nullptr, int ld16 = 0) {
     const int HD = H * D, W = HD + 2 * H;
     const float c = (float)R.phantom[v];
     const float *pw = pws + (size_t)first * W;
@@ -239,12 +240,18 @@ __device__ __forceinline__ void fwd_merge_block(const RelPtrs &R, int H, int D, 
         const float h = S / L;
         const size_t o = (size_t)v * HD + f;
         if (hout) hout[o] = h;
-        if (origin) out[o] = elu1(h) + origin[o];
+        if (origin) {
+            const float xo = elu1(h) + origin[o];
+            if (out16) out16[(size_t)v * ld16 + f] = (__bf16)xo;   // the bf16 x rows replace out
+            else out[o] = xo;
+        }
         if (f == k * D) {                                 // the head's first feature: its (m, l)
             mout[v * H + k] = M;
             lout[v * H + k] = L;
         }
     }
+    if (out16)
+        for (int f = HD + (int)threadIdx.x; f < ld16; f += blockDim.x) out16[(size_t)v * ld16 + f] = (__bf16)0.f;
 }
 
 // Piece hand-off (round 6): the partials are stored write-through (sc1: relaxed
@@ -281,7 +288,11 @@ __device__ __forceinline__ bool piece_arrive(int32_t *cnt, int np, int *flag) {
 // destination's score phase, their (sigma, tau) after its gather, before its stores
 // (vmcnt retires in issue order: the next score phase then waits for neither the
 // stores nor the next residual row) -- so its score phase starts with the scores.
-template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0, bool WL = false>
+// O16 (round 6, the bf16 GEMM mode's bf16 x rows): elu(h) + origin is stored as bf16
+// rows of pitch ld16 (>= ceil8(H*D), pad columns zero) INSTEAD of the fp32 out -- the
+// wide FFN's A operand, LayerNorm residual and dW1 operand (a template flag: the fp32
+// kernels keep their registers)
+template <int NF, int TAU_MODE, int WPN, int OCC = 1, int PF = 0, bool WL = false, bool O16 = false>
 __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, int lph, float slope,
                                                 const float *__restrict__ Z,
                                                 const float *__restrict__ sigma,
@@ -289,7 +300,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                                                 const float *__restrict__ origin,
                                                 float *__restrict__ hout, float *__restrict__ out,
                                                 float *__restrict__ mout, float *__restrict__ lout,
-                                                float *__restrict__ pws, int pinline) {
+                                                float *__restrict__ pws, int pinline,
+                                                __bf16 *__restrict__ out16, int ld16) {
     constexpr int NPB = HSG_WAVES / WPN;
     __shared__ int s_flag[1];
     __shared__ float s_alpha[HSG_WAVES][HSG_CHUNK * HSG_HMAX];
@@ -552,7 +564,13 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                     const size_t o = (size_t)v * HD + f;
                     const float hv = acc[i];
                     if (hout) hout[o] = hv;
-                    if (origin) out[o] = elu1(hv) + org[i];
+                    if (origin) {
+                        const float xo = elu1(hv) + org[i];
+                        if constexpr (O16) out16[(size_t)v * ld16 + f] = (__bf16)xo;
+                        else out[o] = xo;
+                    }
+                } else if (O16 && f < ld16) {             // the zero pad columns
+                    out16[(size_t)v * ld16 + f] = (__bf16)0.f;
                 }
             }
             if (kact && l == 0) {
@@ -568,7 +586,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
                 const int np = __builtin_amdgcn_readfirstlane(piece_count(R.dwork, R.n_dwork, first,
                                                                           R.dwork[4 * first], lane));
                 if (piece_arrive(R.dwork + 4 * R.n_dwork + first, np, &s_flag[0]))
-                    fwd_merge_block(R, H, D, origin, pws, first, np, v, hout, out, mout, lout);
+                    fwd_merge_block(R, H, D, origin, pws, first, np, v, hout, out, mout, lout,
+                                    O16 ? out16 : nullptr, ld16);
             }
             __syncthreads();                              // s_ml / s_acc / s_flag are reused
         }
@@ -578,7 +597,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_fwd(RelPtrs R, int H, int D, i
 __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, const float *__restrict__ origin,
                                                        const float *__restrict__ pws, float *__restrict__ hout,
                                                        float *__restrict__ out, float *__restrict__ mout,
-                                                       float *__restrict__ lout) {
+                                                       float *__restrict__ lout, __bf16 *__restrict__ out16,
+                                                       int ld16) {
     const int item = (int)blockIdx.x;                     // one block per item (dev: HSG_PIECE_INLINE=0)
     const int code = R.dwork[4 * item];
     if (code >= 0 || R.dwork[4 * item + 3] != item) return;   // not a first piece
@@ -588,7 +608,7 @@ __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, 
         if (threadIdx.x == 0) s_np = np;
     }
     __syncthreads();
-    fwd_merge_block(R, H, D, origin, pws, item, s_np, -code - 1, hout, out, mout, lout);
+    fwd_merge_block(R, H, D, origin, pws, item, s_np, -code - 1, hout, out, mout, lout, out16, ld16);
 }
 
 #ifdef HSG_DEV
@@ -2140,14 +2160,15 @@ hipEvent_t kc_take(hipEvent_t &e, bool use) {
         }                                                                                                   \
     } while (0)
 
-template <int TAU, int WPN, int OCC = 1, int PF = 0, bool WL = false>
+template <int TAU, int WPN, int OCC = 1, int PF = 0, bool WL = false, bool O16 = false>
 int fwd_dispatch(int nf, dim3 grid, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope,
                  const float *Z, const float *sg, const float *tau, const float *org, float *h,
-                 float *out, float *m, float *l, float *pws = nullptr, bool last = true, int pinline = 0) {
+                 float *out, float *m, float *l, float *pws = nullptr, bool last = true, int pinline = 0,
+                 __bf16 *out16 = nullptr, int ld16 = 0) {
 #define HSG_FWD(NF_)                                                                                     \
     case NF_:                                                                                            \
-        HSG_KLAUNCH(true, last, (k_gat_fwd<NF_, TAU, WPN, OCC, PF, WL>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
-                    sg, tau, org, h, out, m, l, pws, pinline);                                           \
+        HSG_KLAUNCH(true, last, (k_gat_fwd<NF_, TAU, WPN, OCC, PF, WL, O16>), grid, dim3(256), st, R, H, D, lph, slope, Z, \
+                    sg, tau, org, h, out, m, l, pws, pinline, out16, ld16);                              \
         break;
     switch (nf) {
         HSG_FWD(1) HSG_FWD(2) HSG_FWD(3) HSG_FWD(4) HSG_FWD(5) HSG_FWD(6) HSG_FWD(7) HSG_FWD(8)
@@ -2417,17 +2438,18 @@ size_t hsg_gat_fwd_ws_floats(const hsg_rel *rel, int H, int D) {
     return (size_t)rel->n_dwork * (size_t)(H * D + 2 * H);
 }
 
-int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
-                   const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
-                   float *l, float *ws, void *stream) {
-    if (!rel || !shape_ok(H, D) || (origin && !out) || (!origin && !h)) return HSG_EINVAL;
+static int gat_fwd_impl(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                        const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                        float *l, float *ws, __bf16 *out16, int ld16, void *stream) {
+    if (!rel || !shape_ok(H, D) || (origin && !out && !out16) || (!origin && !h)) return HSG_EINVAL;
+    if (out16 && (!origin || ld16 < (H * D + 7) / 8 * 8 || ld16 % 8 || ((uintptr_t)out16 & 15))) return HSG_EINVAL;
     if (tau_mode != HSG_TAU_TABLE && tau_mode != HSG_TAU_PER_EDGE) return HSG_EINVAL;
     if (rel->n_dst == 0) return 0;
     const RelPtrs R = rel_ptrs(rel);
     hipStream_t st = (hipStream_t)stream;
 #ifdef HSG_DEV
     const int lpn = fwd_lanes_per_node(rel, H, D);
-    if (lpn < 64) {
+    if (lpn < 64 && !out16) {
         const int ng = 256 / lpn;
         int b = (rel->n_dst + ng - 1) / ng;
         const dim3 g(b < kFwdGridCap ? b : kFwdGridCap);
@@ -2447,7 +2469,7 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
         return launch_status();
     }
 #endif
-    if (nf == 1 && fwd_sp() && tau_mode == HSG_TAU_TABLE &&
+    if (nf == 1 && fwd_sp() && tau_mode == HSG_TAU_TABLE && !out16 &&
         (long)rel->n_src * H * D * 4 < 0x7fffffffL) {  // narrow rows: one single-pass wave per destination
         const dim3 g(grid_nodes(rel->n_dst, 1, kFwdGridCap));
         const int eb = fwd_sp();
@@ -2461,7 +2483,7 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
 #ifdef HSG_DEV
     // (k_gat_fwd_b addresses rows by 32-bit buffer offsets)
     const bool b32 = (long)rel->n_src * H * D * 4 < 0x7fffffffL && (long)rel->n_dst * H * D * 4 < 0x7fffffffL;
-    if (wpn == 1 && fwd_batch() && b32) {   // short segments: destination batches per wave (dev A/B)
+    if (wpn == 1 && fwd_batch() && b32 && !out16) {   // short segments: destination batches per wave (dev A/B)
         const int db = fwd_batch();
         const dim3 g(grid_nodes((rel->n_dst + db - 1) / db, 1, kFwdPersistentCap));
 #define HSG_B(DB_) (tau_mode == HSG_TAU_TABLE                                                                \
@@ -2474,7 +2496,7 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
         return HSG_B(4);
 #undef HSG_B
     }
-    if (wpn == 1) {                      // short segments: row-tile float4 kernel
+    if (wpn == 1 && !out16) {            // short segments: row-tile float4 kernel
         const bool al = aligned16p(Z) && aligned16p(h) && (!origin || (aligned16p(origin) && aligned16p(out)));
         const RowsPlan pl = rows_plan(H, D, al);
         if (pl.nq > 0) {
@@ -2499,45 +2521,50 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
         const int pf = fwd_pf();
         if (pf != 0 || occ != 8) {
 #ifdef HSG_DEV
+            if (out16 && pf != 2) return HSG_EINVAL;
             if (pf == 3) {                                 // residual row one destination ahead (dev A/B)
                 // 6 waves per SIMD (the next row's registers): one persistent wave of 1,536 blocks
                 const dim3 g6(grid_nodes(rel->n_dst, 1, 1536));
                 if (tau_mode == HSG_TAU_TABLE)
                     return fwd_dispatch<HSG_TAU_TABLE, 1, 6, 3>(nf, g6, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                                origin, h, out, m, l);
+                                                                origin, h, out, m, l, nullptr, true, 0, out16, ld16);
                 return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 6, 3>(nf, g6, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                               origin, h, out, m, l);
+                                                               origin, h, out, m, l, nullptr, true, 0, out16, ld16);
             }
             if (pf == 1) {                                 // one-level prefetch (dev A/B)
                 if (tau_mode == HSG_TAU_TABLE)
                     return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                                origin, h, out, m, l);
+                                                                origin, h, out, m, l, nullptr, true, 0, out16, ld16);
                 return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 1>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                               origin, h, out, m, l);
+                                                               origin, h, out, m, l, nullptr, true, 0, out16, ld16);
             }
             if (pf == 0) {
                 if (tau_mode == HSG_TAU_TABLE)
                     return fwd_dispatch<HSG_TAU_TABLE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                             origin, h, out, m, l);
+                                                             origin, h, out, m, l, nullptr, true, 0, out16, ld16);
                 return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                            origin, h, out, m, l);
+                                                            origin, h, out, m, l, nullptr, true, 0, out16, ld16);
             }
 #endif
-            if (tau_mode == HSG_TAU_TABLE)
-                return fwd_dispatch<HSG_TAU_TABLE, 1, 7, 2>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                            origin, h, out, m, l);
-            return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7, 2>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                           origin, h, out, m, l);
+#define HSG_F2(TAU, O16_) fwd_dispatch<TAU, 1, 7, 2, false, O16_>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, \
+                                                             origin, h, out, m, l, nullptr, true, 0, out16, ld16)
+            if (tau_mode == HSG_TAU_TABLE) return out16 ? HSG_F2(HSG_TAU_TABLE, true) : HSG_F2(HSG_TAU_TABLE, false);
+            return out16 ? HSG_F2(HSG_TAU_PER_EDGE, true) : HSG_F2(HSG_TAU_PER_EDGE, false);
+#undef HSG_F2
         }
 #ifdef HSG_DEV
-#define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
+#define HSG_FO(TAU, O) fwd_dispatch<TAU, 1, O>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l, \
+                                               nullptr, true, 0, out16, ld16)
+        if (out16) return HSG_EINVAL;
         if (tau_mode == HSG_TAU_TABLE) return HSG_FO(HSG_TAU_TABLE, 8);
         return HSG_FO(HSG_TAU_PER_EDGE, 8);
 #undef HSG_FO
 #endif
     }
-#define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l)
+#define HSG_F(TAU, W) fwd_dispatch<TAU, W>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, origin, h, out, m, l, \
+                                           nullptr, true, 0, out16, ld16)
 #ifdef HSG_DEV
+    if (wpn == 1 && out16) return HSG_EINVAL;
     if (wpn == 1) return tau_mode == HSG_TAU_TABLE ? HSG_F(HSG_TAU_TABLE, 1) : HSG_F(HSG_TAU_PER_EDGE, 1);
 #endif
 #undef HSG_F
@@ -2548,20 +2575,35 @@ int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, 
     const dim3 g4(grid_nodes(wl ? R.n_dwork : rel->n_dst, 4, fcap));
     float *pws = wl ? ws : nullptr;
     const int pin = piece_inline() & 1;
-    const int rc = !wl ? (tau_mode == HSG_TAU_TABLE
-                              ? fwd_dispatch<HSG_TAU_TABLE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, origin,
-                                                               h, out, m, l)
-                              : fwd_dispatch<HSG_TAU_PER_EDGE, 4>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                                  origin, h, out, m, l))
-                 : tau_mode == HSG_TAU_TABLE
-                       ? fwd_dispatch<HSG_TAU_TABLE, 4, 6, 0, true>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau,
-                                                                    origin, h, out, m, l, pws, pin, pin)
-                       : fwd_dispatch<HSG_TAU_PER_EDGE, 4, 6, 0, true>(nf, g4, st, R, H, D, lph, slope, Z, sigma,
-                                                                       tau, origin, h, out, m, l, pws, pin, pin);
+#define HSG_F4(TAU, O16_) fwd_dispatch<TAU, 4, 1, 0, false, O16_>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, \
+                                                             origin, h, out, m, l, nullptr, true, 0, out16, ld16)
+#define HSG_FW(TAU, O16_) fwd_dispatch<TAU, 4, 6, 0, true, O16_>(nf, g4, st, R, H, D, lph, slope, Z, sigma, tau, \
+                                                            origin, h, out, m, l, pws, pin, pin, out16, ld16)
+    const bool tt = tau_mode == HSG_TAU_TABLE;
+    const int rc = !wl ? (tt ? (out16 ? HSG_F4(HSG_TAU_TABLE, true) : HSG_F4(HSG_TAU_TABLE, false))
+                             : (out16 ? HSG_F4(HSG_TAU_PER_EDGE, true) : HSG_F4(HSG_TAU_PER_EDGE, false)))
+                       : (tt ? (out16 ? HSG_FW(HSG_TAU_TABLE, true) : HSG_FW(HSG_TAU_TABLE, false))
+                             : (out16 ? HSG_FW(HSG_TAU_PER_EDGE, true) : HSG_FW(HSG_TAU_PER_EDGE, false)));
+#undef HSG_F4
+#undef HSG_FW
     if (rc != 0 || !wl || pin) return rc;
     HSG_KLAUNCH(false, true, k_gat_fwd_merge, dim3((unsigned)R.n_dwork), dim3(256), st, R, H, D, origin, pws, h, out,
-                m, l);
+                m, l, out16, ld16);
     return launch_status();
+}
+
+int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                   const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                   float *l, float *ws, void *stream) {
+    return gat_fwd_impl(rel, H, D, tau_mode, slope, Z, sigma, tau, origin, h, out, m, l, ws, nullptr, 0, stream);
+}
+
+int hsg_gat_fwd_ws16(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                     const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                     float *l, float *ws, void *out16, int ld16, void *stream) {
+    if (!out16) return HSG_EINVAL;
+    return gat_fwd_impl(rel, H, D, tau_mode, slope, Z, sigma, tau, origin, h, out, m, l, ws,
+                        reinterpret_cast<__bf16 *>(out16), ld16, stream);
 }
 
 int hsg_gat_bwd_blocks(const hsg_rel *rel) {

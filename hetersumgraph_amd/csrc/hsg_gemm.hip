@@ -93,6 +93,8 @@ struct GemmArgs {
     const int64_t *seed = nullptr;
     float eps = 0.f, p_drop = 0.f;
     uint32_t offset = 0;
+    // HSG_EPI_ADD_ELUG with a bf16 x (aux2; k_gemm7 IO bit 4, round 6): its row pitch
+    int ldx = 0;
 };
 
 // Workgroup b is dispatched to XCD b % 8, and so is tile t (the persistent grid is a
@@ -947,7 +949,9 @@ struct EpiMap {
     static constexpr int QPR = BN / 4, QS = QPR <= 16 ? 16 : QPR <= 32 ? 32 : 64, RPS = 64 / QS;
     static constexpr int GW = BN % 64 == 0 ? 64 : BN;
 };
-template <int BN, bool CBF = false, bool AUXBF = false, bool GBF = false>
+// XBF (round 6): the ELU gate's x (aux2) as bf16 rows of pitch p.ldx -- the bf16 mode's
+// bf16 edge-layer output (hsg_gat_fwd_ws16)
+template <int BN, bool CBF = false, bool AUXBF = false, bool GBF = false, bool XBF = false>
 struct EpiRows {
     static constexpr int LDW = BN + 4, QPR = EpiMap<BN>::QPR, QS = EpiMap<BN>::QS, RPS = EpiMap<BN>::RPS;
     static constexpr int GW = EpiMap<BN>::GW;
@@ -981,7 +985,14 @@ struct EpiRows {
             for (int t = 0; t < STEPS; ++t) {
                 const int m = min(row0 + min(t * RPS + rs, 31), p.M - 1);
                 const size_t o = (size_t)m * p.ldaux + nc;
-                ex[t] = *reinterpret_cast<const f32x4 *>(p.aux2 + o) - *reinterpret_cast<const f32x4 *>(p.aux3 + o);
+                if constexpr (XBF) {
+                    const bf16x4v7 xb = *reinterpret_cast<const bf16x4v7 *>(
+                        reinterpret_cast<const __bf16 *>(p.aux2) + (size_t)m * p.ldx + nc);
+                    ex[t] = f32x4{(float)xb[0], (float)xb[1], (float)xb[2], (float)xb[3]} -
+                            *reinterpret_cast<const f32x4 *>(p.aux3 + o);
+                } else {
+                    ex[t] = *reinterpret_cast<const f32x4 *>(p.aux2 + o) - *reinterpret_cast<const f32x4 *>(p.aux3 + o);
+                }
             }
         }
     }
@@ -1304,6 +1315,7 @@ template <int BN, int S, int PM = 0, int OCC = 2, bool SA = false, int IO = 0>
 __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp) {
     constexpr int BM = 128, TN = BN / 16;
     constexpr bool ABF = (IO & 1) != 0, CBF = (IO & 2) != 0, AUXBF = (IO & 4) != 0, GBF = (IO & 8) != 0;
+    constexpr bool XBF = (IO & 16) != 0;
     static_assert(!ABF || (PM == 2 && !SA), "bf16 A: the bf16 mode's one-product path");
     constexpr int A_FL = ABF ? BM * 16 : BM * 32;          // floats of the A tile
     constexpr int B_BF = BN * 32;                          // bf16 per limb-plane tile
@@ -1332,7 +1344,7 @@ __global__ __launch_bounds__(256, OCC) void k_gemm7(GemmArgs p, const __bf16 *__
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
-    EpiRows<BN, CBF, AUXBF, GBF> ep;
+    EpiRows<BN, CBF, AUXBF, GBF, XBF> ep;
 
     uint32_t aoff[BM / 32], boff[NBP];
     if constexpr (SA) {
@@ -2665,6 +2677,7 @@ static int launch7io(GemmArgs p, const __bf16 *pl, int Np, int Kp, int io, hipSt
     case 7: return wide ? launch7<128, 2, 2, 2, false, 7>(p, pl, Np, Kp, st) : launch7io_narrow<7>(p, pl, Np, Kp, st);
     case 3: return wide ? launch7<128, 2, 2, 2, false, 3>(p, pl, Np, Kp, st) : launch7io_narrow<3>(p, pl, Np, Kp, st);
     case 9: return wide ? launch7<128, 2, 2, 2, false, 9>(p, pl, Np, Kp, st) : launch7io_narrow<9>(p, pl, Np, Kp, st);
+    case 25: return wide ? launch7<128, 2, 2, 2, false, 25>(p, pl, Np, Kp, st) : launch7io_narrow<25>(p, pl, Np, Kp, st);
     default: return HSG_EINVAL;
     }
 }
@@ -2841,6 +2854,32 @@ int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, 
     p.rho_d = head_dim;
     if (!epi_rows_ok(p)) return HSG_EINVAL;
     return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, g_bf16 ? 9 : 1, (hipStream_t)stream);
+}
+
+// ... with x given as bf16 rows of pitch ldx (x_bf16: the bf16 mode's bf16 edge-layer
+// output, hsg_gat_fwd_ws16; ldx % 8 == 0, 16-byte aligned), round 6.  x_bf16 == 0 is
+// hsg_gemm_bf16_psw_elug_rho_a16.
+int hsg_gemm_bf16_psw_elug_rho_x16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
+                                   int ldc, const float *aux, const void *x, int ldx, int x_bf16, const float *origin,
+                                   void *G, int ld, float *rho, int head_dim, int g_bf16, void *stream) {
+    if (!x_bf16)
+        return hsg_gemm_bf16_psw_elug_rho_a16(M, N, K, A, lda, planes, C, ldc, aux, reinterpret_cast<const float *>(x),
+                                              origin, G, ld, rho, head_dim, g_bf16, stream);
+    if (M < 0 || N < 0 || K < 0 || !C || !planes || !A || !aux || !x || !origin || !G || !g_bf16) return HSG_EINVAL;
+    if ((lda & 7) || (((uintptr_t)A) & 15) || (((uintptr_t)planes) & 15) || lda < K || ld < N) return HSG_EINVAL;
+    if ((ldx & 7) || ldx < N) return HSG_EINVAL;
+    if (rho && (head_dim < 32 || N % head_dim)) return HSG_EINVAL;
+    if (M == 0 || N == 0) return 0;
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    GemmArgs p{M, N, K, reinterpret_cast<const float *>(A), lda, nullptr, 0, C, ldc, nullptr, aux, ld,
+               HSG_EPI_ADD_ELUG, 0, Kp / 32, nullptr, nullptr, 1, 1, reinterpret_cast<const float *>(x), origin,
+               reinterpret_cast<float *>(G)};
+    p.rho = rho;
+    p.rho_d = head_dim;
+    p.ldx = ldx;
+    if (!epi_rows_ok(p)) return HSG_EINVAL;
+    return launch7io(p, reinterpret_cast<const __bf16 *>(planes), Np, Kp, 25, (hipStream_t)stream);
 }
 
 int hsg_gemm_f32_psw_elug(int M, int N, int K, const float *A, int lda, const void *planes, float *C, int ldc,

@@ -145,13 +145,15 @@ __global__ __launch_bounds__(256) void k_ln_fwd4(int n, int d, const float *__re
 // YBF (round 5, the bf16 GEMM mode): y -- the wide FFN's output, the LayerNorm input --
 // comes as bf16 rows (pitch d), kept as raw quads until the row is consumed (a
 // conversion at the load would wait for the prefetch at once).
-template <int NV, int RPW, bool YBF = false>
+// XBF (round 6): the residual x -- the edge layer's output elu(h) + origin -- comes as
+// bf16 rows of pitch ldx (>= ceil8(d)), likewise kept raw until used.
+template <int NV, int RPW, bool YBF = false, bool XBF = false>
 __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__restrict__ y,
                                                   const float *__restrict__ x, const float *__restrict__ gamma,
                                                   const float *__restrict__ beta, float eps, float p_drop,
                                                   const int64_t *__restrict__ seedp, uint32_t offset,
                                                   float *__restrict__ out, float *__restrict__ mean,
-                                                  float *__restrict__ rstd) {
+                                                  float *__restrict__ rstd, int ldx = 0) {
     const int lane = threadIdx.x & 63;
     const int ng = (n + RPW - 1) / RPW, nw = gridDim.x * 4;
     int g = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
     const uint32_t thr = hsg_drop_threshold(p_drop);
     const float scale = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
     f32x4r yv[RPW][NV], xv[RPW][NV];
-    bf16x4r yb[YBF ? RPW : 1][YBF ? NV : 1];
+    bf16x4r yb[YBF ? RPW : 1][YBF ? NV : 1], xb[XBF ? RPW : 1][XBF ? NV : 1];
     auto load = [&](int gg) {
 #pragma unroll
         for (int q = 0; q < RPW; ++q) {
@@ -172,7 +174,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
                     yb[q][i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + (size_t)r * d + c);
                 else
                     yv[q][i] = *reinterpret_cast<const f32x4r *>(y + (size_t)r * d + c);
-                xv[q][i] = *reinterpret_cast<const f32x4r *>(x + (size_t)r * d + c);
+                if constexpr (XBF)
+                    xb[q][i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(x) + (size_t)r * ldx + c);
+                else
+                    xv[q][i] = *reinterpret_cast<const f32x4r *>(x + (size_t)r * d + c);
             }
         }
     };
@@ -198,7 +203,10 @@ __global__ __launch_bounds__(256) void k_ln_fwd4p(int n, int d, const float *__r
                         for (int e = 0; e < 4; ++e)
                             v[e] = hsg_keep32(dkey, (uint32_t)(o + e), thr) ? v[e] * scale : 0.f;
                     }
-                    s[q][i] = v + xv[q][i];
+                    if constexpr (XBF)
+                        s[q][i] = v + f32x4r{(float)xb[q][i][0], (float)xb[q][i][1], (float)xb[q][i][2], (float)xb[q][i][3]};
+                    else
+                        s[q][i] = v + xv[q][i];
                     acc[q] += (s[q][i][0] + s[q][i][1]) + (s[q][i][2] + s[q][i][3]);
                 }
             }
@@ -338,14 +346,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
 // dW2 = dy^T H, both on bf16-rounded operands) -- is stored as bf16 rows of pitch ld_dy
 // (>= ceil8(d)), the pad columns d .. ceil8(d) - 1 zero (the bf16-A contract of
 // hsg_gemm_bf16_psw_io); db2 still sums the fp32 values.
-template <int NV, bool DYBF = false, bool YBF = false>
+// XBF (round 6): x as bf16 rows of pitch ldx (the forward's k_ln_fwd4p<..., XBF>).
+template <int NV, bool DYBF = false, bool YBF = false, bool XBF = false>
 __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__restrict__ dout,
                                                   const float *__restrict__ y, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ mean,
                                                   const float *__restrict__ rstd, float p_drop,
                                                   const int64_t *__restrict__ seedp, uint32_t offset,
                                                   float *__restrict__ dy, float *__restrict__ dx,
-                                                  float *__restrict__ part, int ld_dy = 0) {
+                                                  float *__restrict__ part, int ld_dy = 0, int ldx = 0) {
     __shared__ __attribute__((aligned(16))) float s_red[4][kMaxPerLane * 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t dkey = p_drop > 0.f ? hsg_drop_key((uint64_t)seedp[0], offset) : 0u;
@@ -365,6 +374,7 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
     int r = blockIdx.x * 4 + wid;
     f32x4r yv[NV], xv[NV], gv[NV];
     bf16x4r yb[YBF ? NV : 1];                                        // YBF: bf16 y rows, raw until used
+    bf16x4r xb[XBF ? NV : 1];                                        // XBF: bf16 x rows, likewise
     float mu = 0.f, rs = 0.f;
     auto load = [&](int rr) {
         mu = mean[rr];
@@ -374,7 +384,10 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
             const size_t o = (size_t)rr * d + cq[i];
             if constexpr (YBF) yb[i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + o);
             else yv[i] = *reinterpret_cast<const f32x4r *>(y + o);
-            xv[i] = *reinterpret_cast<const f32x4r *>(x + o);
+            if constexpr (XBF)
+                xb[i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(x) + (size_t)rr * ldx + cq[i]);
+            else
+                xv[i] = *reinterpret_cast<const f32x4r *>(x + o);
             gv[i] = *reinterpret_cast<const f32x4r *>(dout + o);
         }
     };
@@ -399,7 +412,10 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
                         if (!k) keep &= ~(1u << (4 * i + e));
                         v = k ? v * scale : 0.f;
                     }
-                    xh[i][e] = (v + xv[i][e] - mu) * rs;
+                    float xe;
+                    if constexpr (XBF) xe = (float)xb[i][e];
+                    else xe = xv[i][e];
+                    xh[i][e] = (v + xe - mu) * rs;
                     const float go = gv[i][e];
                     g[i][e] = go * gam[i][e];
                     sg += g[i][e];
@@ -642,6 +658,44 @@ int hsg_ln_fwd_y16(int n, int d, const void *y, const float *x, const float *gam
     const int blocks = kLnFwdPBlocks < (n + 3) / 4 ? kLnFwdPBlocks : (n + 3) / 4;
     hipLaunchKernelGGL((k_ln_fwd4p<2, 1, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, d,
                        reinterpret_cast<const float *>(y), x, gamma, beta, eps, p_drop, seed, offset, out, mean, rstd);
+    return status();
+}
+
+// The bf16 GEMM mode's bf16 x rows (round 6): hsg_ln_fwd_y16 / hsg_ln_bwd_dy16 with the
+// residual x given as bf16 rows of pitch ldx (ldx % 8 == 0, >= ceil8(d), 16-byte aligned)
+// -- the edge layer's output as hsg_gat_fwd_ws16 stores it.  y is bf16 (pitch d) in both,
+// dy bf16 rows of pitch ld_dy in the backward.  HSG_EINVAL off those shapes.
+int hsg_ln_fwd_x16(int n, int d, const void *y, const void *x, int ldx, const float *gamma, const float *beta,
+                   float eps, float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
+                   void *stream) {
+    const auto al = [](const void *q, uintptr_t a) { return ((uintptr_t)q & (a - 1)) == 0; };
+    if (d % 4 || (d + 255) / 256 != 2 || d <= 256 || (ldx & 7) || ldx < (d + 7) / 8 * 8 || p_drop < 0.f ||
+        p_drop >= 1.f || (p_drop > 0.f && !seed) || (p_drop > 0.f && (long)n * d >= (1L << 32)) || !al(y, 8) ||
+        !al(x, 16) || !al(out, 16) || !al(gamma, 16) || !al(beta, 16))
+        return HSG_EINVAL;
+    if (n == 0) return 0;
+    const int blocks = kLnFwdPBlocks < (n + 3) / 4 ? kLnFwdPBlocks : (n + 3) / 4;
+    hipLaunchKernelGGL((k_ln_fwd4p<2, 1, true, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, n, d,
+                       reinterpret_cast<const float *>(y), reinterpret_cast<const float *>(x), gamma, beta, eps,
+                       p_drop, seed, offset, out, mean, rstd, ldx);
+    return status();
+}
+
+int hsg_ln_bwd_x16(int n, int d, const float *dout, const void *y, const void *x, int ldx, const float *gamma,
+                   const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset, void *dy,
+                   int ld_dy, float *dx, float *part, void *stream) {
+    const auto al = [](const void *q, uintptr_t a) { return ((uintptr_t)q & (a - 1)) == 0; };
+    if (d % 4 || (d + 255) / 256 != 2 || d <= 256 || (ld_dy & 7) || ld_dy < (d + 7) / 8 * 8 || (ldx & 7) ||
+        ldx < (d + 7) / 8 * 8 || p_drop < 0.f || p_drop >= 1.f || (p_drop > 0.f && !seed) || !part ||
+        (p_drop > 0.f && (long)n * d >= (1L << 32)) || !al(dout, 16) || !al(y, 8) || !al(x, 16) || !al(gamma, 16) ||
+        !al(dy, 16) || !al(dx, 16))
+        return HSG_EINVAL;
+    hipStream_t st = (hipStream_t)stream;
+    dim3 grid(grid_rows(n, ln_bwd_cap())), block(256);
+    if (n == 0) return (int)hipMemsetAsync(part, 0, sizeof(float) * 3 * d * grid.x, st);
+    hipLaunchKernelGGL((k_ln_bwd4p<2, true, true, true>), grid, block, 0, st, n, d, dout,
+                       reinterpret_cast<const float *>(y), reinterpret_cast<const float *>(x), gamma, mean, rstd,
+                       p_drop, seed, offset, reinterpret_cast<float *>(dy), dx, part, ld_dy, ldx);
     return status();
 }
 

@@ -241,9 +241,13 @@ def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
     lib = load()
     M, K = A.shape
     N = Bs.N
-    ts = (out, x, origin, G)
+    x16 = x.dtype == torch.bfloat16              # the bf16 mode's bf16 x rows (pitch % 8 == 0), round 6
+    ts = (out, origin, G) if x16 else (out, x, origin, G)
     if K != Bs.K or any(t.shape != (M, N) or not t.is_contiguous() for t in ts):
         return False
+    if x16 and (x.shape != (M, N) or x.stride(1) != 1 or x.stride(0) % 8 or A.dtype != torch.bfloat16
+                or G.dtype != torch.bfloat16):
+        raise RuntimeError("gemm_psw_elug: bf16 x rows come with the bf16 dH and G rows")
     if rho is not None and (rho.shape != (M, elug_rho_groups(Bs, M, head_dim), 3) or not rho.is_contiguous()):
         return False
     if rho is not None and rho.dtype != torch.float32:
@@ -253,9 +257,9 @@ def gemm_psw_elug(A, Bs, out, x, origin, G, rho=None, head_dim=0):
     if A.dtype == torch.bfloat16:                # the bf16 mode's bf16 dH rows
         if Bs.mode != "bf16":
             raise RuntimeError("gemm_psw_elug: bf16 activations belong to the 'bf16' GEMM mode")
-        rc = lib.hsg_gemm_bf16_psw_elug_rho_a16(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out),
-                                                ptr(x), ptr(origin), ptr(G), N, ptr(rho), int(head_dim),
-                                                int(G.dtype == torch.bfloat16), stream_of(A))
+        rc = lib.hsg_gemm_bf16_psw_elug_rho_x16(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out),
+                                                ptr(x), x.stride(0), int(x16), ptr(origin), ptr(G), N, ptr(rho),
+                                                int(head_dim), int(G.dtype == torch.bfloat16), stream_of(A))
     else:
         rc = lib.hsg_gemm_psw_elug_rho(M, N, K, ptr(A), _ld(A), ptr(Bs.planes), ptr(out), N, ptr(out), ptr(x),
                                        ptr(origin), ptr(G), N, ptr(rho), int(head_dim), int(Bs.mode == "bf16"),

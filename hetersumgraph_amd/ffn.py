@@ -92,9 +92,27 @@ def ffn_fwd(x, w1, b1, w2, b2, gamma, beta, p_drop, eps=LN_EPS, H_out=None, wspl
     the caller (default: drawn here).  Returns (out, saved)."""
     lib = load()
     n, d = x.shape
-    out = torch.empty_like(x)
-    mean = x.new_empty(n)
-    rstd = x.new_empty(n)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    out = torch.empty(n, d, **f32)
+    mean = torch.empty(n, **f32)
+    rstd = torch.empty(n, **f32)
+    if x.dtype == torch.bfloat16:
+        # the bf16 GEMM mode's bf16 x rows (round 6; the edge layer's hsg_gat_fwd_ws16
+        # output, pitch % 8 == 0, zero pad): the A operand of the first GEMM and the
+        # LayerNorm residual, both read as bf16
+        if isinstance(wsplit, str):
+            wsplit = ffn_wsplit(x, w1, b1, w2, b2)
+        if (wsplit is None or wsplit[0].mode != "bf16" or b2 is None or H_out is None
+                or H_out.dtype != torch.bfloat16 or not bf16_rows_ok(d, w1.shape[0])):
+            raise RuntimeError("ffn_fwd: bf16 x rows belong to the bf16 GEMM mode's bf16-row FFN")
+        H = gemm_psw(x, wsplit[0], bias=b1, relu=True, out=H_out)
+        seed_t, off = _draw(x, p_drop, rng)
+        y = torch.empty(n, d, dtype=torch.bfloat16, device=x.device)
+        gemm_psw(H, wsplit[1], bias=b2, out=y)
+        check(lib.hsg_ln_fwd_x16(n, d, ptr(y), ptr(x), x.stride(0), ptr(gamma), ptr(beta), float(eps),
+                                 float(p_drop), ptr(seed_t), off, ptr(out), ptr(mean), ptr(rstd), stream_of(x)),
+              "hsg_ln_fwd_x16")
+        return out, (x, w1, w2, gamma, H, y, mean, rstd, float(p_drop), seed_t, off, wsplit)
     if b1 is not None and b2 is not None and _fused_ok(lib, x, w1, w2):
         H = H_out if H_out is not None else x.new_empty(n, w1.shape[0])
         y = torch.empty_like(x)
@@ -161,9 +179,15 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
     n, d = x.shape
     st = stream_of(x)
     d_hid = H.shape[1]
-    dy = act_grads[0] if act_grads is not None else torch.empty_like(x)
-    dx = torch.empty_like(x)
+    f32 = dict(dtype=torch.float32, device=x.device)
+    dy = act_grads[0] if act_grads is not None else torch.empty(n, d, **f32)
+    dx = torch.empty(n, d, **f32)
     g_done = False
+    x16 = x.dtype == torch.bfloat16             # the bf16 mode's bf16 x rows (ffn_fwd)
+    if x16 and (act_grads is None or dy.dtype != torch.bfloat16 or y.dtype != torch.bfloat16 or wsplit is None
+                or elug is None or dw1 is not None):
+        raise RuntimeError("ffn_bwd: bf16 x rows come with the fused stack's bf16 rows (dy, y, G) and its "
+                           "batched weight gradients")
     if _fused_ok(lib, x, w1, w2) and H.is_contiguous() and y.is_contiguous():
         # one launch: LN/dropout backward, dH = (dy W2) * relu'(H), dx = ds + dH W1
         nb = rt = lib.hsg_ffn_small_bwd_blocks(n)
@@ -181,8 +205,12 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
         check(rc, "hsg_ffn_small_bwd")
     else:
         nb = lib.hsg_ln_bwd_blocks(n)
-        part = x.new_empty(nb, 3, d)
-        if dy.dtype == torch.bfloat16:       # the bf16 mode's bf16 dy rows (zero pad to ceil8(d))
+        part = torch.empty(nb, 3, d, **f32)
+        if x16:
+            check(lib.hsg_ln_bwd_x16(n, d, ptr(dout), ptr(y), ptr(x), x.stride(0), ptr(gamma), ptr(mean), ptr(rstd),
+                                     p_drop, ptr(seed_t), off, ptr(dy), dy.stride(0), ptr(dx), ptr(part), st),
+                  "hsg_ln_bwd_x16")
+        elif dy.dtype == torch.bfloat16:     # the bf16 mode's bf16 dy rows (zero pad to ceil8(d))
             check(lib.hsg_ln_bwd_dy16(n, d, ptr(dout), ptr(y), int(y.dtype == torch.bfloat16), ptr(x), ptr(gamma),
                                       ptr(mean), ptr(rstd), p_drop, ptr(seed_t), off, ptr(dy), dy.stride(0), ptr(dx),
                                       ptr(part), st), "hsg_ln_bwd_dy16")
@@ -190,12 +218,14 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
             check(lib.hsg_ln_bwd(n, d, ptr(dout), ptr(y), ptr(x), ptr(gamma), ptr(mean), ptr(rstd), p_drop,
                                  ptr(seed_t), off, ptr(dy), ptr(dx), ptr(part), st), "hsg_ln_bwd")
         rt = psw_row_tiles(n, d_hid, d, wsplit[2].mode) if wsplit is not None else row_tiles(n, d_hid, d)
-        hpart = x.new_empty(rt, d_hid)
+        hpart = torch.empty(rt, d_hid, **f32)
         dH_out = act_grads[1] if act_grads is not None else None
         if wsplit is not None:
             dH = gemm_psw(dy, wsplit[2], relu_mask=H, colsum_part=hpart, out=dH_out)
             if elug is not None and gemm_psw_elug(dH, wsplit[3], dx, x, *elug):
                 g_done = True
+            elif x16:
+                raise RuntimeError("ffn_bwd: the ELU-gate dx GEMM declined bf16 x rows")
             else:
                 gemm_psw(dH, wsplit[3], out=dx, add=dx)
         else:
@@ -215,7 +245,7 @@ def ffn_bwd(saved, dout, dst, act_grads=None, batch=None, key=None, elug=None, g
                 batch.add((key, name), o, d, 3 * d, off, 1.0, acc, part, nb)
         return (dx, g_done) if elug is not None or gate is not None else dx
     if any(o is not None for o in outs):
-        db1, dg, dbt, db2 = [o if o is not None else x.new_empty(n_)
+        db1, dg, dbt, db2 = [o if o is not None else torch.empty(n_, **f32)
                              for o, n_ in zip(outs, (d_hid, d, d, d))]   # scratch for unneeded ones
         check(lib.hsg_ffn_colsums(rt, d_hid, ptr(hpart), ptr(db1), nb, d, ptr(part), ptr(dg), ptr(dbt), ptr(db2),
                                   int(bool(acc)), st), "hsg_ffn_colsums")

@@ -163,8 +163,10 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
     and origin instead of h, rises 33 -> 39.6 us (step +8 us).  ``no_h``:
     the same without the switch -- for a caller whose backward hands
     :func:`gat_table_bwd` the G rows from the FFN's last GEMM epilogue
-    (hsg_gemm_f32_psw_elug), so the dst pass reads neither h nor x / origin.  Returns
-    (out, saved)."""
+    (hsg_gemm_f32_psw_elug), so the dst pass reads neither h nor x / origin.  A bf16
+    ``out`` ([n_dst, H*D] view of rows with pitch % 8 == 0, round 6): x is stored as
+    bf16 rows there (hsg_gat_fwd_ws16, the bf16 GEMM mode's bf16 x; with ``no_h`` only,
+    as the backward's G then comes from the FFN epilogue).  Returns (out, saved)."""
     lib = load()
     n_src, n_dst, HD = rel.n_src, rel.n_dst, H * D
     if Z.shape != (n_src, HD):
@@ -184,13 +186,22 @@ def gat_table_fwd(Z, attn, T, wf, bf, origin, rel, H, D, slope, tables=None, out
         out = None
     elif out is None:
         out = Z.new_empty(n_dst, HD)
+    x16 = out is not None and out.dtype == torch.bfloat16
+    if x16 and (not no_h or out.shape != (n_dst, HD) or out.stride(1) != 1 or out.stride(0) % 8):
+        raise ValueError("gat_table_fwd: bf16 x rows need the no-h forward and an [n_dst, H*D] view of rows "
+                         "with a pitch of a multiple of 8")
     m = Z.new_empty(n_dst, H)
     l = Z.new_empty(n_dst, H)
     tok = _clock_start(("gat_fwd", rel.kind), Z)
     try:
         ws = fwd_workspace(lib, relp, H, D, Z)
-        check(lib.hsg_gat_fwd_ws(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
-                                 ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), ptr(ws), st), "hsg_gat_fwd_ws")
+        if x16:
+            check(lib.hsg_gat_fwd_ws16(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau), ptr(origin),
+                                       ptr(h), None, ptr(m), ptr(l), ptr(ws), ptr(out), out.stride(0), st),
+                  "hsg_gat_fwd_ws16")
+        else:
+            check(lib.hsg_gat_fwd_ws(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
+                                     ptr(origin), ptr(h), ptr(out), ptr(m), ptr(l), ptr(ws), st), "hsg_gat_fwd_ws")
     except BaseException:
         _clock_abort(tok)
         raise
@@ -254,6 +265,9 @@ def gat_table_bwd(saved, dout, dZ=True, dst=None, stage=None, G=None, rho=None):
                 check(lib.hsg_gat_bwd_dst_g(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau), ptr(m),
                                             ptr(l), ptr(G), ptr(dpre), ptr(dtp), st), "hsg_gat_bwd_dst_g")
             elif xo is not None:            # forward without h (keep_h=False)
+                if xo[0].dtype != torch.float32:
+                    raise ValueError("gat_table_bwd: a forward with bf16 x rows needs its G rows from the FFN "
+                                     "epilogue (hsg_gemm_bf16_psw_elug_rho_x16)")
                 check(lib.hsg_gat_bwd_dst_noh(relp, H, D, HSG_TAU_TABLE, slope, ptr(Z), ptr(sigma), ptr(tau),
                                               ptr(xo[0]), ptr(xo[1]), ptr(m), ptr(l), ptr(dout), ptr(G), ptr(dpre),
                                               ptr(dtp), st), "hsg_gat_bwd_dst_noh")

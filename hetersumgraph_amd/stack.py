@@ -179,6 +179,25 @@ def rho_partials(G, groups):
     return G.new_empty(G.shape[0], groups, 3, dtype=torch.float32)
 
 
+def _x16_ok(lay, rel, wsplit, d, d_hid):
+    """The bf16 GEMM mode keeps this application's edge-layer output x (the wide FFN's
+    A operand, LayerNorm residual and dW1 operand) as bf16 rows (round 6, VERDICT r5
+    #8): the FFN runs on the bf16 rows (ffn.bf16_rows_ok), the forward stores no h
+    (its backward's G comes from the dx GEMM's epilogue, which then reads the bf16 x:
+    hsg_gemm_bf16_psw_elug_rho_x16) and that backward is the one-pass source-centric
+    launch (bf16 G).  HSG_FFN_BF16_X=0: fp32 x rows (A/B)."""
+    if wsplit is None or isinstance(wsplit, str) or wsplit[0].mode != "bf16" or not bf16_rows_ok(d, d_hid):
+        return False
+    if any(_lib.path_option(k, "1") == "0" for k in ("HSG_FFN_BF16_X", "HSG_FFN_BF16_ROWS", "HSG_FFN_BF16_ACT",
+                                                     "HSG_GAT_GEPI", "HSG_GAT_MERGED")):
+        return False
+    if lay.H * lay.D != d:
+        return False
+    lib, relp = load(), ctypes.byref(rel.cstruct())
+    return (bool(lib.hsg_gat_bwd_dst_noh_supported(relp, lay.H, lay.D))
+            and bool(lib.hsg_gat_bwd_src_g_supported(relp, lay.H, lay.D)))
+
+
 def _merged_bwd(gsaved):
     """The one-pass edge backward (hsg_gat_bwd_src_g) covers this application's
     relation and head shape (HSG_GAT_MERGED=0: the dst + src pair, for A/B tests)."""
@@ -208,7 +227,7 @@ def _apply_bwd(grads, lay, T, saved, dout, nb_grad, nb_acc, stage=None, act_grad
     merged = gsaved[16] is not None and fsaved[11] is not None and _merged_bwd(gsaved)
     gdt = torch.bfloat16 if (merged and fsaved[4].dtype == torch.bfloat16
                              and _lib.path_option("HSG_FFN_BF16_ROWS", "1") != "0") else torch.float32
-    elug = (gsaved[16][1], torch.empty_like(fsaved[0], dtype=gdt)) \
+    elug = (gsaved[16][1], torch.empty(fsaved[0].shape, dtype=gdt, device=fsaved[0].device)) \
         if gsaved[16] is not None and fsaved[11] is not None else None
     if elug is not None and merged:
         # ... and the rho partials, so the edge backward is one source-centric pass
@@ -332,6 +351,10 @@ class _GatStack(torch.autograd.Function):
                 # (HSG_FFN_BF16_ACT=0: fp32 buffers, for the bitwise A/B test)
                 bf = (wsplits[key] is not None and wsplits[key][0].mode == "bf16" and bf16_rows_ok(d, d_hid)
                       and _lib.path_option("HSG_FFN_BF16_ACT", "1") != "0")
+                if _x16_ok(lay, rel, wsplits[key], d, d_hid):
+                    # ... and its input x as bf16 rows, pitch ceil8(d) (zero pad: the bf16-A
+                    # contract), written by the edge forward (hsg_gat_fwd_ws16)
+                    X = X.new_empty(n_app[key], rel.n_dst, (d + 7) // 8 * 8, dtype=torch.bfloat16)[:, :, :d]
                 bufs[key] = (X, X.new_empty(n_app[key], rel.n_dst, d_hid,
                                             dtype=torch.bfloat16 if bf else torch.float32))
             a = slot[key]
@@ -412,8 +435,10 @@ class _GatStack(torch.autograd.Function):
             todo = []
             DYf = DY.reshape(-1, DY.shape[2]) if DY.is_contiguous() else \
                 DY.as_strided((DY.shape[0] * DY.shape[1], DY.shape[2]), (DY.stride(1), 1))
+            Xf = X.reshape(-1, d) if X.is_contiguous() else \
+                X.as_strided((X.shape[0] * X.shape[1], d), (X.stride(1), 1))      # bf16 x rows, pitch ceil8(d)
             for p, A, B, (m, n) in ((lay.w2, DYf, Hh.view(-1, d_hid), (d, d_hid)),
-                                    (lay.w1, DH.view(-1, d_hid), X.view(-1, d), (d_hid, d))):
+                                    (lay.w1, DH.view(-1, d_hid), Xf, (d_hid, d))):
                 dw, a_w = pgrads.dst(p)
                 if dw is not None:
                     todo.append((p, A, B, m, n, dw, a_w))

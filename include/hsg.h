@@ -91,6 +91,15 @@ size_t hsg_gat_fwd_ws_floats(const hsg_rel *rel, int H, int D);
 int hsg_gat_fwd_ws(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
                    const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
                    float *l, float *ws, void *stream);
+/* hsg_gat_fwd_ws with an origin, the result x = elu(h) + origin stored as bf16 rows
+ * (round-to-nearest-even) of pitch ld16 in out16 INSTEAD of the fp32 out (out may be
+ * NULL): the bf16 GEMM mode's bf16 x rows (round 6) -- the wide FFN's A operand,
+ * LayerNorm residual and dW1 operand.  ld16 % 8 == 0, ld16 >= ceil8(H*D), out16 16-byte
+ * aligned; columns H*D .. ld16 - 1 are written zero (the bf16-A contract of
+ * hsg_gemm_bf16_psw_io).  Per element |x16 - x| <= 2^-9 |x|. */
+int hsg_gat_fwd_ws16(const hsg_rel *rel, int H, int D, int tau_mode, float slope, const float *Z,
+                     const float *sigma, const float *tau, const float *origin, float *h, float *out, float *m,
+                     float *l, float *ws, void *out16, int ld16, void *stream);
 
 /* Backward, destination-centric half: given dOut, computes
  *   G = origin_mode ? dOut * elu'(h) : dOut                      [n_dst, H*D]
@@ -353,6 +362,12 @@ int hsg_gemm_bf16_psw_io(int M, int N, int K, const void *A, int lda, const void
 int hsg_gemm_bf16_psw_elug_rho_a16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
                                    int ldc, const float *aux, const float *x, const float *origin, void *G, int ld,
                                    float *rho, int head_dim, int g_bf16, void *stream);
+/* ... with x given as bf16 rows of pitch ldx when x_bf16 != 0 (hsg_gat_fwd_ws16's rows;
+ * ldx % 8 == 0; G must be bf16 then, g_bf16 != 0): elu(h) = x - origin from the bf16 x.
+ * x_bf16 == 0: hsg_gemm_bf16_psw_elug_rho_a16 (x fp32, pitch ld). */
+int hsg_gemm_bf16_psw_elug_rho_x16(int M, int N, int K, const void *A, int lda, const void *planes, float *C,
+                                   int ldc, const float *aux, const void *x, int ldx, int x_bf16, const float *origin,
+                                   void *G, int ld, float *rho, int head_dim, int g_bf16, void *stream);
 /* Same contract as hsg_gemm_f32 (fp32 A, B, C, epilogues, split-K, colsum_part), but
  * the MFMA takes A and B rounded to bf16 (round-to-nearest-even) and accumulates in
  * fp32 (v_mfma_f32_32x32x16_bf16): the reduced-precision mode of config 5 (NYT50,
@@ -489,6 +504,16 @@ int hsg_ln_bwd_dy16(int n, int d, const float *dout, const void *y, int y_bf16, 
 int hsg_ln_fwd_y16(int n, int d, const void *y, const float *x, const float *gamma, const float *beta, float eps,
                    float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
                    void *stream);
+/* hsg_ln_fwd_y16 / hsg_ln_bwd_dy16 (bf16 y, pitch d; bf16 dy rows of pitch ld_dy) with the
+ * residual x also given as bf16 rows, pitch ldx (% 8 == 0, >= ceil8(d), 16-byte aligned):
+ * hsg_gat_fwd_ws16's rows (round 6).  out, mean, rstd, dx and the partials as hsg_ln_fwd /
+ * hsg_ln_bwd on the bf16 values of y and x; HSG_EINVAL off the vector kernels' shapes. */
+int hsg_ln_fwd_x16(int n, int d, const void *y, const void *x, int ldx, const float *gamma, const float *beta,
+                   float eps, float p_drop, const int64_t *seed, uint32_t offset, float *out, float *mean, float *rstd,
+                   void *stream);
+int hsg_ln_bwd_x16(int n, int d, const float *dout, const void *y, const void *x, int ldx, const float *gamma,
+                   const float *mean, const float *rstd, float p_drop, const int64_t *seed, uint32_t offset, void *dy,
+                   int ld_dy, float *dx, float *part, void *stream);
 
 /* ---- head projection with per-head input dropout (GATStackLayer.py:56) ----------
  * Training-mode  z_k = fc_k(dropout_k(h))  for all heads without materialising the

@@ -1,4 +1,4 @@
-"""Dev tool: A/B the bench step (cfg2 unless HSG_AB_CONFIG) under environment
+"""Dev tool: A/B the bench step (cfg2 unless HSG_AB_CONFIG; GEMM mode HSG_AB_DTYPE) under environment
 variants in ONE process: for every variant 'VAR=a,VAR2=b' (the empty string is the
 baseline) set the variables, re-capture the step into a HIP graph and time 100
 replays; rounds interleave the variants.  Also prints each variant's in-step
@@ -20,6 +20,8 @@ def main(variants):
     from hetersumgraph_amd import rng as hsg_rng
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    from hetersumgraph_amd.dense import set_gemm_dtype
+    set_gemm_dtype(os.environ.get("HSG_AB_DTYPE", "f32"))             # bench.py --dtype
     docs, G, _, _ = bench.make_shard(os.environ.get("HSG_AB_CONFIG", "cfg2"), 0, 1, 0)
     G.to(dev)
     torch.manual_seed(0)
@@ -41,7 +43,7 @@ def main(variants):
         Xs.grad = None
 
     def apply(v):
-        for k in [k for k in os.environ if k.startswith("HSG_") and k != "HSG_AB_CONFIG"]:
+        for k in [k for k in os.environ if k.startswith("HSG_") and k not in ("HSG_AB_CONFIG", "HSG_AB_DTYPE")]:
             del os.environ[k]
         for kv in filter(None, v.split(",")):
             k, val = kv.split("=", 1)
