@@ -1706,6 +1706,9 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
     __shared__ float s_acc[HSG_WAVES][512];
     __shared__ float s_dsig[HSG_WAVES][HSG_HMAX];
     __shared__ float s_dtau[HSG_WAVES][HSG_NT * HSG_HMAX];
+    // the list kernel on fp32 G keeps wave 0's d a1 sums in LDS: in registers it spilled
+    constexpr bool LDA1 = WL && !GBF;
+    __shared__ float s_da1[LDA1 ? 512 : 1];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int HD = H * D;
     const int k = lane / lph, l = lane - (lane / lph) * lph;
@@ -1713,16 +1716,19 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
     const int kc = kact ? k : H - 1, gl = kc * lph, c0 = kc * D;
     float *sd = s_dtau[wid];
     for (int i = lane; i < HSG_NT * HSG_HMAX; i += 64) sd[i] = 0.f;
+    if constexpr (LDA1)
+        if (wid == 0)
+            for (int i = lane; i < 512; i += 64) s_da1[i] = 0.f;
     wave_lds_sync();
     // rho partial addresses of head kc: rgw-column groups r0 (and r1 when the head
     // straddles two; D <= rgw), slot = head - first head of the group
     const int r0 = c0 / rgw, r1 = (c0 + D - 1) / rgw;
     const int o0 = r0 * 3 + (kc - (rgw * r0) / D), o1 = r1 * 3 + (kc - (rgw * r1) / D);
-    float da1[NE];                                // wave 0: sum_u dsigma[u,k] Z[u,k,:], (k, l) features
+    float da1[LDA1 ? 1 : NE];                       // wave 0: sum_u dsigma[u,k] Z[u,k,:], (k, l) features
     int fo[NE];                                   // the lane's features c0 + d, clamped to the head
 #pragma unroll
     for (int i = 0; i < NE; ++i) {
-        da1[i] = 0.f;
+        if constexpr (!LDA1) da1[i] = 0.f;
         fo[i] = c0 + min(l + lph * i, D - 1);
     }
 
@@ -1832,9 +1838,10 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
             // ([HD | H] per item), for the merge; its ds * Z_u into d a1 as any source's
             // (written through, sc1, when the last piece block merges in-kernel)
             float *pw = piece ? pws + (size_t)item * (HD + H) : nullptr;
+            const bool pin = PIN && pinline;              // the merge launch's kernel: plain stores
             if (kact && l == 0) {
                 if (piece) {
-                    if (pinline) st_sc1(&pw[HD + k], ds);
+                    if (pin) st_sc1(&pw[HD + k], ds);
                     else pw[HD + k] = ds;
                 } else if (dsigma) {
                     dsigma[u * H + k] = ds;
@@ -1848,16 +1855,17 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
 #pragma unroll
                     for (int w = 0; w < WPN; ++w) a += s_acc[w][f];
                     if (piece) {
-                        if (pinline) st_sc1(&pw[f], a);
+                        if (pin) st_sc1(&pw[f], a);
                         else pw[f] = a;
                     } else {
                         if (a1) a = fmaf(ds, a1[f], a);
                         dZ[(size_t)u * HD + f] = a;
                     }
-                    da1[i] = fmaf(ds, zk[i], da1[i]);
+                    if constexpr (LDA1) s_da1[f] = fmaf(ds, zk[i], s_da1[f]);    // lane-private slots
+                    else da1[i] = fmaf(ds, zk[i], da1[i]);
                 }
             }
-            if (piece && pinline) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (piece && pin) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         if constexpr (WL && PIN) {
             // a piece, merged in-kernel (round 6): the last of u's pieces to arrive sums them
@@ -1875,7 +1883,8 @@ __global__ __launch_bounds__(256, OCC) void k_gat_bwd_src_g(RelPtrs R, int H, in
     if (wid == 0 && da1_part) {                            // block partial of d a1
 #pragma unroll
         for (int i = 0; i < NE; ++i)
-            if (kact && l + lph * i < D) da1_part[(size_t)blockIdx.x * HD + fo[i]] = da1[i];
+            if (kact && l + lph * i < D)
+                da1_part[(size_t)blockIdx.x * HD + fo[i]] = LDA1 ? s_da1[fo[i]] : da1[LDA1 ? 0 : i];
     }
     // block partial of d tau (s_dtau written by lane (k, 0) of each wave; the loop's
     // last barrier orders them, this one covers a block without sources)

@@ -61,6 +61,57 @@ class TableColumn:
         return TableColumn(self.weight, self.index.to(device), self.tag)
 
 
+class EdgeScoreColumn(TableColumn):
+    """``g.edata['e']`` as the reference's WSWGAT leaves it, materialised on read.
+
+    Every head of the reference writes its attention logits
+    ``e = leaky_relu(attn_fc([z_src, z_dst, feat_fc(tfidfembed)]))`` into ``g.edata['e']``
+    on its typed edges (GATLayer.py:89-93 via ``apply_edges`` at :112 / :148), and the
+    column stays on the graph (GATLayer.py:111-115 pops only ``z`` and ``sh``).  Heads
+    run in order (GATStackLayer.py:56-58) and ``apply_edges`` writes only its rows, so
+    after a forward each typed edge holds the LAST head's logit of the LAST application
+    over its relation; the other rows keep what they held (zeros from the initializer).
+    The HIP path never forms per-edge logits, so the column keeps one ``segment`` per
+    relation (an object with ``eid`` [E_T] and ``scores()`` [E_T], see
+    ``module.GATLayer.LastHeadScores``) over an optional ``base`` tensor and computes the
+    rows only when someone reads the column.  Values are detached (the reference's
+    column carries autograd history, which no reference caller differentiates)."""
+
+    def __init__(self, n: int, segments, base=None):
+        self.n = n
+        self.segments = list(segments)
+        self.base = base
+        self.tag = "e"
+
+    @property
+    def shape(self):
+        return (self.n, 1)
+
+    def materialize(self) -> torch.Tensor:
+        dev = self.segments[0].eid.device if self.segments else (self.base.device if self.base is not None else None)
+        out = self.base.detach().clone() if self.base is not None else torch.zeros(self.n, 1, device=dev)
+        for seg in self.segments:
+            v = seg.scores().to(out.dtype).reshape(-1, *out.shape[1:])
+            out = out.index_copy(0, seg.eid.to(out.device), v.to(out.device))
+        return out
+
+    def to(self, device):
+        return EdgeScoreColumn(self.n, [s.to(device) for s in self.segments],
+                               self.base.to(device) if self.base is not None else None)
+
+
+def record_edge_scores(g, segment):
+    """Set ``g.edata['e']`` to ``segment``'s rows over whatever the column held (a later
+    segment of the same relation replaces the earlier one: its rows are the same)."""
+    f = g._eframe()
+    cur = f.cols.get("e")
+    if isinstance(cur, EdgeScoreColumn):
+        segs = [s for s in cur.segments if s.key != segment.key] + [segment]
+        f.cols["e"] = EdgeScoreColumn(f.n, segs, cur.base)
+    else:
+        f.cols["e"] = EdgeScoreColumn(f.n, [segment], cur.materialize() if isinstance(cur, TableColumn) else cur)
+
+
 def _as_index(ids, n, device):
     """Normalise a DGL id argument to an int64 tensor on ``device`` (or ALL)."""
     if isinstance(ids, slice):

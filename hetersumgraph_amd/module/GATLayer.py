@@ -18,6 +18,7 @@ from ..ffn import ffn_forward
 from ..dense import linear as native_linear
 from ..hproj import head_projection_dropout
 from ..ops import LEAKY_SLOPE, gat_aggregate, gat_heads_table, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
+from ..graph import record_edge_scores
 from ..relation import N_BOX
 
 # The reference asserts "no NaN" around every FFN (GATLayer.py:36, 43), a host sync
@@ -135,6 +136,50 @@ def edge_tau(g, rel, a3, wf, bf):
     return tau, HSG_TAU_PER_EDGE
 
 
+class LastHeadScores:
+    """One relation's rows of ``g.edata['e']`` (graph.EdgeScoreColumn): the last head's
+    logits e = leaky_relu(a1 . z_src + a3 . feat_fc(tfidfembed)) on the typed edges
+    (GATLayer.py:89-93; z_dst is the zero-initialised column there, so a2 adds
+    nothing).  Holds the application's projected features Z and the head parameters
+    (detached) and forms the rows on demand: per-edge logits are never built on the
+    HIP path.  The edge term comes from ``T`` (the [10, F] tf-idf table), ``tau_table``
+    ([11, H] per tf-idf box) or ``tau_edge`` ([E_T, H], CSR order)."""
+
+    def __init__(self, kind, rel, Z, attn, wf, bf, T=None, tau_table=None, tau_edge=None):
+        self.key = kind
+        d = rel.dev
+        self.eid, self.src, self.tf = d["eid"], d["src"], d["tf"]
+        H = attn.shape[0]
+        D = Z.shape[1] // H
+        k = H - 1
+        self.z = Z.detach()[:, k * D:]                                   # [n_src, D]
+        self.a1 = attn.detach()[k, :D]
+        self.a3 = attn.detach()[k, 2 * D:]
+        self.wf = wf.detach()[k]                                         # [D, F]
+        self.bf = bf.detach()[k] if bf is not None else None
+        self.T = T.detach() if T is not None else None
+        self.tau_table = tau_table.detach()[:, k] if tau_table is not None else None
+        self.tau_edge = tau_edge.detach()[:, k] if tau_edge is not None else None
+
+    def scores(self):
+        sig = self.z @ self.a1                                           # [n_src]
+        if self.T is not None:
+            rows = self.T @ (self.wf.t() @ self.a3)                      # [10]
+            if self.bf is not None:
+                rows = rows + (self.a3 * self.bf).sum()
+            tau = rows[self.tf.long()]
+        elif self.tau_table is not None:
+            tau = self.tau_table[self.tf.long()]
+        else:
+            tau = self.tau_edge
+        return F.leaky_relu(sig[self.src.long()] + tau, LEAKY_SLOPE)
+
+    def to(self, device):
+        c = LastHeadScores.__new__(LastHeadScores)
+        c.__dict__.update({k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in self.__dict__.items()})
+        return c
+
+
 def fused_heads(g, h, params, kind, origin=None, dropout=None):
     """All heads of one layer application in one pass (+ ELU/residual if origin).
 
@@ -156,9 +201,16 @@ def fused_heads(g, h, params, kind, origin=None, dropout=None):
         Z = native_linear(h, W)                                          # hsg_gemm_f32 (no vendor GEMM)
     T = table_weight(g)
     if T is not None and T.shape[1] == wf.shape[2]:
-        return gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, LEAKY_SLOPE)
+        out = gat_heads_table(Z, attn, T, wf, bf, origin, rel, H, D, LEAKY_SLOPE)
+        record_edge_scores(g, LastHeadScores(kind, rel, Z, attn, wf, bf, T=T))
+        return out
     tau, mode = edge_tau(g, rel, a3, wf, bf)
-    return gat_aggregate(Z, a1, tau, origin, rel, H, D, LEAKY_SLOPE, mode)
+    out = gat_aggregate(Z, a1, tau, origin, rel, H, D, LEAKY_SLOPE, mode)
+    if mode == HSG_TAU_TABLE:
+        record_edge_scores(g, LastHeadScores(kind, rel, Z, attn, wf, bf, tau_table=tau))
+    else:
+        record_edge_scores(g, LastHeadScores(kind, rel, Z, attn, wf, bf, tau_edge=tau))
+    return out
 
 
 def table_weight(g):

@@ -38,6 +38,7 @@ from . import _lib
 from . import rng as hsg_rng
 from ._lib import load, stream_of
 from .dense import elug_rho_groups, gemm, gemm_dw_slabs, gemm_slabs
+from .graph import record_edge_scores
 from .ffn import bf16_rows_ok, ffn_bwd, ffn_fwd, ffn_wsplit
 from .hproj import dropmasks, hproj_bwd, hproj_fwd, narrow_heads, transposed_weight
 from .reduce import SlabBatch
@@ -374,6 +375,15 @@ class _GatStack(torch.autograd.Function):
         for i in range(n_iter):
             run(s2w, rs, ("s", i + 1), ("w", i), ("w", i + 1))
             run(w2s, rw, ("w", i + 1), ("s", i + 1), ("s", i + 2))
+        # g.edata['e'] as the reference leaves it: the last head's logits of the last
+        # application of each relation, formed only if someone reads the column
+        from .module.GATLayer import LastHeadScores
+        last = {lay.kind: (lay, saved) for lay, saved, *_ in apps}
+        for kind in ("W2S", "S2W"):
+            if kind in last:
+                lay, saved = last[kind]
+                record_edge_scores(G, LastHeadScores(kind, G.relation(kind), saved[2][0], lay.attn, lay.wf,
+                                                     lay.bf, T=T))
         ctx.cfg, ctx.apps, ctx.bufs = cfg, apps, bufs
         ctx.params = params
         ctx.need = (w0.requires_grad, s0.requires_grad)

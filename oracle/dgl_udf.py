@@ -36,6 +36,9 @@ class UdfGraph:
         self.tffrac = torch.from_numpy(np.asarray(tffrac, np.int64))
         self.edtype = np.asarray(edtype)
         self.rel = {k: self._schedule(k) for k in ("W2S", "S2W")}
+        # edata['e'] as the reference's heads leave it (GATLayer.py:89-93, 112 / 148):
+        # each head's apply_edges writes its logits on its typed edges, the last one stays
+        self.e = torch.zeros(len(self.src), 1)
 
     def _schedule(self, kind):
         su, du = (0.0, 1.0) if kind == "W2S" else (1.0, 0.0)
@@ -67,6 +70,7 @@ def _head(g, kind, X, fc, feat_w, feat_b, attn, tfidfembed):
     z2 = torch.cat([zcol[g.src[te]], zcol[g.dst[te]], dfeat], 1)
     e = F.leaky_relu(z2 @ attn.t(), SLOPE)                                              # [E_T, 1]
     ecol = torch.zeros(len(g.src), 1, dtype=z.dtype).index_copy(0, te, e)
+    g.e = g.e.index_copy(0, te, e.detach().to(g.e.dtype))
     sh = torch.zeros(g.n, D, dtype=z.dtype)
     for nodes, mat in r["buckets"]:                                                     # degree buckets
         mb_e = ecol[mat]                                                                # [nb, deg, 1]

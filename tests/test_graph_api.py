@@ -169,3 +169,39 @@ def test_dataloader_workers_pickle_graphs():
         assert list(idx) == list(ridx)
         _same_graph(G, R)
         assert G.batch_num_nodes == R.batch_num_nodes
+
+
+def test_edge_score_column_semantics():
+    """g.edata['e'] (graph.EdgeScoreColumn): each relation's rows come from its latest
+    segment, other rows keep what the column held, and reading materialises a plain
+    [E, 1] tensor (the reference: apply_edges(edge_attention) writes only the typed
+    edges of the head, GATLayer.py:112 / 148, and the column persists)."""
+    from hetersumgraph_amd import graph as hg
+
+    class Seg:
+        def __init__(self, key, eid, val):
+            self.key, self.eid, self.val = key, torch.tensor(eid), torch.tensor(val)
+
+        def scores(self):
+            return self.val
+
+        def to(self, device):
+            return self
+
+    g = hg.DGLGraph()
+    g.add_nodes(4)
+    g.add_edges([0, 1, 2, 3, 0], [1, 2, 3, 0, 2])
+    g.edata["e"] = torch.full((5, 1), 7.0)                 # a column the caller wrote
+    hg.record_edge_scores(g, Seg("W2S", [0, 2], [1.0, 2.0]))
+    hg.record_edge_scores(g, Seg("S2W", [1], [3.0]))
+    hg.record_edge_scores(g, Seg("W2S", [0, 2], [4.0, 5.0]))   # the next W2S application
+    e = g.edata["e"]
+    assert isinstance(e, torch.Tensor) and e.shape == (5, 1)
+    assert e[:, 0].tolist() == [4.0, 3.0, 5.0, 7.0, 7.0]
+    g.edges[[3]].data["e"] = torch.tensor([[9.0]])            # a row write materialises the column
+    assert g.edata["e"][:, 0].tolist() == [4.0, 3.0, 5.0, 9.0, 7.0]
+    g2 = hg.DGLGraph()
+    g2.add_nodes(2)
+    g2.add_edges([0, 1], [1, 0])
+    hg.record_edge_scores(g2, Seg("W2S", [1], [2.5]))          # no column before: zeros elsewhere
+    assert g2.edata["e"][:, 0].tolist() == [0.0, 2.5]
