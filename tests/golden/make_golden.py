@@ -156,6 +156,73 @@ def gat_case(GAT, docs, seed, full_grads, keep_rows=None):
     return res
 
 
+# ---------------------------------------------------------- train-mode stack --
+def stack_train_case(GAT, docs, seed, drop_seed, off0=0, n_iter=2, p=0.1, keep_rows=160):
+    """The reference's own WSWGAT modules chained as HiGraph.py:99-106 (W2S, then
+    n_iter x (S2W, W2S)) in TRAIN mode, with every ``nn.Dropout`` call (H per head
+    input, GATStackLayer.py:56; one per FFN output, GATLayer.py:41) replaced by the
+    keep-mask and scale the fused stack draws for it at (drop_seed, offset):
+    oracle/masks.py, which restates the device generators bit for bit
+    (tests/test_gpu_dropout_masks.py).  The reference's code computes everything
+    else.  Outputs in fp32 and fp64, gradients of ``(s * R).sum()`` from the fp64 run."""
+    sys.path.insert(0, REPO)
+    from oracle import masks as om
+    res = {}
+    for dt in (torch.float32, torch.float64):
+        G = shim_batch(docs)
+        n_w = int((G.ndata["unit"] == 0).sum())
+        n_s = int((G.ndata["unit"] == 1).sum())
+        Xw = torch.from_numpy(weights.feature(seed, "Xw", (n_w, 300), 0.4)).to(dt).requires_grad_()
+        Xs = torch.from_numpy(weights.feature(seed, "Xs", (n_s, 64), 1.0)).to(dt).requires_grad_()
+        T = torch.from_numpy(weights.param_value(seed, "_TFembed.weight", (10, 50))).to(dt).requires_grad_()
+        wsedge = G.filter_edges(lambda e: e.data["dtype"] == 0)
+        G.edges[wsedge].data["tfidfembed"] = F.embedding(G.edata["tffrac"][wsedge], T)
+        w2s = GAT.WSWGAT(300, 64, 8, p, 512, p, 50, "W2S")
+        s2w = GAT.WSWGAT(64, 300, 6, p, 512, p, 50, "S2W")
+        weights.seed_module(w2s, seed * 100 + 1).train().to(dt)
+        weights.seed_module(s2w, seed * 100 + 2).train().to(dt)
+        calls, off = [], off0
+        for kind in ["W2S"] + ["S2W", "W2S"] * n_iter:
+            n_src, d_in, H, n_dst, d = (n_w, 300, 8, n_s, 64) if kind == "W2S" else (n_s, 64, 6, n_w, 300)
+            hk = om.hproj_keep(drop_seed, off + 1, n_src, d_in, H, p)
+            calls += [(hk[k], om.hproj_scale(p)) for k in range(H)]
+            calls.append((om.ffn_keep(drop_seed, off + 2, n_dst, d, p), om.ffn_scale(p)))
+            off += 2
+        it = iter(calls)
+
+        class MaskDropout(torch.nn.Module):
+            def forward(self, x):
+                keep, scale = next(it)
+                return x * torch.from_numpy(keep).to(x.dtype).reshape(x.shape) * scale
+
+        for mod in (w2s, s2w):
+            mod.layer.dropout = MaskDropout()
+            mod.ffn.dropout = MaskDropout()
+        w, s = Xw, w2s(G, Xw, Xs)
+        for _ in range(n_iter):
+            w = s2w(G, w, s)
+            s = w2s(G, w, s)
+        assert next(it, None) is None, "dropout calls out of step with the fused stack's draws"
+        if dt == torch.float32:
+            res["out"] = s.detach().numpy()
+    R = torch.from_numpy(np.random.default_rng(seed).standard_normal(tuple(s.shape)))
+    (s * R).sum().backward()
+    rows = np.sort(np.random.default_rng(seed).choice(n_w, size=keep_rows, replace=False))
+    res.update({"n_w": n_w, "n_s": n_s, "seed": np.array(seed), "drop_seed": np.array(drop_seed),
+                "off0": np.array(off0), "n_iter": np.array(n_iter), "p": np.array(p),
+                "out64": s.detach().numpy(), "grad_Xs": Xs.grad.numpy(), "grad_T": T.grad.numpy(),
+                "rows_w": rows, "grad_Xw_rows": Xw.grad.numpy()[rows],
+                "proj_grad_Xw": projections(Xw.grad, seed, "grad_Xw")})
+    for tag, mod in (("w2s", w2s), ("s2w", s2w)):
+        for name, q in mod.named_parameters():
+            key = f"grad.{tag}.{name}"
+            if q.numel() <= 40000:
+                res[key] = q.grad.numpy()
+            else:
+                res["proj." + key] = projections(q.grad, seed, key)
+    return res
+
+
 # --------------------------------------------------------------- model level --
 class HPS:
     def __init__(self, **kw):
@@ -267,6 +334,12 @@ def main():
                  "vocab_size": np.array(5000), "doc_max_timesteps": np.array(80)}
         np.savez_compressed(os.path.join(HERE, "model_hsg_cfg5.npz"), **graph_arrays(cdocs), **compact(res),
                             **extra, **meta)
+    if args.only == "stack_train_cfg2":
+        # the TIMED configuration: the fused stack's train mode (dropout 0.1, masks
+        # injected, see stack_train_case) on the bench's full cfg2 batch (159,040 edges)
+        cdocs = sort_by_sentences(synth.make_batch_docs("cfg2", seed=0))
+        res = stack_train_case(GAT, cdocs, 46, 1046)
+        np.savez_compressed(os.path.join(HERE, "stack_train_cfg2.npz"), **graph_arrays(cdocs), **compact(res), **meta)
     if args.only is not None:
         return
 
