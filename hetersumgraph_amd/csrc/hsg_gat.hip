@@ -612,6 +612,207 @@ __global__ __launch_bounds__(256) void k_gat_fwd_merge(RelPtrs R, int H, int D, 
 }
 
 #ifdef HSG_DEV
+// ---------------------------------------------------- forward, destination tiles ----
+// (round 6, dev: measured slower -- 24.1 / 27.7 us with 48- / 24-destination tiles
+// against 16.3 us for k_gat_fwd on the cfg2 S2W pass) The short-segment
+// forward (one destination per wave, the S2W words: ~2
+// sentence edges each) by tiles of kTileW consecutive destinations per block.  The
+// block first stages everything its destinations' edges will read -- their indptr
+// range, the (source, box) of every edge, and the source rows Z and logits sigma of
+// the window [s0, s0 + kTileZ) around the smallest source the tile touches (documents
+// are contiguous in node order, so one document's sentences cover a tile) -- with
+// coalesced loads, then its 8 waves walk the tile's destinations reading scores and
+// gathered rows from LDS: the per-destination chain has no dependent global load
+// left (the residual row is requested one destination ahead).  Sources outside the
+// window and edges past kTileE are read from global memory (flat pointers), so any
+// graph is covered.  Per destination the arithmetic is k_gat_fwd's (WPN = 1): the same
+// score order, online (max, sum) merge and gather order -- bitwise equal results.
+// blocks b run on XCD b % 8: XCD x takes the contiguous run x of the tiles (a bijection)
+__device__ __forceinline__ int xcd_run(int b, int total) {
+    const int x = b & 7, j = b >> 3, per = total >> 3, rem = total & 7;
+    return x * per + min(x, rem) + j;
+}
+
+constexpr int kTileW = 48;                 // destinations per block
+constexpr int kTileZ = 48;                 // staged source rows
+constexpr int kTileE = 512;                // staged edges
+constexpr int kTileCh = 16;                // edges per score / gather chunk
+constexpr int kTileWaves = 8;
+
+template <int NF, int TAU_MODE, bool O16 = false, int TW = kTileW>
+__global__ __launch_bounds__(512, 4) void k_gat_fwd_tile(RelPtrs R, int H, int D, int lph, float slope,
+                                                         const float *__restrict__ Z,
+                                                         const float *__restrict__ sigma,
+                                                         const float *__restrict__ tau,
+                                                         const float *__restrict__ origin,
+                                                         float *__restrict__ hout, float *__restrict__ out,
+                                                         float *__restrict__ mout, float *__restrict__ lout,
+                                                         __bf16 *__restrict__ out16, int ld16, int ntiles) {
+    constexpr int HDP = 64 * NF;           // staged row pitch (floats)
+    __shared__ __attribute__((aligned(16))) float sZ[kTileZ * HDP];
+    __shared__ float sSig[kTileZ * HSG_HMAX];
+    __shared__ int sSrc[kTileE];
+    __shared__ int sTau[kTileE];
+    __shared__ int sPtr[TW + 1];
+    __shared__ float s_alpha[kTileWaves][kTileCh * HSG_HMAX];
+    __shared__ int s_nb[kTileWaves][kTileCh];
+    __shared__ int s_min[kTileWaves];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int HD = H * D;
+    const int t = xcd_run((int)blockIdx.x, ntiles);       // XCD-local runs of tiles
+    const int v0 = t * TW, v1 = min(R.n_dst, v0 + TW), nv = v1 - v0;
+    // 1. the tile's indptr range, then its edges' (source, box) and the source window
+    for (int i = threadIdx.x; i <= nv; i += blockDim.x) sPtr[i] = R.indptr[v0 + i];
+    __syncthreads();
+    const int e0 = sPtr[0], ne = sPtr[nv] - e0, nes = min(ne, kTileE);
+    int mn = 0x7fffffff;
+    for (int i = threadIdx.x; i < nes; i += blockDim.x) {
+        const int u = R.src[e0 + i];
+        sSrc[i] = u;
+        sTau[i] = tau_row<TAU_MODE>(R, e0 + i);
+        mn = min(mn, u);
+    }
+    for (int o = 32; o >= 1; o >>= 1) mn = min(mn, __shfl_xor(mn, o));
+    if (lane == 0) s_min[wid] = mn;
+    __syncthreads();
+    int s0 = s_min[0];
+#pragma unroll
+    for (int w = 1; w < kTileWaves; ++w) s0 = min(s0, s_min[w]);
+    if (nes == 0) s0 = 0;
+    const int nz = nes > 0 ? min(kTileZ, R.n_src - s0) : 0;  // window rows [s0, s0 + nz)
+    if (HD % 4 == 0) {
+        const int q = HD / 4;                                  // float4 quads per row
+        for (int i = threadIdx.x; i < nz * q; i += blockDim.x) {
+            const int r = i / q, c = (i - r * q) * 4;
+            *reinterpret_cast<float4 *>(&sZ[r * HDP + c]) =
+                *reinterpret_cast<const float4 *>(Z + (size_t)(s0 + r) * HD + c);
+        }
+    } else {
+        for (int i = threadIdx.x; i < nz * HD; i += blockDim.x) {
+            const int r = i / HD, c = i - r * HD;
+            sZ[r * HDP + c] = Z[(size_t)(s0 + r) * HD + c];
+        }
+    }
+    for (int i = threadIdx.x; i < nz * H; i += blockDim.x) sSig[i] = sigma[(size_t)s0 * H + i];
+    __syncthreads();
+
+    // 2. the destinations, one per wave at a time
+    const int k = lane / lph, l = lane - (lane / lph) * lph;
+    const bool kact = k < H;
+    int fh[NF], fo[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+        const int f = lane + 64 * i;
+        fh[i] = f < HD ? div_small(f, 1.f / (float)D) : 0;
+        fo[i] = f < HD ? f : HD - 1;
+    }
+    float *sa = s_alpha[wid];
+    int *sn = s_nb[wid];
+    // a source row / logit: from the window when staged, else from global memory
+    auto zrow = [&](int u) -> const float * {
+        return (unsigned)(u - s0) < (unsigned)nz ? &sZ[(u - s0) * HDP] : Z + (size_t)u * HD;
+    };
+    auto sig = [&](int u, int kk) -> float {
+        return (unsigned)(u - s0) < (unsigned)nz ? sSig[(u - s0) * H + kk] : sigma[(size_t)u * H + kk];
+    };
+    auto edge = [&](int e, int &u, int &tr) {               // e relative to e0
+        if (e < kTileE) { u = sSrc[e]; tr = sTau[e]; }
+        else { u = R.src[e0 + e]; tr = tau_row<TAU_MODE>(R, e0 + e); }
+    };
+    float orgn[NF];
+    int vv = v0 + wid;
+    if (origin && vv < v1) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) orgn[i] = origin[(size_t)vv * HD + fo[i]];
+    }
+    for (; vv < v1; vv += kTileWaves) {
+        const int v = __builtin_amdgcn_readfirstlane(vv);
+        const int beg = sPtr[v - v0] - e0, end = sPtr[v - v0 + 1] - e0;
+        const int c = R.phantom[v];
+        float org[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) org[i] = orgn[i];
+        const int vn = v + kTileWaves;                       // the next destination's residual row
+        if (origin && vn < v1) {
+#pragma unroll
+            for (int i = 0; i < NF; ++i) orgn[i] = origin[(size_t)vn * HD + fo[i]];
+        }
+        const int n1 = end - beg;
+        const bool single = n1 <= kTileCh;
+        float mx = -INFINITY, sm = 0.f;
+        if (kact) {
+            for (int j = l; j < n1; j += lph) {
+                int u, tr;
+                edge(beg + j, u, tr);
+                const float s = leaky(sig(u, k) + tau[tr * H + k], slope);
+                if (single) {
+                    sa[j * H + k] = s;
+                    if (k == 0) sn[j] = u;
+                }
+                if (s > mx) { sm = sm * __expf(mx - s) + 1.f; mx = s; }
+                else sm += __expf(s - mx);
+            }
+        }
+        for (int o = lph >> 1; o >= 1; o >>= 1) {
+            const float om = __shfl_xor(mx, o), os = __shfl_xor(sm, o);
+            lse_merge(mx, sm, om, os);
+        }
+        if (c > 0) lse_merge(mx, sm, 0.f, (float)c);
+        const bool any = end > beg;
+        const float inv = any ? 1.f / sm : 0.f;
+        float acc[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) acc[i] = 0.f;
+        for (int cb = 0; cb < n1; cb += kTileCh) {
+            const int n = min(kTileCh, n1 - cb);
+            if (kact) {
+                for (int j = l; j < n; j += lph) {
+                    float s;
+                    if (single) {
+                        s = sa[j * H + k];
+                    } else {
+                        int u, tr;
+                        edge(beg + cb + j, u, tr);
+                        s = leaky(sig(u, k) + tau[tr * H + k], slope);
+                        if (k == 0) sn[j] = u;
+                    }
+                    sa[j * H + k] = __expf(s - mx) * inv;
+                }
+            }
+            wave_lds_sync();
+            for (int j = 0; j < n; ++j) {
+                const float *xr = zrow(sn[j]);
+                float xv[NF];
+#pragma unroll
+                for (int i = 0; i < NF; ++i) xv[i] = xr[fo[i]];
+#pragma unroll
+                for (int i = 0; i < NF; ++i) acc[i] = fmaf(sa[j * H + fh[i]], xv[i], acc[i]);
+            }
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int f = lane + 64 * i;
+            if (f < HD) {
+                const size_t o = (size_t)v * HD + f;
+                const float hv = acc[i];
+                if (hout) hout[o] = hv;
+                if (origin) {
+                    const float xo = elu1(hv) + org[i];
+                    if constexpr (O16) out16[(size_t)v * ld16 + f] = (__bf16)xo;
+                    else out[o] = xo;
+                }
+            } else if (O16 && f < ld16) {
+                out16[(size_t)v * ld16 + f] = (__bf16)0.f;
+            }
+        }
+        if (kact && l == 0) {
+            mout[v * H + k] = any ? mx : 0.f;
+            lout[v * H + k] = any ? sm : 1.f;
+        }
+    }
+}
+
 // Launch floor probe (dev, round 6): the same grid as the edge launch
 // it replaces, every wave reads its first index word and stores nothing, so the step
 // trace shows what dispatch, ramp and drain of that grid cost in the step.
@@ -2314,6 +2515,38 @@ int piece_inline() {
     return e ? atoi(e) : 1;
 }
 
+#ifdef HSG_DEV
+// the destination-tile forward (k_gat_fwd_tile) for short segments; dev: HSG_GAT_FWD_TILE
+int fwd_tile() {
+    int v = 0;
+    if (const char *e = HSG_DEV_ENV("HSG_GAT_FWD_TILE")) v = atoi(e);
+    return v;
+}
+
+template <int TAU, bool O16>
+int tile_dispatch(int nf, hipStream_t st, RelPtrs R, int H, int D, int lph, float slope, const float *Z,
+                  const float *sg, const float *tau, const float *org, float *h, float *out, float *m, float *l,
+                  __bf16 *out16, int ld16) {
+    const int tw = fwd_tile() == 2 ? 24 : kTileW;
+    const int ntiles = (R.n_dst + tw - 1) / tw;
+#define HSG_FT(NF_)                                                                                        \
+    case NF_:                                                                                              \
+        if (tw == 24)                                                                                      \
+            HSG_KLAUNCH(true, true, (k_gat_fwd_tile<NF_, TAU, O16, 24>), dim3((unsigned)ntiles), dim3(512), st, R, H, \
+                        D, lph, slope, Z, sg, tau, org, h, out, m, l, out16, ld16, ntiles);                \
+        else                                                                                               \
+            HSG_KLAUNCH(true, true, (k_gat_fwd_tile<NF_, TAU, O16>), dim3((unsigned)ntiles), dim3(512), st, R, H, \
+                        D, lph, slope, Z, sg, tau, org, h, out, m, l, out16, ld16, ntiles);                \
+        break;
+    switch (nf) {
+        HSG_FT(1) HSG_FT(2) HSG_FT(3) HSG_FT(4) HSG_FT(5)
+        default: return HSG_EINVAL;
+    }
+#undef HSG_FT
+    return launch_status();
+}
+#endif
+
 int fwd_pf() {
     const char *e = HSG_DEV_ENV("HSG_GAT_FWD_PF");
     return e ? (atoi(e) == 0 ? 0 : atoi(e) == 1 ? 1 : atoi(e) == 3 ? 3 : 2) : 2;
@@ -2553,6 +2786,19 @@ static int gat_fwd_impl(const hsg_rel *rel, int H, int D, int tau_mode, float sl
                                                              origin, h, out, m, l, nullptr, true, 0, out16, ld16);
                 return fwd_dispatch<HSG_TAU_PER_EDGE, 1, 7>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau,
                                                             origin, h, out, m, l, nullptr, true, 0, out16, ld16);
+            }
+#endif
+#ifdef HSG_DEV
+            if (fwd_tile() && nf <= 5 && lph <= 64) {          // destination tiles (round 6, dev)
+                const bool tt = tau_mode == HSG_TAU_TABLE;
+                return tt ? (out16 ? tile_dispatch<HSG_TAU_TABLE, true>(nf, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                       origin, h, out, m, l, out16, ld16)
+                                   : tile_dispatch<HSG_TAU_TABLE, false>(nf, st, R, H, D, lph, slope, Z, sigma, tau,
+                                                                        origin, h, out, m, l, out16, ld16))
+                          : (out16 ? tile_dispatch<HSG_TAU_PER_EDGE, true>(nf, st, R, H, D, lph, slope, Z, sigma,
+                                                                          tau, origin, h, out, m, l, out16, ld16)
+                                   : tile_dispatch<HSG_TAU_PER_EDGE, false>(nf, st, R, H, D, lph, slope, Z, sigma,
+                                                                           tau, origin, h, out, m, l, out16, ld16));
             }
 #endif
 #define HSG_F2(TAU, O16_) fwd_dispatch<TAU, 1, 7, 2, false, O16_>(nf, grid, st, R, H, D, lph, slope, Z, sigma, tau, \
