@@ -6,16 +6,20 @@ Same constructor signature and ``forward(g, w, s)`` contract:
   returns the new supernode state [n_unit1, out_dim];
 * ``layerType="S2W"``: origin = w, neighbour = s; returns the new word state
   [n_unit0, out_dim];
+* ``layerType="S2S"``: w and s must be equal (GAT.py:50); origin = neighbour = s,
+  heads :class:`MultiHeadSGATLayer` (sentence -> sentence over all in-edges of the
+  unit-1 nodes, GATLayer.py:49-78); returns [n_unit1, out_dim];
 * ``out = FFN(elu(MultiHeadLayer(g, neighbour)) + origin)``.
 
 The ELU and residual run inside the edge kernel's epilogue.
 """
 from __future__ import annotations
 
+import torch
 import torch.nn as nn
 
 from .GATLayer import PositionwiseFeedForward, SWGATLayer, WSGATLayer
-from .GATStackLayer import MultiHeadLayer
+from .GATStackLayer import MultiHeadLayer, MultiHeadSGATLayer
 
 
 class WSWGAT(nn.Module):
@@ -31,9 +35,8 @@ class WSWGAT(nn.Module):
             self.layer = MultiHeadLayer(in_dim, head_dim, num_heads, attn_drop_out, feat_embed_size,
                                         layer=SWGATLayer)
         elif layerType == "S2S":
-            # GAT.py:38-39 builds MultiHeadSGATLayer, which no model constructs
-            # (SURVEY §2 rows 1-2); it is outside this build's hot path.
-            raise NotImplementedError("S2S (SGATLayer) is not part of the WSWGAT hot path")
+            # GAT.py:38-39; no model constructs it
+            self.layer = MultiHeadSGATLayer(in_dim, head_dim, num_heads, attn_drop_out)
         else:
             raise NotImplementedError("GAT Layer has not been implemented!")
         self.ffn = PositionwiseFeedForward(out_dim, ffn_inner_hidden_size, ffn_drop_out)
@@ -41,6 +44,10 @@ class WSWGAT(nn.Module):
     def forward(self, g, w, s):
         if self.layerType == "W2S":
             origin, neighbor = s, w
+        elif self.layerType == "S2S":
+            if w is not s and not torch.equal(w, s):     # GAT.py:50 (a host sync there too)
+                raise AssertionError("S2S: w and s differ")
+            origin, neighbor = w, s
         else:
             origin, neighbor = w, s
         h = self.layer(g, neighbor, origin=origin)   # elu(heads) + origin, fused

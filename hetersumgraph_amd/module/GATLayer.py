@@ -19,7 +19,7 @@ from ..dense import linear as native_linear
 from ..hproj import head_projection_dropout
 from ..ops import LEAKY_SLOPE, gat_aggregate, gat_heads_table, HSG_TAU_PER_EDGE, HSG_TAU_TABLE
 from ..graph import record_edge_scores
-from ..relation import N_BOX
+from ..relation import N_BOX, edge_dst
 
 # The reference asserts "no NaN" around every FFN (GATLayer.py:36, 43), a host sync
 # per call.  Same error behaviour behind a switch (default off: it would serialise
@@ -106,6 +106,121 @@ class SWGATLayer(_HeadParams):
 
     kind = "S2W"
     feat_bias = True
+
+
+class SGATLayer(nn.Module):
+    """Sentence -> sentence head (GATLayer.py:49-78): ``fc`` and ``attn_fc`` over
+    [z_src, z_dst], no edge feature.  Only ``WSWGAT(layerType="S2S")`` builds it
+    (GAT.py:38-39), through :class:`..GATStackLayer.MultiHeadSGATLayer`, which moves
+    the values into fused tensors and ``bind``s the head like ``_HeadParams``."""
+
+    kind = "S2S"
+
+    def __init__(self, in_dim, out_dim, weight=0):
+        super().__init__()
+        self.weight = weight
+        self.fc = nn.Linear(in_dim, out_dim, bias=False)
+        self.attn_fc = nn.Linear(2 * out_dim, 1, bias=False)
+        self._index = 0
+
+    def bind(self, parent, index):
+        del self.fc, self.attn_fc
+        object.__setattr__(self, "_parent_layer", parent)
+        self._index = index
+
+    def params(self):
+        """(fc_weight [D, in], attn_weight [1, 2D])."""
+        p = self.__dict__.get("_parent_layer")
+        if p is None:
+            return self.fc.weight, self.attn_fc.weight
+        k, D = self._index, p.head_dim
+        return p.fc_weight[k * D:(k + 1) * D], p.attn_weight[k:k + 1]
+
+    def forward(self, g, h):
+        """One head on its own (reference signature): [n_unit1, out_dim]."""
+        return sgat_heads(g, h, self.params(), origin=None, dropout=None)
+
+
+def sgat_heads(g, h, params, origin=None, dropout=None):
+    """All S2S heads in one pass of the WSWGAT edge kernel (+ ELU/residual if origin).
+
+    What the reference computes per head (GATLayer.py:71-78): z = fc(h) on the unit-1
+    nodes (words keep the zero-initialised column); e = leaky(a1.z_src + a2.z_dst) on
+    the dtype-0 edges; a pull onto every unit-1 node over ALL its in-edges.  On those
+    in-edges:
+      * from a unit-1 node (s->s, s->doc): e is never written there (0), message z_u;
+      * from a word (w->s, w->doc; dtype 0): e = leaky(a2.z_v) =: p_v for every such
+        edge of v (z_src = 0), message 0.
+    That is the S2S relation (relation.KINDS) with c_v = #word in-edges as phantoms,
+    except that the phantoms score p_v instead of 0.  Shifting every score of v by
+    -p_v (softmax is shift-invariant) gives phantoms 0 and typed edges -p_v, which the
+    kernel's per-edge tau mode expresses with sigma = 0 and tau_e = t(p_v), t chosen
+    so leaky(t) = -p_v.  The gradient reaches p (and a2, Z) through tau by autograd.
+
+    ``params``: a MultiHeadSGATLayer or (fc_weight [H*D, in], attn_weight [H, 2D])."""
+    rel = g.relation("S2S")
+    W, attn = params.fused_params()[:2] if hasattr(params, "fused_params") else params
+    H = attn.shape[0]
+    D = W.shape[0] // H
+    if attn.shape[1] != 2 * D:
+        raise ValueError(f"S2S attn_fc has {attn.shape[1]} inputs, expected 2 * {D}")
+    if h.shape[0] != rel.n_src:
+        raise ValueError(f"S2S: input has {h.shape[0]} rows, graph has {rel.n_src} unit-1 nodes")
+    if dropout is not None and dropout.training and dropout.p > 0:
+        Z = head_projection_dropout(h, W, H, D, dropout.p)
+    else:
+        Z = native_linear(h, W)
+    p = F.leaky_relu((Z.view(-1, H, D) * attn[:, D:]).sum(-1), LEAKY_SLOPE)       # [n, H]
+    t = torch.where(p > 0, p * (-1.0 / LEAKY_SLOPE), -p)                           # leaky(t) = -p
+    tau = t[edge_dst(rel)]                                                         # [E_T, H]
+    out = gat_aggregate(Z, Z.new_zeros(H, D), tau, origin, rel, H, D, LEAKY_SLOPE, HSG_TAU_PER_EDGE)
+    record_edge_scores(g, SGATScores(g, Z, attn))
+    return out
+
+
+class SGATScores:
+    """The S2S rows of ``g.edata['e']``: the last head's e = leaky(a1.z_src + a2.z_dst)
+    on every dtype-0 edge (GATLayer.py:56-59, 74-75), z = 0 on words.  Formed on read,
+    like :class:`LastHeadScores`."""
+
+    key = "S2S"
+
+    def __init__(self, g, Z, attn):
+        self.eid, self.srank, self.drank = _dtype0_edges(g)
+        H = attn.shape[0]
+        D = Z.shape[1] // H
+        self.z = Z.detach()[:, (H - 1) * D:]
+        self.a = attn.detach()[H - 1]
+
+    def scores(self):
+        D = self.z.shape[1]
+        zero = self.z.new_zeros(1)
+        s1 = torch.cat([self.z @ self.a[:D], zero])                     # row n_s: a word
+        s2 = torch.cat([self.z @ self.a[D:], zero])
+        return F.leaky_relu(s1[self.srank] + s2[self.drank], LEAKY_SLOPE)
+
+    def to(self, device):
+        c = SGATScores.__new__(SGATScores)
+        c.__dict__.update({k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in self.__dict__.items()})
+        return c
+
+
+def _dtype0_edges(g):
+    """(eid, src rank, dst rank) of the dtype-0 edges (GATLayer.py:68), ranks among the
+    unit-1 nodes with n_unit1 for a word; cached per graph and device."""
+    key = ("s2s_e", str(g.device))
+    if key not in g._rel_cache:
+        g._flush()
+        ef = g._eframe().cols
+        if "dtype" not in ef:
+            raise KeyError("dtype")   # edges.data['dtype'] in GATLayer.py:68
+        is1 = g._nframe.cols["unit"] == 1
+        rank = torch.cumsum(is1.long(), 0) - 1
+        rank = torch.where(is1, rank, is1.sum())
+        eid = (ef["dtype"] == 0).nonzero().view(-1)
+        src, dst = g._src_t(), g._dst_t()
+        g._rel_cache[key] = (eid, rank[src[eid]], rank[dst[eid]])
+    return g._rel_cache[key]
 
 
 def edge_tau(g, rel, a3, wf, bf):

@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from .GATLayer import fused_heads
+from .GATLayer import SGATLayer, fused_heads, sgat_heads
 
 _FUSED = ("fc_weight", "attn_weight", "feat_weight", "feat_bias")
 
@@ -86,6 +86,52 @@ class MultiHeadLayer(nn.Module):
         return fused_heads(g, h, self, self.kind, origin=origin, dropout=self.dropout)
 
 
+class MultiHeadSGATLayer(nn.Module):
+    """Multi-head S2S wrapper (reference: module/GATStackLayer.py:27-44), fused like
+    :class:`MultiHeadLayer`: ``fc_weight`` [H*D, in] and ``attn_weight`` [H, 2D]
+    (row k = heads.k.attn_fc.weight over [z_src, z_dst]); state_dict speaks the
+    reference's per-head keys ``heads.{k}.fc.weight`` / ``heads.{k}.attn_fc.weight``."""
+
+    kind = "S2S"
+
+    def __init__(self, in_dim, out_dim, num_heads, attn_drop_out, merge="cat"):
+        super().__init__()
+        if merge != "cat":
+            raise NotImplementedError("only merge='cat' is used by WSWGAT (GAT.py:38)")
+        heads = [SGATLayer(in_dim, out_dim) for _ in range(num_heads)]
+        self.merge = merge
+        self.dropout = nn.Dropout(attn_drop_out)
+        self.num_heads, self.head_dim = num_heads, out_dim
+        with torch.no_grad():
+            self.fc_weight = nn.Parameter(torch.cat([h.fc.weight for h in heads], 0).clone())
+            self.attn_weight = nn.Parameter(torch.cat([h.attn_fc.weight for h in heads], 0).clone())
+        self.register_parameter("feat_weight", None)
+        self.register_parameter("feat_bias", None)
+        for k, h in enumerate(heads):
+            h.bind(self, k)
+        self.heads = nn.ModuleList(heads)
+        self._register_state_dict_hook(_to_reference_keys)
+        self._register_load_state_dict_pre_hook(_from_reference_keys, with_module=True)
+
+    def head_views(self, k):
+        D = self.head_dim
+        return {"fc.weight": self.fc_weight[k * D:(k + 1) * D], "attn_fc.weight": self.attn_weight[k:k + 1]}
+
+    def reference_named_grads(self, prefix=""):
+        D = self.head_dim
+        g = lambda p, sl: p.grad[sl] if p.grad is not None else None
+        for k in range(self.num_heads):
+            yield f"{prefix}heads.{k}.fc.weight", g(self.fc_weight, slice(k * D, (k + 1) * D))
+            yield f"{prefix}heads.{k}.attn_fc.weight", g(self.attn_weight, slice(k, k + 1))
+
+    def fused_params(self):
+        return self.fc_weight, self.attn_weight, None, None
+
+    def forward(self, g, h, origin=None):
+        """[n_unit1, H*out_dim] head concat; with ``origin`` elu(heads) + origin."""
+        return sgat_heads(g, h, self, origin=origin, dropout=self.dropout)
+
+
 def _to_reference_keys(module, state_dict, prefix, local_metadata):
     for name in _FUSED:
         state_dict.pop(prefix + name, None)
@@ -103,7 +149,8 @@ def _from_reference_keys(module, state_dict, prefix, local_metadata, strict, mis
         return
     state_dict[prefix + "fc_weight"] = torch.cat([state_dict.pop(key(k, "fc.weight")) for k in range(H)], 0)
     state_dict[prefix + "attn_weight"] = torch.cat([state_dict.pop(key(k, "attn_fc.weight")) for k in range(H)], 0)
-    state_dict[prefix + "feat_weight"] = torch.stack([state_dict.pop(key(k, "feat_fc.weight")) for k in range(H)])
+    if module.feat_weight is not None:
+        state_dict[prefix + "feat_weight"] = torch.stack([state_dict.pop(key(k, "feat_fc.weight")) for k in range(H)])
     if module.feat_bias is not None:
         state_dict[prefix + "feat_bias"] = torch.stack([state_dict.pop(key(k, "feat_fc.bias")) for k in range(H)])
 
@@ -115,7 +162,7 @@ def reference_named_grads(model):
     fused_ids = set()
     out = []
     for mname, mod in model.named_modules():
-        if isinstance(mod, MultiHeadLayer):
+        if isinstance(mod, (MultiHeadLayer, MultiHeadSGATLayer)):
             out.extend(mod.reference_named_grads(mname + "." if mname else ""))
             fused_ids |= {id(p) for p in mod.fused_params() if p is not None}
     for n, p in model.named_parameters():

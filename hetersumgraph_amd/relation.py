@@ -28,7 +28,10 @@ import torch
 N_BOX = 10
 ZERO_ROW = 10
 
-KINDS = {"W2S": (0.0, 1.0), "S2W": (1.0, 0.0)}
+KINDS = {"W2S": (0.0, 1.0), "S2W": (1.0, 0.0), "S2S": (1.0, 1.0)}
+# the relations of the two models' layers (built on every batch by DGLGraph.to);
+# S2S (GAT.py:38-39, no model constructs it) is built on first use
+HOT_KINDS = ("W2S", "S2W")
 
 
 class Relation:
@@ -182,6 +185,17 @@ def build_relation(kind, src, dst, unit, tffrac=None, edtype=None):
     return Relation.on_device(kind, n_src, n_dst, d, E)
 
 
+def edge_dst(rel):
+    """Destination rank of every typed edge in CSR order ([E_T] int64), built on first
+    use and kept with the relation's device arrays (the S2S score shift reads it)."""
+    d = rel.dev
+    if "edst" not in d:
+        ip = d["indptr"].long()
+        d["edst"] = torch.repeat_interleave(torch.arange(rel.n_dst, device=ip.device), ip[1:] - ip[:-1],
+                                            output_size=rel.n_typed)
+    return d["edst"]
+
+
 def attach_work_lists(d, n_src, n_dst, n_typed):
     """Add the CSR / CSC work lists (``dwork`` / ``swork``) of a relation's device arrays
     ``d`` when some segment is long enough to be split (hsg_rel_work)."""
@@ -225,5 +239,5 @@ def prefetch_relations(g, device):
     """Called by ``DGLGraph.to``: build both relations once per batch, on the device."""
     if "unit" not in g._nframe.cols:
         return
-    for kind in KINDS:
+    for kind in HOT_KINDS:
         get_relation(g, kind)

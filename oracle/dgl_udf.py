@@ -35,13 +35,13 @@ class UdfGraph:
         self.n = len(self.unit)
         self.tffrac = torch.from_numpy(np.asarray(tffrac, np.int64))
         self.edtype = np.asarray(edtype)
-        self.rel = {k: self._schedule(k) for k in ("W2S", "S2W")}
+        self.rel = {k: self._schedule(k) for k in ("W2S", "S2W", "S2S")}
         # edata['e'] as the reference's heads leave it (GATLayer.py:89-93, 112 / 148):
         # each head's apply_edges writes its logits on its typed edges, the last one stays
         self.e = torch.zeros(len(self.src), 1)
 
     def _schedule(self, kind):
-        su, du = (0.0, 1.0) if kind == "W2S" else (1.0, 0.0)
+        su, du = {"W2S": (0.0, 1.0), "S2W": (1.0, 0.0), "S2S": (1.0, 1.0)}[kind]
         src, dst = self.src.numpy(), self.dst.numpy()
         s_nodes = np.nonzero(self.unit == su)[0]
         d_nodes = np.nonzero(self.unit == du)[0]
@@ -80,15 +80,40 @@ def _head(g, kind, X, fc, feat_w, feat_b, attn, tfidfembed):
     return sh[r["d_nodes"]]
 
 
-def wswgat(g, kind, Xw, Xs, p, tfidfembed, prefix="", drop=0.0, training=False):
-    """WSWGAT.forward (GAT.py:45-59) on the UDF-structured CPU path."""
+def _sgat_head(g, X, fc, attn):
+    """SGATLayer.forward (GATLayer.py:71-78): z on the unit-1 nodes (zero column
+    elsewhere), e = leaky(attn_fc([z_src, z_dst])) written on the dtype-0 edges
+    (GATLayer.py:56-59, 68, 74), pull over ALL in-edges of the unit-1 nodes reading
+    the edge column (edges never written hold the zero initializer)."""
+    r = g.rel["S2S"]
+    z = X @ fc.t()
+    D = z.shape[1]
+    zcol = torch.zeros(g.n, D, dtype=z.dtype).index_copy(0, r["s_nodes"], z)
+    te = torch.from_numpy(np.nonzero(g.edtype == 0)[0])
+    e = F.leaky_relu(torch.cat([zcol[g.src[te]], zcol[g.dst[te]]], 1) @ attn.t(), SLOPE)
+    ecol = torch.zeros(len(g.src), 1, dtype=z.dtype).index_copy(0, te, e)
+    g.e = g.e.index_copy(0, te, e.detach().to(g.e.dtype))
+    sh = torch.zeros(g.n, D, dtype=z.dtype)
+    for nodes, mat in r["buckets"]:
+        alpha = F.softmax(ecol[mat], dim=1)
+        sh = sh.index_copy(0, nodes, torch.sum(alpha * zcol[g.src[mat]], dim=1))
+    return sh[r["d_nodes"]]
+
+
+def wswgat(g, kind, Xw, Xs, p, tfidfembed, prefix="", drop=0.0, training=False, head_masks=None):
+    """WSWGAT.forward (GAT.py:45-59) on the UDF-structured CPU path.  ``head_masks``:
+    per-head input multipliers (keep / (1 - p)) replacing F.dropout of the heads."""
     origin, neighbor = (Xs, Xw) if kind == "W2S" else (Xw, Xs)
     outs = []
     i = 0
     while f"{prefix}layer.heads.{i}.fc.weight" in p:
         q = lambda n: p.get(f"{prefix}layer.heads.{i}.{n}")
-        outs.append(_head(g, kind, F.dropout(neighbor, drop, training), q("fc.weight"), q("feat_fc.weight"),
-                          q("feat_fc.bias"), q("attn_fc.weight"), tfidfembed))
+        x = neighbor * head_masks[i] if head_masks is not None else F.dropout(neighbor, drop, training)
+        if kind == "S2S":
+            outs.append(_sgat_head(g, x, q("fc.weight"), q("attn_fc.weight")))
+        else:
+            outs.append(_head(g, kind, x, q("fc.weight"), q("feat_fc.weight"), q("feat_fc.bias"),
+                              q("attn_fc.weight"), tfidfembed))
         i += 1
     h = F.elu(torch.cat(outs, 1)) + origin
     x = h.t().unsqueeze(0)                                                             # Conv1d layout

@@ -29,7 +29,7 @@ SLOPE = 0.01
 
 def typed_relation(kind, src, dst, unit, tffrac, edtype):
     """Typed edges and phantom counts of one layer type (numpy, edge-id order)."""
-    su, du = (0.0, 1.0) if kind == "W2S" else (1.0, 0.0)
+    su, du = {"W2S": (0.0, 1.0), "S2W": (1.0, 0.0), "S2S": (1.0, 1.0)}[kind]
     unit = np.asarray(unit)
     src = np.asarray(src, np.int64)
     dst = np.asarray(dst, np.int64)

@@ -156,6 +156,30 @@ def gat_case(GAT, docs, seed, full_grads, keep_rows=None):
     return res
 
 
+def s2s_case(GAT, docs, seed, d=64, H=8):
+    """WSWGAT(layerType="S2S") (GAT.py:38-39, 49-51: MultiHeadSGATLayer of SGATLayer
+    heads, GATLayer.py:49-78) on one batched graph, eval mode.  Forward in fp32 and
+    fp64, gradients of ``(out * R).sum()`` from the fp64 run, and the edge column
+    ``edata['e']`` the fp64 forward leaves on the graph."""
+    res = {}
+    for dt in (torch.float32, torch.float64):
+        G = shim_batch(docs)
+        n_s = int((G.ndata["unit"] == 1).sum())
+        Xs = torch.from_numpy(weights.feature(seed, "Xs", (n_s, d), 1.0)).to(dt).requires_grad_()
+        s2s = GAT.WSWGAT(d, d, H, 0.1, 512, 0.1, 50, "S2S")
+        weights.seed_module(s2s, seed * 100 + 3).eval().to(dt)
+        out = s2s(G, Xs, Xs)
+        if dt == torch.float32:
+            res["out_s2s"] = out.detach().numpy()
+    R = torch.from_numpy(weights.feature(seed, "R_s2s", tuple(out.shape))).double()
+    (out * R).sum().backward()
+    res.update({"n_s": n_s, "out64_s2s": out.detach().numpy(), "grad_Xs": Xs.grad.numpy(),
+                "e64": G.edata["e"].detach().numpy()})
+    for name, p in s2s.named_parameters():
+        res[f"grad.s2s.{name}"] = p.grad.numpy()
+    return res
+
+
 # ---------------------------------------------------------- train-mode stack --
 def stack_train_case(GAT, docs, seed, drop_seed, off0=0, n_iter=2, p=0.1, keep_rows=160):
     """The reference's own WSWGAT modules chained as HiGraph.py:99-106 (W2S, then
@@ -340,6 +364,21 @@ def main():
         cdocs = sort_by_sentences(synth.make_batch_docs("cfg2", seed=0))
         res = stack_train_case(GAT, cdocs, 46, 1046)
         np.savez_compressed(os.path.join(HERE, "stack_train_cfg2.npz"), **graph_arrays(cdocs), **compact(res), **meta)
+    if want("s2s_small"):
+        # S2S on an HSG batch (w->s phantoms, s->s typed; a sentence with no words)
+        # and an HDSG batch (doc nodes: s->doc typed, w->doc phantoms)
+        rng = np.random.default_rng(16)
+        hs = sort_by_sentences([synth.make_hsg_doc(rng, N=5, W=16, k=4, k_jitter=4, isolated_words=2,
+                                                   vocab_size=500, tf_range=(0.0, 1.0)),
+                                synth.make_hsg_doc(rng, N=3, W=9, k=3, vocab_size=500),
+                                synth.make_hsg_doc(rng, N=6, W=8, k=1, k_jitter=1, vocab_size=500)])
+        rng = np.random.default_rng(17)
+        hd = sort_by_sentences([synth.make_hdsg_example(rng, (3, 2), W=20, k=4, doc_words=6, vocab_size=500),
+                                synth.make_hdsg_example(rng, (2, 1, 2), W=15, k=3, doc_words=5, vocab_size=500)])
+        out = {}
+        for tag, docs, sd in (("hsg", hs, 31), ("hdsg", hd, 32)):
+            out.update({f"{tag}.{k}": v for k, v in compact({**graph_arrays(docs), **s2s_case(GAT, docs, sd)}).items()})
+        np.savez_compressed(os.path.join(HERE, "s2s_small.npz"), **out, **meta)
     if args.only is not None:
         return
 

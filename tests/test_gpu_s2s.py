@@ -1,0 +1,108 @@
+"""S2S on the HIP path (module/GATLayer.sgat_heads: the WSWGAT edge kernel in per-edge
+tau mode over the S2S relation) against the reference's golden vectors
+(tests/golden/s2s_small.npz; /root/reference/module/GAT.py:38-39, 49-51,
+GATLayer.py:49-78, GATStackLayer.py:27-44) and against the UDF oracle
+(oracle/dgl_udf.py) on a cfg2 / cfg4 batch and in train mode with the head masks
+restated by oracle/masks.py.  Tolerance: fp32 path vs fp64 reference 1e-4 absolute on
+outputs / edge logits, 1e-4 relative to the largest entry on gradients."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import weights
+from helpers import build_graph, concat_arrays, load_fixture, synth_fixture
+from oracle import dgl_udf, fused, masks
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda")
+
+
+def _case(tag):
+    z = load_fixture("s2s_small")
+    return {k[len(tag) + 1:]: v for k, v in z.items() if k.startswith(tag + ".")}
+
+
+def _module(seed, d=64, H=8):
+    from hetersumgraph_amd.module.GAT import WSWGAT
+    return weights.seed_module(WSWGAT(d, d, H, 0.1, 512, 0.1, 50, "S2S"), seed * 100 + 3).eval()
+
+
+def _rel_err(a, ref):
+    return np.abs(a - ref).max() / max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("tag,seed", [("hsg", 31), ("hdsg", 32)])
+def test_s2s_matches_reference_golden(tag, seed):
+    from hetersumgraph_amd.module.GATStackLayer import reference_named_grads
+    z = _case(tag)
+    G = build_graph(z).to(DEV)
+    m = _module(seed).to(DEV)
+    Xs = torch.from_numpy(weights.feature(seed, "Xs", (int(z["n_s"]), 64), 1.0)).to(DEV).requires_grad_()
+    out = m(G, Xs, Xs)
+    assert np.abs(out.detach().cpu().numpy() - z["out64_s2s"]).max() <= 1e-4
+    e = G.edata["e"].cpu().numpy()
+    assert np.abs(e - z["e64"]).max() <= 1e-4
+    R = torch.from_numpy(weights.feature(seed, "R_s2s", tuple(out.shape))).to(DEV)
+    (out * R).sum().backward()
+    assert _rel_err(Xs.grad.cpu().numpy(), z["grad_Xs"]) <= 1e-4
+    for name, g in reference_named_grads(m):
+        assert _rel_err(g.cpu().numpy(), z["grad.s2s." + name]) <= 1e-4, name
+
+
+def test_s2s_requires_equal_inputs():
+    z = _case("hsg")
+    G = build_graph(z).to(DEV)
+    m = _module(31).to(DEV)
+    Xs = torch.randn(int(z["n_s"]), 64, device=DEV)
+    with pytest.raises(AssertionError):
+        m(G, Xs, Xs + 1)
+    torch.testing.assert_close(m(G, Xs, Xs.clone()), m(G, Xs, Xs), rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("config,n_docs", [("cfg2", 8), ("cfg4", 6)])
+def test_s2s_full_docs_vs_udf_oracle(config, n_docs):
+    """Whole cfg2 documents (35 sentences: 35 s->s in-edges + ~20 word phantoms per
+    sentence) and cfg4 examples (doc nodes: ~250 word phantoms, 15 s->doc typed)."""
+    from hetersumgraph_amd import synth
+    z = synth_fixture(synth.make_batch_docs(config, seed=0)[:n_docs])
+    G = build_graph(z).to(DEV)
+    m = _module(40)
+    Xs = torch.from_numpy(weights.feature(40, "Xs", (int(z["n_s"]), 64), 1.0))
+    Xd = Xs.to(DEV).requires_grad_()
+    out = m.to(DEV)(G, Xd, Xd)
+    out.sum().backward()
+    a = concat_arrays(z)
+    ug = dgl_udf.UdfGraph(a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    p = fused.as_params(m, dtype=torch.float64)
+    X64 = Xs.double().requires_grad_()
+    ref = dgl_udf.wswgat(ug, "S2S", X64, X64, p, None)
+    ref.sum().backward()
+    assert (out.detach().cpu().double() - ref.detach()).abs().max().item() <= 1e-4
+    assert _rel_err(Xd.grad.cpu().double().numpy(), X64.grad.numpy()) <= 1e-4
+    assert (G.edata["e"].cpu().double() - ug.e).abs().max().item() <= 1e-4
+
+
+def test_s2s_train_mode_head_masks():
+    """Train-mode heads: each head projects its own dropout of s (GATStackLayer.py:38);
+    the masks are the ones oracle/masks.py restates for (seed, offset 1)."""
+    from hetersumgraph_amd import rng, synth
+    z = synth_fixture(synth.make_batch_docs("cfg2", seed=1)[:4])
+    G = build_graph(z).to(DEV)
+    m = _module(41).to(DEV).train()
+    n_s, H, D, p = int(z["n_s"]), 8, 8, 0.1
+    Xs = torch.from_numpy(weights.feature(41, "Xs", (n_s, 64), 1.0))
+    rng.manual_seed(777, DEV)
+    h = m.layer(G, Xs.to(DEV), origin=Xs.to(DEV))
+    keep = masks.hproj_keep(777, 1, n_s, 64, H, p)
+    scale = masks.hproj_scale(p)
+    a = concat_arrays(z)
+    ug = dgl_udf.UdfGraph(a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    q = fused.as_params(m, dtype=torch.float64, requires_grad=False)
+    X64 = Xs.double()
+    heads = [dgl_udf._sgat_head(ug, X64 * torch.from_numpy(keep[k]).double() * scale,
+                                q[f"layer.heads.{k}.fc.weight"], q[f"layer.heads.{k}.attn_fc.weight"])
+             for k in range(H)]
+    ref = F.elu(torch.cat(heads, 1)) + X64
+    assert (h.detach().cpu().double() - ref).abs().max().item() <= 1e-4
