@@ -1532,6 +1532,228 @@ int launch7(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------
+// k_gemm12 (round 6): k_gemm7's products with the weight tile RESIDENT in LDS and no
+// barrier in the K loop.  The k_gemm7 diagnostics (tools/gemm5_sweep.py plans 35-38,
+// profiles/r06/g7diag/) put its floor in the per-K-step barrier + one-stage DMA
+// prefetch: with B loads alone (no A, no MFMA) it still takes 31 of its 47 us.  Here a
+// block (4 waves, one per SIMD, one block per CU) keeps the whole 64-column B tile of
+// its column range (3 limb planes x Kp, K <= 320: 120 KB) in LDS, loaded ONCE; the A
+// rows a wave multiplies are private to it, so they go global -> registers, two K steps
+// ahead, with no LDS and no barrier.  A wave's task is a 32-row band x 64 columns over
+// the full K (k_gemm7's wave tile, same fragments, same product order: C is bitwise
+// k_gemm7's).  XCD x (blockIdx % 8) owns the contiguous x-th eighth of the row bands
+// and all column tiles, so A is fetched from HBM once per XCD L2 and reused by the
+// column tiles there.  Column partials (colpart) are per 32-row band.
+// MEASURED SLOWER (dev opt-in HSG_GEMM12=1; profiles/r06/g12/): C bitwise k_gemm7's,
+// but 59-71 us against k_gemm7's 47 us on ffn1 / dH at cfg2 whatever the A prefetch
+// depth (1-6 steps), the iglp / sched_group_barrier interleave, or an explicit
+// software pipeline of the split and the B reads: one wave per SIMD has no partner to
+// fill its LDS-read, split and epilogue latencies, and the LDS a resident B tile takes
+// leaves no room for a second block.
+// ---------------------------------------------------------------------------------
+#ifdef HSG_DEV
+constexpr int kG12BN = 64;
+constexpr int kG12MaxKp = 320;
+
+__host__ __device__ constexpr size_t g12_lds_bytes(int nt) {
+    return (size_t)nt * 3 * kG12BN * 32 * 2 + (size_t)4 * 32 * (kG12BN + 4) * 4;
+}
+
+template <int PD, bool IGLP>
+__global__ __launch_bounds__(256, 1) void k_gemm12(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp,
+                                                   int tiles_n, int q) {
+    constexpr int BN = kG12BN, TN = BN / 16, BPC = BN / 16, B_BF = BN * 32;
+    extern __shared__ __attribute__((aligned(16))) float g12_lds[];
+    const int nt = Kp / 32;
+    __bf16 *sB = reinterpret_cast<__bf16 *>(g12_lds);
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float *wl = g12_lds + nt * 3 * B_BF / 2 + wid * 32 * (BN + 4);
+    const int xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int ct = local % tiles_n, sub = local / tiles_n;
+    const int n0 = ct * BN;
+    const int nbands = (p.M + 31) / 32;
+    const int bb = xcd * nbands / 8, be = (xcd + 1) * nbands / 8;
+    const int S = 4 * q, s = 4 * sub + wid;
+
+    // the block's B tile: nt K tiles x 3 limbs x BPC 1-KB pieces, k_gemm7's image per tile
+    for (int pc = wid; pc < nt * 3 * BPC; pc += 4) {
+        const int kt = pc / (3 * BPC), rem = pc % (3 * BPC);
+        const int limb = rem / BPC, prow = (rem % BPC) * 16;
+        const int r = prow + (lane >> 2);
+        const int c = (lane & 3) ^ bswz16(r);
+        const __bf16 *src = planes + ((size_t)(limb * Np + n0 + r) * Kp + kt * 32 + 8 * c);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(sB + (kt * 3 + limb) * B_BF +
+                                                                                    prow * 32),
+                                         16, 0, 0);
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+
+    const int ntask = s < be - bb ? (be - bb - s + S - 1) / S : 0;
+    const int nsteps = ntask * nt;
+    const int li = lane & 15, kb = lane >> 4;
+    f32x4v7 acc[2][TN];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
+    EpiRows<BN> ep;
+
+    // A fragments of flattened step st (task st / nt, K tile st % nt): rows 16 i + li,
+    // k = 8 kb .. 8 kb + 7 of the tile as two float4 (K % 4 == 0: whole quads)
+    auto load_step = [&](int st, f32x4 (&R)[4]) {
+        if (st >= nsteps) return;
+        const int band = bb + s + (st / nt) * S, k = (st % nt) * 32 + 8 * kb;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int m = min(band * 32 + 16 * i + li, p.M - 1);
+            const float *a = p.A + (size_t)m * p.lda + k;
+            R[2 * i] = k < p.K ? *reinterpret_cast<const f32x4 *>(a) : f32x4{0.f, 0.f, 0.f, 0.f};
+            R[2 * i + 1] = k + 4 < p.K ? *reinterpret_cast<const f32x4 *>(a + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+    // software pipeline (one wave per SIMD has no partner to hide its latencies): step
+    // st's MFMAs run on fragments made during step st - 1 -- the split limbs of its A
+    // rows and its B fragments read from LDS -- while that step's VALU split and
+    // ds_reads for st + 1 are interleaved between them (sched_group_barrier)
+    auto split_a = [&](const f32x4 (&R)[4], bf16x8 (&a)[2][3]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) split_rne8(R[2 * i], R[2 * i + 1], a[i][0], a[i][1], a[i][2]);
+    };
+    auto read_b = [&](int kt, bf16x8 (&b)[TN][3]) {
+        const __bf16 *sb = sB + kt * 3 * B_BF;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int r = 16 * j + li;
+            const int off = r * 32 + 8 * (kb ^ bswz16(r));
+#pragma unroll
+            for (int l = 0; l < 3; ++l) b[j][l] = *reinterpret_cast<const bf16x8 *>(&sb[l * B_BF + off]);
+        }
+    };
+    auto mfmas = [&](const bf16x8 (&a)[2][3], const bf16x8 (&b)[TN][3]) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {   // k_gemm7's order: small products first
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+            }
+    };
+    // two register sets, even / odd steps (nt is even: a band starts on the even set)
+    f32x4 R[2][4];
+    bf16x8 A0[2][3], A1[2][3], B0[TN][3], B1[TN][3];
+    load_step(0, R[0]);
+    load_step(1, R[1]);
+    if (nsteps > 0) {
+        split_a(R[0], A0);
+        read_b(0, B0);
+    }
+    auto step = [&](int st, int kt, f32x4 (&Rn)[4], const bf16x8 (&Ac)[2][3], const bf16x8 (&Bc)[TN][3],
+                    bf16x8 (&An)[2][3], bf16x8 (&Bn)[TN][3], f32x4 (&Rl)[4]) {
+        // Rn holds step st + 1's A rows; Rl (= step st's ring slot, consumed) gets st + 2's
+        if (st + 1 < nsteps) {
+            read_b(kt + 1 == nt ? 0 : kt + 1, Bn);
+            split_a(Rn, An);
+        }
+        load_step(st + 2, Rl);
+        mfmas(Ac, Bc);
+        if constexpr (IGLP) {
+#pragma unroll
+            for (int g = 0; g < 12; ++g) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // 4 MFMA
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 ds_read
+                __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);   // 6 VALU
+            }
+        }
+    };
+    for (int task = 0; task < ntask; ++task) {
+        const int row0 = (bb + s + task * S) * 32;
+        for (int kt = 0; kt < nt; kt += 2) {
+            const int st = task * nt + kt;
+            if (kt + 2 >= nt) ep.load(p, row0, n0, lane);       // overlaps the last steps' MFMAs
+            step(st, kt, R[1], A0, B0, A1, B1, R[0]);
+            step(st + 1, kt + 1, R[0], A1, B1, A0, B0, R[1]);
+        }
+        // the band's epilogue through the wave's private LDS rows (k_gemm7's EpiRows)
+        const int c = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) wl[(16 * i + rq + e) * (BN + 4) + 16 * j + c] = acc[i][j][e];
+                acc[i][j] = f32x4v7{0.f, 0.f, 0.f, 0.f};
+            }
+        f32x4 cs;
+        ep.finish(wl, row0, n0, lane, p, cs);
+        if (p.colpart) {
+            // 32-row partial of this band: the lane sums over its rows (rs = lane / 16)
+            // added in rs order, then one float4 per column quad
+            constexpr int QS = EpiMap<BN>::QS;
+            static_assert(QS == 16, "BN = 64: 16 quads per row step");
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float v1 = __shfl(cs[e], (lane & 15) + 16), v2 = __shfl(cs[e], (lane & 15) + 32),
+                            v3 = __shfl(cs[e], (lane & 15) + 48);
+                cs[e] = ((cs[e] + v1) + v2) + v3;
+            }
+            const int n = n0 + 4 * c;
+            if (lane < 16 && n < p.N) *reinterpret_cast<f32x4 *>(p.colpart + (size_t)(row0 / 32) * p.N + n) = cs;
+        }
+    }
+}
+
+// k_gemm12's plan: fp32-accurate products, wide FFN shapes (N > 320) with the whole
+// K in one resident B tile, and rows enough for every wave of the grid
+bool plan12(int M, int N, int K) {
+    int Np, Kp;
+    hsg_wsplit_dims(N, K, &Np, &Kp);
+    const char *f = HSG_DEV_ENV("HSG_GEMM12");               // dev opt-in: 1 = k_gemm12
+    if (!f || atoi(f) != 1) return false;
+    return N > 320 && Kp <= kG12MaxKp && (Kp / 32) % 5 == 0 && (K & 3) == 0 && M >= 8 * 32 * 32 &&
+           (N + kG12BN - 1) / kG12BN <= 32;
+}
+
+int launch12(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
+    const int tiles_n = (p.N + kG12BN - 1) / kG12BN;
+    if (tiles_n * kG12BN > Np || !epi_rows_ok(p) || p.epi == HSG_EPI_ADD_ELUG) return HSG_EINVAL;
+    if ((p.lda & 3) || (((uintptr_t)p.A) & 15)) return HSG_EINVAL;
+    const int q = max(1, 32 / tiles_n);
+    int pd = 4, ig = 0;
+#ifdef HSG_DEV
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM12_PD")) pd = atoi(f);
+    if (const char *f = HSG_DEV_ENV("HSG_GEMM12_IGLP")) ig = atoi(f);
+#endif
+    const auto go = [&](auto kern) {
+        static bool attr = false;
+        if (!attr) {
+            if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)g12_lds_bytes(kG12MaxKp / 32)) != hipSuccess)
+                return (int)HSG_EINVAL;
+            attr = true;
+        }
+        hipLaunchKernelGGL(kern, dim3(8 * tiles_n * q), dim3(256), g12_lds_bytes(Kp / 32), st, p, planes, Np, Kp,
+                           tiles_n, q);
+        hipError_t e = hipGetLastError();
+        return e == hipSuccess ? 0 : (int)e;
+    };
+#ifdef HSG_DEV
+    if (pd == 1) return ig ? go(k_gemm12<1, true>) : go(k_gemm12<1, false>);
+    if (ig) return go(k_gemm12<4, true>);
+#endif
+    (void)pd;
+    (void)ig;
+    return go(k_gemm12<4, false>);
+}
+#endif  // HSG_DEV
+
+// ---------------------------------------------------------------------------------
 // k_gemm11 (round 4): the pre-split-weight FFN GEMM on ONE round of big tiles.
 // k_gemm7's 128 x 64 blocks (two per CU) move (128 x 4 + 64 x 6) B of operand per K
 // for 8,192 outputs; at cfg2 its loads alone took 36 of its ~48 us per S2W FFN GEMM
@@ -2636,6 +2858,15 @@ int hsg_gemm_f32_psw(int M, int N, int K, const float *A, int lda, const void *p
             return rc;
     }
 #endif
+    // dev opt-in: the resident-B kernel for N > 320 with K <= 320 (measured slower).  Its
+    // column partials are per 32-row band (hsg_gemm_psw_row_tiles), so a call it refuses
+    // with colsum_part is refused, not handed to k_gemm7's 64-row partials
+#ifdef HSG_DEV
+    if (plan12(M, N, K)) {
+        const int rc = launch12(p, pl, Np, Kp, st);
+        if (rc != HSG_EINVAL || colsum_part) return rc;
+    }
+#endif
     // N <= 320 (ffn2 y = H W2^T at N = 300): 112-wide tiles, 3 per row band instead of 5
     // of 64 -- 450 tiles at cfg2, ONE round of the 512 resident blocks instead of 1.46 --
     // and each wave's A split feeds 7 instead of 4 column subtiles: 44.1 -> 39.1 us back
@@ -2806,6 +3037,7 @@ int hsg_gemm_psw_row_tiles(int M, int N, int K, int bf16) {
     const int pl = gemm11_on() && atoi(HSG_DEV_ENV("HSG_GEMM11")) == 1 ? plan11(M, N, device_cus()) : 0;
     if (pl == 1) return (M + 159) / 160 * 2;               // k_gemm11<160, 256, 2, 4>: 80-row bands
     if (pl == 2) return (M + 191) / 192 * 4;               // k_gemm11<192, 160, 4, 2>: 48-row bands
+    if (!bf16 && plan12(M, N, K)) return (M + 31) / 32;    // k_gemm12: 32-row bands
 #endif
     return (M + 63) / 64;
 }

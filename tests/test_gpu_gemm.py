@@ -238,6 +238,47 @@ def test_psw_epilogues_and_colsums():
     assert (acc.double() - accr).abs().max().item() < 2e-3
 
 
+@pytest.mark.parametrize("M", [19200, 28800, 10001])
+def test_resident_b_gemm(M, monkeypatch):
+    """Dev-only k_gemm12 (HSG_GEMM12=1; the wide FFN GEMMs with K <= 320, B resident in
+    LDS, A straight to registers; measured slower than k_gemm7): C within the split's
+    fp32 class of fp64 for the bias + ReLU and the ReLU-mask epilogues, 32-row column
+    partials equal to the band sums, and C bitwise equal to k_gemm7 (same fragments,
+    same product order) with the same column totals."""
+    from hetersumgraph_amd.dense import gemm_psw, psw_row_tiles, split_weights
+    from helpers import dev_lib
+    if not dev_lib():
+        pytest.skip("k_gemm12 is in the dev library only (HSG_LIB_PATH=.../libhsg_dev.so)")
+    monkeypatch.setenv("HSG_GEMM12", "1")
+    torch.manual_seed(M)
+    N, K = 512, 300
+    X = torch.randn(M, K, device="cuda")
+    W1 = torch.randn(N, K, device="cuda") * 0.05
+    W2 = torch.randn(K, N, device="cuda") * 0.05
+    b = torch.randn(N, device="cuda")
+    s1, s2t = split_weights((W1, False), (W2, True))
+    rt = psw_row_tiles(M, N, K)
+    assert rt == (M + 31) // 32
+    H = gemm_psw(X, s1, bias=b, relu=True)
+    Hr = torch.relu(X.double() @ W1.double().t() + b.double())
+    unit = X.double().abs() @ W1.double().abs().t() + b.double().abs()
+    assert ((H.double() - Hr).abs() / unit).max().item() < 2e-6
+    G = torch.randn(M, K, device="cuda")
+    part = torch.full((rt, N), float("nan"), device="cuda")
+    dH = gemm_psw(G, s2t, relu_mask=H, colsum_part=part)
+    dHr = (G.double() @ W2.double()) * (H.double() > 0)
+    unit = (G.double().abs() @ W2.double().abs())
+    assert ((dH.double() - dHr).abs() / unit).max().item() < 2e-6
+    bands = torch.nn.functional.pad(dH.double(), (0, 0, 0, rt * 32 - M)).view(rt, 32, N).sum(1)
+    assert torch.allclose(part.double(), bands, rtol=1e-6, atol=1e-4)
+    monkeypatch.setenv("HSG_GEMM12", "0")
+    assert psw_row_tiles(M, N, K) == (M + 63) // 64
+    part7 = torch.zeros((M + 63) // 64, N, device="cuda")
+    assert torch.equal(gemm_psw(X, s1, bias=b, relu=True), H)
+    assert torch.equal(gemm_psw(G, s2t, relu_mask=H, colsum_part=part7), dH)
+    assert torch.allclose(part7.sum(0), part.sum(0), rtol=1e-5, atol=1e-3)
+
+
 def test_psw_rejects_bad_operands():
     from hetersumgraph_amd._lib import HSG_EINVAL, load
     lib = load()
