@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NPL <= 2 ? 
 // (>= ceil8(d)), the pad columns d .. ceil8(d) - 1 zero (the bf16-A contract of
 // hsg_gemm_bf16_psw_io); db2 still sums the fp32 values.
 // XBF (round 6): x as bf16 rows of pitch ldx (the forward's k_ln_fwd4p<..., XBF>).
-template <int NV, bool DYBF = false, bool YBF = false, bool XBF = false>
+template <int NV, bool DYBF = false, bool YBF = false, bool XBF = false, int PF = 1>
 __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__restrict__ dout,
                                                   const float *__restrict__ y, const float *__restrict__ x,
                                                   const float *__restrict__ gamma, const float *__restrict__ mean,
@@ -372,81 +372,90 @@ __global__ __launch_bounds__(256) void k_ln_bwd4p(int n, int d, const float *__r
     }
     const int nw = gridDim.x * 4;
     int r = blockIdx.x * 4 + wid;
-    f32x4r yv[NV], xv[NV], gv[NV];
-    bf16x4r yb[YBF ? NV : 1];                                        // YBF: bf16 y rows, raw until used
-    bf16x4r xb[XBF ? NV : 1];                                        // XBF: bf16 x rows, likewise
-    float mu = 0.f, rs = 0.f;
-    auto load = [&](int rr) {
-        mu = mean[rr];
-        rs = rstd[rr];
+    // PF row buffers (dev PF = 2: two rows of the wave's walk in flight; the buffer index
+    // is a compile-time constant after unrolling, so the buffers stay in registers)
+    f32x4r yv[PF][NV], xv[PF][NV], gv[PF][NV];
+    bf16x4r yb[PF][YBF ? NV : 1];                                    // YBF: bf16 y rows, raw until used
+    bf16x4r xb[PF][XBF ? NV : 1];                                    // XBF: bf16 x rows, likewise
+    float mu[PF], rs[PF];
+    auto load = [&](int rr, int bf) {
+        mu[bf] = mean[rr];
+        rs[bf] = rstd[rr];
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
             const size_t o = (size_t)rr * d + cq[i];
-            if constexpr (YBF) yb[i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + o);
-            else yv[i] = *reinterpret_cast<const f32x4r *>(y + o);
+            if constexpr (YBF) yb[bf][i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(y) + o);
+            else yv[bf][i] = *reinterpret_cast<const f32x4r *>(y + o);
             if constexpr (XBF)
-                xb[i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(x) + (size_t)rr * ldx + cq[i]);
+                xb[bf][i] = *reinterpret_cast<const bf16x4r *>(reinterpret_cast<const __bf16 *>(x) + (size_t)rr * ldx + cq[i]);
             else
-                xv[i] = *reinterpret_cast<const f32x4r *>(x + o);
-            gv[i] = *reinterpret_cast<const f32x4r *>(dout + o);
+                xv[bf][i] = *reinterpret_cast<const f32x4r *>(x + o);
+            gv[bf][i] = *reinterpret_cast<const f32x4r *>(dout + o);
         }
     };
-    if (r < n) load(r);
-    for (; r < n; r += nw) {
-        const size_t rb = (size_t)r * d;
-        f32x4r xh[NV], g[NV];
-        uint32_t keep = 0xFFFFFFFFu;                                 // bit 4 i + e
-        float sg = 0.f, sgx = 0.f;
-        const float rsr = rs;
 #pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            xh[i] = g[i] = f32x4r{0.f, 0.f, 0.f, 0.f};
-            if (cok[i]) {
+    for (int bf = 0; bf < PF; ++bf)
+        if (r + bf * nw < n) load(r + bf * nw, bf);
+    for (; r < n; r += PF * nw) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    float v;
-                    if constexpr (YBF) v = (float)yb[i][e];
-                    else v = yv[i][e];
-                    if (p_drop > 0.f) {
-                        const bool k = hsg_keep32(dkey, (uint32_t)(rb + cq[i] + e), thr);
-                        if (!k) keep &= ~(1u << (4 * i + e));
-                        v = k ? v * scale : 0.f;
+        for (int bf = 0; bf < PF; ++bf) {
+            const int rr = r + bf * nw;
+            if (rr >= n) break;                                      // wave-uniform
+            const size_t rb = (size_t)rr * d;
+            f32x4r xh[NV], g[NV];
+            uint32_t keep = 0xFFFFFFFFu;                             // bit 4 i + e
+            float sg = 0.f, sgx = 0.f;
+            const float rsr = rs[bf], mur = mu[bf];
+#pragma unroll
+            for (int i = 0; i < NV; ++i) {
+                xh[i] = g[i] = f32x4r{0.f, 0.f, 0.f, 0.f};
+                if (cok[i]) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float v;
+                        if constexpr (YBF) v = (float)yb[bf][i][e];
+                        else v = yv[bf][i][e];
+                        if (p_drop > 0.f) {
+                            const bool k = hsg_keep32(dkey, (uint32_t)(rb + cq[i] + e), thr);
+                            if (!k) keep &= ~(1u << (4 * i + e));
+                            v = k ? v * scale : 0.f;
+                        }
+                        float xe;
+                        if constexpr (XBF) xe = (float)xb[bf][i][e];
+                        else xe = xv[bf][i][e];
+                        xh[i][e] = (v + xe - mur) * rsr;
+                        const float go = gv[bf][i][e];
+                        g[i][e] = go * gam[i][e];
+                        sg += g[i][e];
+                        sgx = fmaf(g[i][e], xh[i][e], sgx);
+                        dg[i][e] = fmaf(go, xh[i][e], dg[i][e]);
+                        db[i][e] += go;
                     }
-                    float xe;
-                    if constexpr (XBF) xe = (float)xb[i][e];
-                    else xe = xv[i][e];
-                    xh[i][e] = (v + xe - mu) * rs;
-                    const float go = gv[i][e];
-                    g[i][e] = go * gam[i][e];
-                    sg += g[i][e];
-                    sgx = fmaf(g[i][e], xh[i][e], sgx);
-                    dg[i][e] = fmaf(go, xh[i][e], dg[i][e]);
-                    db[i][e] += go;
                 }
             }
-        }
-        if (r + nw < n) load(r + nw);
-        const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
+            if (rr + PF * nw < n) load(rr + PF * nw, bf);
+            const float mg = wsum(sg) / d, mgx = wsum(sgx) / d;
 #pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            if (cok[i]) {
-                f32x4r ds, dyv;
+            for (int i = 0; i < NV; ++i) {
+                if (cok[i]) {
+                    f32x4r ds, dyv;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    ds[e] = rsr * (g[i][e] - mg - xh[i][e] * mgx);
-                    dyv[e] = (keep >> (4 * i + e)) & 1u ? ds[e] * scale : 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        ds[e] = rsr * (g[i][e] - mg - xh[i][e] * mgx);
+                        dyv[e] = (keep >> (4 * i + e)) & 1u ? ds[e] * scale : 0.f;
+                    }
+                    *reinterpret_cast<f32x4r *>(dx + rb + cq[i]) = ds;
+                    if constexpr (DYBF) {
+                        *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)rr * ld_dy + cq[i]) =
+                            bf16x4r{(__bf16)dyv[0], (__bf16)dyv[1], (__bf16)dyv[2], (__bf16)dyv[3]};
+                    } else {
+                        *reinterpret_cast<f32x4r *>(dy + rb + cq[i]) = dyv;
+                    }
+                    dyb[i] += dyv;
+                } else if (DYBF && 4 * lane + 256 * i == d && d + 4 <= ld_dy) {   // the zero pad quad
+                    *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)rr * ld_dy + d) =
+                        bf16x4r{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
                 }
-                *reinterpret_cast<f32x4r *>(dx + rb + cq[i]) = ds;
-                if constexpr (DYBF) {
-                    *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)r * ld_dy + cq[i]) =
-                        bf16x4r{(__bf16)dyv[0], (__bf16)dyv[1], (__bf16)dyv[2], (__bf16)dyv[3]};
-                } else {
-                    *reinterpret_cast<f32x4r *>(dy + rb + cq[i]) = dyv;
-                }
-                dyb[i] += dyv;
-            } else if (DYBF && 4 * lane + 256 * i == d && d + 4 <= ld_dy) {   // the zero pad quad
-                *reinterpret_cast<bf16x4r *>(reinterpret_cast<__bf16 *>(dy) + (size_t)r * ld_dy + d) =
-                    bf16x4r{(__bf16)0.f, (__bf16)0.f, (__bf16)0.f, (__bf16)0.f};
             }
         }
     }
@@ -604,6 +613,13 @@ int hsg_ln_bwd(int n, int d, const float *dout, const float *y, const float *x, 
     if (const char *e = HSG_DEV_ENV("HSG_LN_BWDP")) vec = atoi(e) != 0;            // dev A/B
     const auto al = [](const void *q) { return ((uintptr_t)q & 15) == 0; };
     if (vec && d % 4 == 0 && (d + 255) / 256 == 2 && al(dout) && al(y) && al(x) && al(gamma) && al(dy) && al(dx)) {
+#ifdef HSG_DEV
+        if (const char *e = HSG_DEV_ENV("HSG_LN_BWD_PF"); e && atoi(e) == 2) {   // dev A/B: two rows in flight
+            hipLaunchKernelGGL((k_ln_bwd4p<2, false, false, false, 2>), grid, block, 0, st, n, d, dout, y, x, gamma,
+                               mean, rstd, p_drop, seed, offset, dy, dx, part);
+            return status();
+        }
+#endif
         hipLaunchKernelGGL((k_ln_bwd4p<2>), grid, block, 0, st, n, d, dout, y, x, gamma, mean, rstd, p_drop, seed,
                            offset, dy, dx, part);
         return status();
