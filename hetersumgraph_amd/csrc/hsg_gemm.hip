@@ -1559,7 +1559,7 @@ __host__ __device__ constexpr size_t g12_lds_bytes(int nt) {
     return (size_t)nt * 3 * kG12BN * 32 * 2 + (size_t)4 * 32 * (kG12BN + 4) * 4;
 }
 
-template <int PD, bool IGLP>
+template <bool IGLP>
 __global__ __launch_bounds__(256, 1) void k_gemm12(GemmArgs p, const __bf16 *__restrict__ planes, int Np, int Kp,
                                                    int tiles_n, int q) {
     constexpr int BN = kG12BN, TN = BN / 16, BPC = BN / 16, B_BF = BN * 32;
@@ -1725,11 +1725,8 @@ int launch12(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
     if (tiles_n * kG12BN > Np || !epi_rows_ok(p) || p.epi == HSG_EPI_ADD_ELUG) return HSG_EINVAL;
     if ((p.lda & 3) || (((uintptr_t)p.A) & 15)) return HSG_EINVAL;
     const int q = max(1, 32 / tiles_n);
-    int pd = 4, ig = 0;
-#ifdef HSG_DEV
-    if (const char *f = HSG_DEV_ENV("HSG_GEMM12_PD")) pd = atoi(f);
+    int ig = 0;                                               // dev: sched_group_barrier interleave
     if (const char *f = HSG_DEV_ENV("HSG_GEMM12_IGLP")) ig = atoi(f);
-#endif
     const auto go = [&](auto kern) {
         static bool attr = false;
         if (!attr) {
@@ -1743,13 +1740,7 @@ int launch12(GemmArgs p, const __bf16 *planes, int Np, int Kp, hipStream_t st) {
         hipError_t e = hipGetLastError();
         return e == hipSuccess ? 0 : (int)e;
     };
-#ifdef HSG_DEV
-    if (pd == 1) return ig ? go(k_gemm12<1, true>) : go(k_gemm12<1, false>);
-    if (ig) return go(k_gemm12<4, true>);
-#endif
-    (void)pd;
-    (void)ig;
-    return go(k_gemm12<4, false>);
+    return ig ? go(k_gemm12<true>) : go(k_gemm12<false>);
 }
 #endif  // HSG_DEV
 

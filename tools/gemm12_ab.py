@@ -63,7 +63,8 @@ for name, run in (("ffn1", lambda out, part: gemm_psw(x, s1, bias=b1, relu=True,
     print(f"{name}: k_gemm12 == k_gemm7 bitwise {eq}; err vs fp64 {err:.2e}; colsum max|diff| {cs:.2e}", flush=True)
     out = torch.empty(n, dh, device="cuda")
     part = torch.empty(max(psw_row_tiles(n, dh, d), (n + 63) // 64), dh, device="cuda")
-    # variants: "pd,iglp" of k_gemm12 (HSG_GEMM12_PD / HSG_GEMM12_IGLP), "g7" = k_gemm7
+    # variants: "pd,iglp" of k_gemm12 (HSG_GEMM12_IGLP; pd named the A prefetch depth of the
+    # earlier ring versions, profiles/r06/g12/; the pipelined kernel has none), "g7" = k_gemm7
     variants = os.environ.get("VARIANTS", "4,0;g7").split(";")
     t = {v: [] for v in variants}
     for _ in range(5):
