@@ -61,10 +61,11 @@ def test_s2s_requires_equal_inputs():
     torch.testing.assert_close(m(G, Xs, Xs.clone()), m(G, Xs, Xs), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("config,n_docs", [("cfg2", 8), ("cfg4", 6)])
+@pytest.mark.parametrize("config,n_docs", [("cfg2", 8), ("cfg4", 6), ("cfg5", 4)])
 def test_s2s_full_docs_vs_udf_oracle(config, n_docs):
     """Whole cfg2 documents (35 sentences: 35 s->s in-edges + ~20 word phantoms per
-    sentence) and cfg4 examples (doc nodes: ~250 word phantoms, 15 s->doc typed)."""
+    sentence), cfg4 examples (doc nodes: ~250 word phantoms, 15 s->doc typed) and cfg5
+    documents (80 sentences: 80 s->s in-edges per sentence)."""
     from hetersumgraph_amd import synth
     z = synth_fixture(synth.make_batch_docs(config, seed=0)[:n_docs])
     G = build_graph(z).to(DEV)
@@ -106,3 +107,40 @@ def test_s2s_train_mode_head_masks():
              for k in range(H)]
     ref = F.elu(torch.cat(heads, 1)) + X64
     assert (h.detach().cpu().double() - ref).abs().max().item() <= 1e-4
+
+
+def test_edge_column_after_w2s_s2s_w2s():
+    """g.edata['e'] through W2S, then S2S, then W2S again: S2S rewrites every dtype-0
+    edge (w->s included), the second W2S rewrites its own typed rows, and the s->w rows
+    keep S2S's logits -- what the reference's apply_edges writes leave (GATLayer.py:74,
+    112), checked against the UDF oracle's column after each application."""
+    from hetersumgraph_amd import synth
+    from hetersumgraph_amd.HiGraph import register_tfidf_table
+    from helpers import gat_inputs, seeded_gat_params
+    z = synth_fixture(synth.make_batch_docs("cfg2", seed=3)[:3])
+    G = build_graph(z).to(DEV)
+    Xw, Xs, T = gat_inputs(5, int(z["n_w"]), int(z["n_s"]))
+    register_tfidf_table(G, T.to(DEV))
+    w2s, _ = seeded_gat_params(501, 502)
+    w2s = w2s.to(DEV)
+    s2s = _module(50, d=64, H=8).to(DEV)
+    a = concat_arrays(z)
+    ug = dgl_udf.UdfGraph(a["src"], a["dst"], a["unit"], a["tffrac"], a["edtype"])
+    te = dgl_udf.tfidf_embed(ug, T)
+    p1 = fused.as_params(w2s, dtype=torch.float32)
+    p3 = fused.as_params(s2s, dtype=torch.float32)
+    with torch.no_grad():
+        s1 = w2s(G, Xw.to(DEV), Xs.to(DEV))
+        o1 = dgl_udf.wswgat(ug, "W2S", Xw, Xs, p1, te)
+        assert (G.edata["e"].cpu() - ug.e).abs().max().item() <= 1e-4
+        s2 = s2s(G, s1, s1)
+        o2 = dgl_udf.wswgat(ug, "S2S", o1, o1, p3, None)
+        assert (s2.cpu() - o2).abs().max().item() <= 1e-4
+        assert (G.edata["e"].cpu() - ug.e).abs().max().item() <= 1e-4
+        w2s(G, Xw.to(DEV), s2)
+        dgl_udf.wswgat(ug, "W2S", Xw, o2, p1, te)
+        e = G.edata["e"].cpu()
+    assert (e - ug.e).abs().max().item() <= 1e-4
+    # the s->w dtype-0 rows still hold S2S's logits (no S2W ran), and they are not zero
+    sw = torch.from_numpy((ug.unit[a["src"]] == 1) & (ug.unit[a["dst"]] == 0) & (a["edtype"] == 0))
+    assert e[sw].abs().max() > 0
